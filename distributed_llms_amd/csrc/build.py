@@ -1,0 +1,127 @@
+"""In-tree build of the native extensions (no torch JIT cache, no hipify).
+
+    python -m distributed_llms_amd.csrc.build [--force] [-j N]
+
+* ``_C_kernels``: every ``csrc/kernels/*.hip`` compiled by ``hipcc --offload-arch=gfx950``
+  plus the pybind11 binding TU, linked into ``distributed_llms_amd/_C_kernels<EXT_SUFFIX>``.
+* ``_C_runtime``: host-only C++17 (``csrc/runtime/*.cpp``), paged-KV block manager and
+  wire-frame codec, linked into ``distributed_llms_amd/_C_runtime<EXT_SUFFIX>``.
+
+Objects go to ``build/`` (git-ignored); the ``.so`` files land in the package
+directory so they travel to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+BUILD = os.path.join(ROOT, "build", "native")
+ARCH = os.environ.get("DLLM_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
+
+
+def _py_includes():
+    import pybind11
+    return [pybind11.get_include(), sysconfig.get_paths()["include"]]
+
+
+def _ext_path(name: str) -> str:
+    return os.path.join(PKG, name + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def build_kernels(force=False, jobs=8, verbose=False) -> str:
+    src_dir = os.path.join(HERE, "kernels")
+    out_dir = os.path.join(BUILD, "kernels")
+    os.makedirs(out_dir, exist_ok=True)
+    headers = glob.glob(os.path.join(src_dir, "*.h"))
+    hips = sorted(glob.glob(os.path.join(src_dir, "*.hip")))
+    incs = [f"-I{p}" for p in _py_includes()] + [f"-I{src_dir}"]
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+              "-mcode-object-version=5"]
+    jobs_list = []
+    objs = []
+    for src in hips:
+        obj = os.path.join(out_dir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src] + headers):
+            jobs_list.append([HIPCC, "-c", src, "-o", obj] + common + incs)
+    bind = os.path.join(src_dir, "bindings.cpp")
+    bobj = os.path.join(out_dir, "bindings.o")
+    objs.append(bobj)
+    if force or _stale(bobj, [bind] + headers):
+        jobs_list.append([CXX, "-c", bind, "-o", bobj, "-O2", "-std=c++17", "-fPIC",
+                          "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__"] + incs)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for out in ex.map(_run, jobs_list):
+            if verbose and out.strip():
+                print(out)
+    target = _ext_path("_C_kernels")
+    if force or _stale(target, objs):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", target] + objs)
+    return target
+
+
+def build_runtime(force=False, jobs=8, verbose=False) -> str:
+    src_dir = os.path.join(HERE, "runtime")
+    out_dir = os.path.join(BUILD, "runtime")
+    os.makedirs(out_dir, exist_ok=True)
+    headers = glob.glob(os.path.join(src_dir, "*.h"))
+    srcs = sorted(glob.glob(os.path.join(src_dir, "*.cpp")))
+    incs = [f"-I{p}" for p in _py_includes()] + [f"-I{src_dir}"]
+    objs, jobs_list = [], []
+    for src in srcs:
+        obj = os.path.join(out_dir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src] + headers):
+            jobs_list.append([CXX, "-c", src, "-o", obj, "-O2", "-std=c++17", "-fPIC",
+                              "-fvisibility=hidden", "-Wall"] + incs)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(_run, jobs_list))
+    target = _ext_path("_C_runtime")
+    if force or _stale(target, objs):
+        _run([CXX, "-shared", "-fPIC", "-o", target] + objs)
+    return target
+
+
+def build_all(force=False, jobs=8, verbose=False):
+    return build_runtime(force, jobs, verbose), build_kernels(force, jobs, verbose)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--only", choices=["kernels", "runtime"], default=None)
+    a = ap.parse_args(argv)
+    if a.only in (None, "runtime"):
+        print("built", build_runtime(a.force, a.jobs, a.verbose))
+    if a.only in (None, "kernels"):
+        print("built", build_kernels(a.force, a.jobs, a.verbose))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

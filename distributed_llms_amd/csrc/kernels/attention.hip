@@ -1,0 +1,324 @@
+// K6 + K7: paged attention on MFMA (v_mfma_f32_16x16x32_bf16), decode and prefill.
+//
+// Layout (one pair per layer, block_size BS = 32 tokens):
+//   k_cache [NB, Hkv, 32, D]   key rows contiguous       -> QK A-operand = 16 B / lane
+//   v_cache [NB, Hkv, D, 32]   V stored transposed       -> PV A-operand = 2 x 8 B / lane
+// The 16 MFMA columns are (query row, head-in-GQA-group) pairs, so the K/V bytes of
+// one kv-head are read once for all G = Hq/Hkv query heads:
+//   decode : 1 query  x G heads   (G <= 16 columns used)
+//   prefill: 16/G rows x G heads  (all 16 columns used when G | 16)
+// Scores are computed transposed (S^T = K Q^T): each lane then holds 8 keys of ONE
+// column, the row max needs 2 cross-lane shuffles, and the lane's 8 probabilities are
+// exactly its B-operand fragment for O^T += V^T P^T (the k-order of the PV product is
+// permuted to match, so P never leaves the lane).  Online softmax in base 2.
+#include "common.h"
+#include "launchers.h"
+
+namespace dllm {
+
+constexpr int kBS = 32;       // tokens per KV block (== keys per MFMA chunk)
+constexpr int kWaves = 4;     // waves per workgroup
+
+template <int D>
+struct WaveState {
+  f32x4 acc[D / 16];
+  float m;      // running max (log2 domain) of this lane's column
+  float lsum;   // lane-partial softmax denominator
+};
+
+// Process one 32-key chunk (one KV block) for the wave's 16 columns.
+//   kmax_col : last admissible key index for this lane's column (causal / range), inclusive
+template <int D>
+__device__ __forceinline__ void attend_chunk(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
+                                             const bf16* __restrict__ kblk, const bf16* __restrict__ vblk,
+                                             int t0, int kmax_col, float scale_log2, int lane) {
+  const int r = lane & 15, g = lane >> 4;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(kblk + r * D + ks * 32 + 8 * g);
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(kblk + (16 + r) * D + ks * 32 + 8 * g);
+    s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qf[ks], s0, 0, 0, 0);
+    s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qf[ks], s1, 0, 0, 0);
+  }
+  float p[8];
+  float cm = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k0 = t0 + 4 * g + i, k1 = t0 + 16 + 4 * g + i;
+    p[i] = (k0 <= kmax_col) ? s0[i] * scale_log2 : -INFINITY;
+    p[4 + i] = (k1 <= kmax_col) ? s1[i] * scale_log2 : -INFINITY;
+    cm = fmaxf(cm, fmaxf(p[i], p[4 + i]));
+  }
+  cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+  cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+  // No early exit here: MFMA reads all 64 lanes' operands regardless of EXEC, so every
+  // lane must run the same instruction stream. A fully masked column uses mref = 0,
+  // which turns its probabilities (and its alpha) into exact zeros.
+  const float mn = fmaxf(st.m, cm);
+  const float mref = (mn == -INFINITY) ? 0.f : mn;
+  const float alpha = exp2f(st.m - mref);
+  st.m = mn;
+  bf16x8 pb;
+  float ps = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float e = exp2f(p[j] - mref);
+    ps += e;
+    pb[j] = f2bf(e);
+  }
+  st.lsum = st.lsum * alpha + ps;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    st.acc[dt] *= alpha;
+    const bf16* vr = vblk + (dt * 16 + r) * kBS;
+    const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vr + 4 * g);
+    const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vr + 16 + 4 * g);
+    bf16x8 va;
+    va[0] = lo[0]; va[1] = lo[1]; va[2] = lo[2]; va[3] = lo[3];
+    va[4] = hi[0]; va[5] = hi[1]; va[6] = hi[2]; va[7] = hi[3];
+    st.acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, st.acc[dt], 0, 0, 0);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void init_state(WaveState<D>& st) {
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) st.acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  st.m = -INFINITY;
+  st.lsum = 0.f;
+}
+
+// ---------------------------------------------------------------------------
+// Decode: grid (num_splits, Hkv, B); 4 waves split the WG's key range by chunk,
+// then combine through LDS. num_splits > 1 writes (o, m, l) partials for the
+// split-reduce kernel below.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ void __launch_bounds__(256) attn_decode_kernel(
+    bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
+    const int32_t* __restrict__ seq_lens, float* __restrict__ part_o, float* __restrict__ part_ml,
+    int hq, int hkv, int max_blocks, int split_len, float scale_log2) {
+  __shared__ float sm_o[kWaves][D][16];
+  __shared__ float sm_m[kWaves][16];
+  __shared__ float sm_l[kWaves][16];
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int nsplit = gridDim.x;
+  const int G = hq / hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int ctx = seq_lens[b];
+  const int kbeg = split * split_len;
+  const int kend = min(kbeg + split_len, ctx);  // exclusive
+
+  // Q^T fragments: column r = head kvh*G + r (zero beyond G)
+  bf16x8 qf[D / 32];
+  const bool col_ok = r < G;
+  const bf16* qrow = q + ((size_t)b * hq + kvh * G + (col_ok ? r : 0)) * D;
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
+    if (!col_ok) v = bf16x8{};
+    qf[ks] = v;
+  }
+  WaveState<D> st;
+  init_state(st);
+  const int kmax = kend - 1;
+  const size_t kv_head_stride = (size_t)kBS * D;
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  for (int c = kbeg / kBS + w; c * kBS < kend; c += kWaves) {
+    const int blk = bt[c];
+    const size_t base = ((size_t)blk * hkv + kvh) * kv_head_stride;
+    attend_chunk<D>(st, qf, k_cache + base, v_cache + base, c * kBS, kmax, scale_log2, lane);
+  }
+  float lt = st.lsum;
+  lt += __shfl_xor(lt, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+  // stage this wave's (m, l, O^T) into LDS
+  if (g == 0) { sm_m[w][r] = st.m; sm_l[w][r] = lt; }
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm_o[w][dt * 16 + 4 * g + i][r] = st.acc[dt][i];
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < D * G; idx += blockDim.x) {
+    const int c = idx % G, d = idx / G;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) M = fmaxf(M, sm_m[ww][c]);
+    float num = 0.f, den = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) {
+        const float f = exp2f(sm_m[ww][c] - M);
+        num += sm_o[ww][d][c] * f;
+        den += sm_l[ww][c] * f;
+      }
+    }
+    const int h = kvh * G + c;
+    if (nsplit == 1) {
+      out[((size_t)b * hq + h) * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+    } else {
+      const size_t pi = ((size_t)b * hq + h) * nsplit + split;
+      part_o[pi * D + d] = num;
+      if (d == 0) { part_ml[pi * 2] = M; part_ml[pi * 2 + 1] = den; }
+    }
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(D) attn_split_reduce_kernel(bf16* __restrict__ out,
+                                                              const float* __restrict__ part_o,
+                                                              const float* __restrict__ part_ml,
+                                                              int nsplit) {
+  const int bh = blockIdx.x, d = threadIdx.x;
+  const float* ml = part_ml + (size_t)bh * nsplit * 2;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
+  float num = 0.f, den = 0.f;
+  if (M != -INFINITY) {
+    for (int s = 0; s < nsplit; ++s) {
+      const float f = exp2f(ml[2 * s] - M);
+      num += part_o[((size_t)bh * nsplit + s) * D + d] * f;
+      den += ml[2 * s + 1] * f;
+    }
+  }
+  out[(size_t)bh * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+}
+
+// ---------------------------------------------------------------------------
+// Prefill (causal, varlen, context already in the paged cache): grid
+// (q_tiles, Hkv, B). Each wave owns R = 16/G query rows x G heads; rows of
+// sequence b are its LAST q_len tokens of ctx (chunked prefill supported).
+// ---------------------------------------------------------------------------
+template <int D, int G>
+__global__ void __launch_bounds__(256) attn_prefill_kernel(
+    bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
+    const int32_t* __restrict__ cu_seqlens_q, const int32_t* __restrict__ seq_lens, int hq, int hkv,
+    int max_blocks, float scale_log2) {
+  constexpr int R = 16 / G;
+  const int kvh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int qs = cu_seqlens_q[b], ql = cu_seqlens_q[b + 1] - qs;
+  const int row0 = (blockIdx.x * kWaves + w) * R;
+  if (row0 >= ql) return;
+  const int ctx = seq_lens[b];
+  const int qpos0 = ctx - ql;  // position of row 0
+  const int crow = row0 + r / G, ch = r % G;
+  const bool col_ok = crow < ql;
+  const int kmax_col = col_ok ? qpos0 + crow : -1;
+  bf16x8 qf[D / 32];
+  const bf16* qrow = q + ((size_t)(qs + (col_ok ? crow : 0)) * hq + kvh * G + ch) * D;
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
+    if (!col_ok) v = bf16x8{};
+    qf[ks] = v;
+  }
+  WaveState<D> st;
+  init_state(st);
+  const int wave_kmax = qpos0 + min(row0 + R, ql) - 1;
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  const size_t kv_head_stride = (size_t)kBS * D;
+  for (int c = 0; c * kBS <= wave_kmax; ++c) {
+    const int blk = bt[c];
+    const size_t base = ((size_t)blk * hkv + kvh) * kv_head_stride;
+    attend_chunk<D>(st, qf, k_cache + base, v_cache + base, c * kBS, kmax_col, scale_log2, lane);
+  }
+  float lt = st.lsum;
+  lt += __shfl_xor(lt, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+  if (!col_ok) return;
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  bf16* orow = out + ((size_t)(qs + crow) * hq + kvh * G + ch) * D;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    bf16x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = f2bf(st.acc[dt][i] * inv);
+    *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = o;
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
+                            uintptr_t block_tables, uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml,
+                            int batch, int hq, int hkv, int d, int block_size, int max_blocks, int num_splits,
+                            int split_len, float scale, uintptr_t stream) {
+  DLLM_HOST_CHECK(block_size == kBS, "paged attention requires block_size 32");
+  DLLM_HOST_CHECK(hq % hkv == 0 && hq / hkv <= 16, "GQA group size must be <= 16");
+  DLLM_HOST_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
+  DLLM_HOST_CHECK(num_splits >= 1 && split_len % kBS == 0 && split_len > 0, "split_len multiple of 32");
+  DLLM_HOST_CHECK(num_splits == 1 || (part_o && part_ml), "split workspace");
+  DLLM_HOST_CHECK((long)num_splits * split_len >= 1, "splits");
+  if (batch == 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float sl2 = scale * 1.4426950408889634f;
+  dim3 grid(num_splits, hkv, batch);
+  if (d == 128)
+    hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,
+                       (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)block_tables,
+                       (const int32_t*)seq_lens, (float*)part_o, (float*)part_ml, hq, hkv, max_blocks,
+                       split_len, sl2);
+  else
+    hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,
+                       (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)block_tables,
+                       (const int32_t*)seq_lens, (float*)part_o, (float*)part_ml, hq, hkv, max_blocks,
+                       split_len, sl2);
+  DLLM_HIP_CHECK(hipGetLastError());
+  if (num_splits > 1) {
+    if (d == 128)
+      hipLaunchKernelGGL(attn_split_reduce_kernel<128>, dim3(batch * hq), dim3(128), 0, s, (bf16*)out,
+                         (const float*)part_o, (const float*)part_ml, num_splits);
+    else
+      hipLaunchKernelGGL(attn_split_reduce_kernel<64>, dim3(batch * hq), dim3(64), 0, s, (bf16*)out,
+                         (const float*)part_o, (const float*)part_ml, num_splits);
+    DLLM_HIP_CHECK(hipGetLastError());
+  }
+}
+
+template <int D>
+static void launch_prefill(int g, dim3 grid, hipStream_t s, uintptr_t out, uintptr_t q, uintptr_t k_cache,
+                           uintptr_t v_cache, uintptr_t bt, uintptr_t cu, uintptr_t sl, int hq, int hkv,
+                           int max_blocks, float sl2) {
+#define DLLM_PF(GG)                                                                                     \
+  hipLaunchKernelGGL((attn_prefill_kernel<D, GG>), grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q, \
+                     (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt, (const int32_t*)cu, \
+                     (const int32_t*)sl, hq, hkv, max_blocks, sl2)
+  switch (g) {
+    case 1: DLLM_PF(1); break;
+    case 2: DLLM_PF(2); break;
+    case 4: DLLM_PF(4); break;
+    case 8: DLLM_PF(8); break;
+    case 16: DLLM_PF(16); break;
+    default: throw std::runtime_error("prefill attention: GQA group must be 1,2,4,8,16");
+  }
+#undef DLLM_PF
+}
+
+void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
+                             uintptr_t block_tables, uintptr_t cu_seqlens_q, uintptr_t seq_lens, int batch,
+                             int hq, int hkv, int d, int block_size, int max_blocks, int max_q_len, float scale,
+                             uintptr_t stream) {
+  DLLM_HOST_CHECK(block_size == kBS, "paged attention requires block_size 32");
+  DLLM_HOST_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
+  DLLM_HOST_CHECK(hq % hkv == 0, "Hq % Hkv");
+  if (batch == 0 || max_q_len == 0) return;
+  const int G = hq / hkv;
+  const int rows_per_wg = kWaves * (16 / G);
+  dim3 grid((max_q_len + rows_per_wg - 1) / rows_per_wg, hkv, batch);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float sl2 = scale * 1.4426950408889634f;
+  if (d == 128)
+    launch_prefill<128>(G, grid, s, out, q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, hq, hkv,
+                        max_blocks, sl2);
+  else
+    launch_prefill<64>(G, grid, s, out, q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, hq, hkv,
+                       max_blocks, sl2);
+  DLLM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dllm

@@ -1,0 +1,22 @@
+// pybind11 bindings for the gfx950 kernel launchers.
+// Tensors cross the boundary as raw device pointers (uintptr_t) plus explicit
+// shapes; the Python wrappers in distributed_llms_amd/ops check dtype/contiguity
+// and pass torch's current HIP stream, so every launch is graph-capturable.
+#include <pybind11/pybind11.h>
+
+#include "launchers.h"
+
+namespace py = pybind11;
+
+PYBIND11_MODULE(_C_kernels, m) {
+  m.doc() = "distributed_llms_amd HIP kernels (gfx950 / CDNA4)";
+  m.attr("arch") = "gfx950";
+  m.def("rms_norm", &dllm::rms_norm, py::arg("y"), py::arg("x"), py::arg("residual"), py::arg("w"),
+        py::arg("rows"), py::arg("hidden"), py::arg("eps"), py::arg("stream"));
+  m.def("embedding", &dllm::embedding);
+  m.def("rope_cache_append", &dllm::rope_cache_append);
+  m.def("silu_mul", &dllm::silu_mul);
+  m.def("argmax", &dllm::argmax);
+  m.def("paged_attention_decode", &dllm::paged_attention_decode);
+  m.def("paged_attention_prefill", &dllm::paged_attention_prefill);
+}

@@ -1,0 +1,29 @@
+// Host-side launcher declarations (C++ ABI, pointers as uintptr_t, stream as uintptr_t).
+// Every launcher validates the shapes its grid assumes before launching.
+#pragma once
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+namespace dllm {
+
+void rms_norm(uintptr_t y, uintptr_t x, uintptr_t residual, uintptr_t w, int rows, int hidden, float eps,
+              uintptr_t stream);
+void embedding(uintptr_t out, uintptr_t ids, uintptr_t table, int tokens, int hidden, int vocab,
+               uintptr_t stream);
+void rope_cache_append(uintptr_t q_out, uintptr_t qkv, uintptr_t positions, uintptr_t cos_sin,
+                       uintptr_t k_cache, uintptr_t v_cache, uintptr_t slots, int tokens, int hq, int hkv,
+                       int d, int bs, uintptr_t stream);
+void silu_mul(uintptr_t out, uintptr_t gu, int tokens, int inter, uintptr_t stream);
+void argmax(uintptr_t out, uintptr_t logits, int rows, int vocab, long row_stride, uintptr_t stream);
+
+void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
+                            uintptr_t block_tables, uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml,
+                            int batch, int hq, int hkv, int d, int block_size, int max_blocks, int num_splits,
+                            int split_len, float scale, uintptr_t stream);
+void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
+                             uintptr_t block_tables, uintptr_t cu_seqlens_q, uintptr_t seq_lens, int batch,
+                             int hq, int hkv, int d, int block_size, int max_blocks, int max_q_len, float scale,
+                             uintptr_t stream);
+
+}  // namespace dllm

@@ -1,0 +1,235 @@
+"""Engine ops: HIP/CDNA4 kernels for GPU tensors, PyTorch reference for CPU tensors.
+
+Device dispatch only (no backend choice on the GPU): a CUDA tensor always goes to the
+in-tree ``_C_kernels`` module and raises if it is not built -- there is no silent
+eager fallback on the GPU.  The single exception is the plain dense GEMM for large
+M (prefill), which is a library GEMM (hipBLASLt through ``torch.matmul``); small-M
+decode GEMMs run on the hand-written MFMA kernel (``linear``).
+
+Every wrapper checks dtype/contiguity/shape on the host before launching, and launches
+on torch's current stream so the whole decode step can be captured in a HIP graph.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .. import _ext
+from . import reference as ref
+
+__all__ = [
+    "embedding", "rms_norm", "fused_add_rms_norm", "layer_norm", "linear", "silu_mul",
+    "gelu_tanh", "rope_cache_append", "paged_attention_decode", "paged_attention_prefill",
+    "argmax", "moe_route", "moe_mlp", "decode_split_plan",
+]
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ck(t: torch.Tensor, name: str, dtype=torch.bfloat16):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# --------------------------------------------------------------------- K1
+def embedding(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    if not _gpu(weight):
+        return ref.embedding(ids, weight)
+    _ck(weight, "embedding.weight")
+    _ck(ids, "embedding.ids", torch.int32)
+    t, (v, h) = ids.numel(), weight.shape
+    out = torch.empty(t, h, dtype=weight.dtype, device=weight.device)
+    _ext.kernels().embedding(out.data_ptr(), ids.data_ptr(), weight.data_ptr(), t, h, v, _stream())
+    return out
+
+
+# --------------------------------------------------------------------- K2
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    if not _gpu(x):
+        return ref.rms_norm(x, w, eps)
+    _ck(x, "rms_norm.x")
+    _ck(w, "rms_norm.w")
+    h = x.shape[-1]
+    y = torch.empty_like(x)
+    _ext.kernels().rms_norm(y.data_ptr(), x.data_ptr(), 0, w.data_ptr(), x.numel() // h, h, float(eps), _stream())
+    return y
+
+
+def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                       eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """residual <- x + residual (in place); returns (rms_norm(residual) * w, residual)."""
+    if not _gpu(x):
+        return ref.fused_add_rms_norm(x, residual, w, eps)
+    _ck(x, "fused_add_rms_norm.x")
+    _ck(residual, "fused_add_rms_norm.residual")
+    _ck(w, "fused_add_rms_norm.w")
+    if x.shape != residual.shape:
+        raise ValueError("x/residual shape mismatch")
+    h = x.shape[-1]
+    y = torch.empty_like(x)
+    _ext.kernels().rms_norm(y.data_ptr(), x.data_ptr(), residual.data_ptr(), w.data_ptr(), x.numel() // h, h,
+                            float(eps), _stream())
+    return y, residual
+
+
+def layer_norm(x, w, b, eps):
+    # GPT-2 plumbing config only: torch path on both devices.
+    return ref.layer_norm(x, w, b, eps)
+
+
+def gelu_tanh(x):
+    return ref.gelu_tanh(x)
+
+
+# --------------------------------------------------------------- GEMM
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w^T (+bias). w is [N, K]."""
+    if not _gpu(x):
+        return ref.linear(x, w, bias)
+    from . import gemm
+    return gemm.linear(x, w, bias)
+
+
+# ------------------------------------------------------------ SwiGLU
+def silu_mul(gu: torch.Tensor) -> torch.Tensor:
+    if not _gpu(gu):
+        return ref.silu_mul(gu)
+    _ck(gu, "silu_mul.gu")
+    t, two_i = gu.shape
+    out = torch.empty(t, two_i // 2, dtype=gu.dtype, device=gu.device)
+    _ext.kernels().silu_mul(out.data_ptr(), gu.data_ptr(), t, two_i // 2, _stream())
+    return out
+
+
+# ----------------------------------------------------------- K4 + K5
+def rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, num_heads, num_kv_heads,
+                      head_dim) -> torch.Tensor:
+    if not _gpu(qkv):
+        return ref.rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, num_heads,
+                                     num_kv_heads, head_dim)
+    _ck(qkv, "rope.qkv")
+    _ck(k_cache, "k_cache")
+    _ck(v_cache, "v_cache")
+    _ck(positions, "positions", torch.int32)
+    _ck(slot_mapping, "slot_mapping", torch.int32)
+    t = qkv.shape[0]
+    if qkv.shape[1] != (num_heads + 2 * num_kv_heads) * head_dim:
+        raise ValueError("qkv width mismatch")
+    if cos_sin is not None:
+        _ck(cos_sin, "cos_sin", torch.float32)
+        if cos_sin.shape[1] != head_dim:
+            raise ValueError("cos_sin width must equal head_dim")
+    q = torch.empty(t, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
+    _ext.kernels().rope_cache_append(q.data_ptr(), qkv.data_ptr(), positions.data_ptr(),
+                                     0 if cos_sin is None else cos_sin.data_ptr(), k_cache.data_ptr(),
+                                     v_cache.data_ptr(), slot_mapping.data_ptr(), t, num_heads, num_kv_heads,
+                                     head_dim, k_cache.shape[2], _stream())
+    return q
+
+
+# ---------------------------------------------------------- K6 / K7
+def decode_split_plan(batch: int, num_kv_heads: int, max_ctx: int, block_size: int = 32,
+                      target_wgs: int = 1024) -> Tuple[int, int]:
+    """(num_splits, split_len) for the decode kernel.
+
+    Enough workgroups to fill 256 CUs several times over, each split a multiple of
+    4 waves x 32 keys; fixed for a given (batch, max_ctx) bucket so graphs can replay.
+    """
+    chunk = 4 * block_size
+    max_splits = max(1, -(-max_ctx // chunk))
+    want = max(1, -(-target_wgs // max(1, batch * num_kv_heads)))
+    splits = min(want, max_splits, 64)
+    split_len = -(-max_ctx // splits)
+    split_len = -(-split_len // block_size) * block_size
+    splits = -(-max_ctx // split_len)
+    return splits, split_len
+
+
+def paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale: float,
+                           max_ctx: Optional[int] = None, workspace: Optional[tuple] = None):
+    if not _gpu(q):
+        return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
+    _ck(q, "attn.q")
+    _ck(k_cache, "k_cache")
+    _ck(v_cache, "v_cache")
+    _ck(block_tables, "block_tables", torch.int32)
+    _ck(seq_lens, "seq_lens", torch.int32)
+    b, hq, d = q.shape
+    hkv, bs = k_cache.shape[1], k_cache.shape[2]
+    max_blocks = block_tables.shape[1]
+    if max_ctx is None:
+        max_ctx = max_blocks * bs
+    if max_ctx > max_blocks * bs:
+        raise ValueError("max_ctx exceeds block table capacity")
+    splits, split_len = decode_split_plan(b, hkv, max_ctx, bs)
+    out = torch.empty_like(q)
+    po = pml = 0
+    if splits > 1:
+        if workspace is None:
+            po_t = torch.empty(b * hq * splits * d, dtype=torch.float32, device=q.device)
+            pml_t = torch.empty(b * hq * splits * 2, dtype=torch.float32, device=q.device)
+        else:
+            po_t, pml_t = workspace
+            if po_t.numel() < b * hq * splits * d or pml_t.numel() < b * hq * splits * 2:
+                raise ValueError("attention workspace too small")
+        po, pml = po_t.data_ptr(), pml_t.data_ptr()
+    _ext.kernels().paged_attention_decode(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                          block_tables.data_ptr(), seq_lens.data_ptr(), po, pml, b, hq, hkv, d,
+                                          bs, max_blocks, splits, split_len, float(scale), _stream())
+    return out
+
+
+def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, scale: float,
+                            max_q_len: Optional[int] = None):
+    if not _gpu(q):
+        return ref.paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, scale)
+    _ck(q, "attn.q")
+    _ck(k_cache, "k_cache")
+    _ck(v_cache, "v_cache")
+    _ck(block_tables, "block_tables", torch.int32)
+    _ck(cu_seqlens_q, "cu_seqlens_q", torch.int32)
+    _ck(seq_lens, "seq_lens", torch.int32)
+    t, hq, d = q.shape
+    b = seq_lens.shape[0]
+    if max_q_len is None:
+        max_q_len = int((cu_seqlens_q[1:] - cu_seqlens_q[:-1]).max().item()) if b else 0
+    out = torch.empty_like(q)
+    _ext.kernels().paged_attention_prefill(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                           block_tables.data_ptr(), cu_seqlens_q.data_ptr(), seq_lens.data_ptr(),
+                                           b, hq, k_cache.shape[1], d, k_cache.shape[2], block_tables.shape[1],
+                                           int(max_q_len), float(scale), _stream())
+    return out
+
+
+# ------------------------------------------------------------- K10
+def argmax(logits: torch.Tensor) -> torch.Tensor:
+    if not _gpu(logits):
+        return ref.argmax(logits)
+    if logits.dtype != torch.bfloat16:
+        return logits.argmax(-1).to(torch.int32)
+    if logits.stride(-1) != 1:
+        raise ValueError("argmax: last dim must be contiguous")
+    rows, v = logits.shape
+    out = torch.empty(rows, dtype=torch.int32, device=logits.device)
+    _ext.kernels().argmax(out.data_ptr(), logits.data_ptr(), rows, v, logits.stride(0), _stream())
+    return out
+
+
+# ------------------------------------------------------------ K11/K12
+def moe_route(router_logits: torch.Tensor, top_k: int):
+    from . import moe
+    return moe.route(router_logits, top_k)
+
+
+def moe_mlp(x, w_gate_up, w_down, topk_w, topk_ids):
+    from . import moe
+    return moe.mlp(x, w_gate_up, w_down, topk_w, topk_ids)

@@ -1,0 +1,135 @@
+"""HIP kernel numerics vs the plain-PyTorch fp32 reference of the same op (gfx950 only)."""
+import math
+
+import pytest
+import torch
+
+from distributed_llms_amd import _ext, ops
+from distributed_llms_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(*shape, scale=1.0, dev="cuda"):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+def test_native_module_loaded(cuda):
+    k = _ext.kernels()
+    assert k.arch == "gfx950"
+
+
+@pytest.mark.parametrize("rows,hidden", [(1, 4096), (7, 4096), (64, 8192), (3, 768), (5, 128)])
+def test_rms_norm(cuda, rows, hidden):
+    x, w = _bf(rows, hidden), _bf(hidden)
+    y = ops.rms_norm(x, w, 1e-5)
+    yr = ref.rms_norm(x.float(), w.float(), 1e-5)
+    torch.testing.assert_close(y.float(), yr, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("rows,hidden", [(1, 4096), (33, 4096), (16, 8192)])
+def test_fused_add_rms_norm(cuda, rows, hidden):
+    x, r, w = _bf(rows, hidden), _bf(rows, hidden), _bf(hidden)
+    r0 = r.clone()
+    y, r2 = ops.fused_add_rms_norm(x, r, w, 1e-5)
+    rr = (x.float() + r0.float()).to(torch.bfloat16)
+    torch.testing.assert_close(r2, rr, atol=0, rtol=0)
+    yr = ref.rms_norm(rr.float(), w.float(), 1e-5)
+    torch.testing.assert_close(y.float(), yr, atol=2e-2, rtol=2e-2)
+
+
+def test_embedding(cuda):
+    table = _bf(1000, 512)
+    ids = torch.randint(0, 1000, (37,), device="cuda", dtype=torch.int32)
+    torch.testing.assert_close(ops.embedding(ids, table), table[ids.long()], atol=0, rtol=0)
+
+
+def test_silu_mul(cuda):
+    gu = _bf(19, 2 * 1024)
+    torch.testing.assert_close(ops.silu_mul(gu).float(), ref.silu_mul(gu.float()), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("rows,vocab", [(1, 128256), (9, 50257), (4, 32000)])
+def test_argmax(cuda, rows, vocab):
+    logits = _bf(rows, vocab, scale=3.0)
+    expect = logits.float().argmax(-1).to(torch.int32)
+    torch.testing.assert_close(ops.argmax(logits), expect)
+
+
+def _cache(nb, hkv, d, bs=32):
+    k = torch.zeros(nb, hkv, bs, d, dtype=torch.bfloat16, device="cuda")
+    v = torch.zeros(nb, hkv, d, bs, dtype=torch.bfloat16, device="cuda")
+    return k, v
+
+
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (12, 12, 64), (64, 8, 128)])
+def test_rope_cache_append(cuda, hq, hkv, d):
+    t, nb = 21, 8
+    qkv = _bf(t, (hq + 2 * hkv) * d)
+    pos = torch.randint(0, 500, (t,), device="cuda", dtype=torch.int32)
+    slots = torch.randperm(nb * 32, device="cuda")[:t].to(torch.int32)
+    cs = ref.rope_cos_sin(d, 1024, 500000.0, device="cuda")
+    k1, v1 = _cache(nb, hkv, d)
+    k2, v2 = _cache(nb, hkv, d)
+    q1 = ops.rope_cache_append(qkv, pos, cs, k1, v1, slots, hq, hkv, d)
+    q2 = ref.rope_cache_append(qkv.float(), pos, cs, k2, v2, slots, hq, hkv, d)
+    torch.testing.assert_close(q1.float(), q2.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(k1.float(), k2.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(v1, v2, atol=0, rtol=0)
+
+
+def _fill_paged(seq_lens, hkv, d, nb_total=None):
+    bs = 32
+    nblocks = [(n + bs - 1) // bs for n in seq_lens]
+    nb_total = nb_total or sum(nblocks) + 3
+    k, v = _cache(nb_total, hkv, d)
+    k.normal_()
+    v.normal_()
+    perm = torch.randperm(nb_total).tolist()
+    mb = max(nblocks)
+    bt = torch.zeros(len(seq_lens), mb, dtype=torch.int32)
+    i = 0
+    for s, n in enumerate(nblocks):
+        bt[s, :n] = torch.tensor(perm[i:i + n])
+        i += n
+    return k, v, bt.cuda()
+
+
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (4, 1, 128)])
+@pytest.mark.parametrize("lens", [[1], [7, 33, 100], [640, 5, 2049, 32]])
+def test_paged_attention_decode(cuda, hq, hkv, d, lens):
+    k, v, bt = _fill_paged(lens, hkv, d)
+    sl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = _bf(len(lens), hq, d)
+    scale = 1 / math.sqrt(d)
+    out = ops.paged_attention_decode(q, k, v, bt, sl, scale)
+    expect = ref.paged_attention_decode(q.float(), k.float(), v.float(), bt, sl, scale)
+    torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 64)])
+def test_paged_attention_prefill(cuda, hq, hkv, d):
+    ctx = [37, 128, 300, 5]
+    qlen = [37, 64, 1, 5]       # second/third: chunked prefill with prior context
+    k, v, bt = _fill_paged(ctx, hkv, d)
+    cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32, device="cuda")
+    sl = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+    q = _bf(sum(qlen), hq, d)
+    scale = 1 / math.sqrt(d)
+    out = ops.paged_attention_prefill(q, k, v, bt, cu, sl, scale)
+    expect = ref.paged_attention_prefill(q.float(), k.float(), v.float(), bt, cu, sl, scale)
+    torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
+
+
+def test_attention_masked_spike(cuda):
+    """Force the online-softmax rescale: one key far above the rest, late in the sequence."""
+    hq, hkv, d = 32, 8, 128
+    lens = [1000]
+    k, v, bt = _fill_paged(lens, hkv, d)
+    q = _bf(1, hq, d)
+    blk = bt[0, 900 // 32].item()
+    k[blk, :, 900 % 32, :] = q[0, ::4].to(k.dtype) * 4
+    sl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    out = ops.paged_attention_decode(q, k, v, bt, sl, 1 / math.sqrt(d))
+    expect = ref.paged_attention_decode(q.float(), k.float(), v.float(), bt, sl, 1 / math.sqrt(d))
+    torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
