@@ -15,6 +15,7 @@ void rope_cache_append(uintptr_t q_out, uintptr_t qkv, uintptr_t positions, uint
                        uintptr_t k_cache, uintptr_t v_cache, uintptr_t slots, int tokens, int hq, int hkv,
                        int d, int bs, uintptr_t stream);
 void silu_mul(uintptr_t out, uintptr_t gu, int tokens, int inter, uintptr_t stream);
+void add_inplace(uintptr_t a, uintptr_t b, long n, uintptr_t stream);
 void argmax(uintptr_t out, uintptr_t logits, int rows, int vocab, long row_stride, uintptr_t stream);
 
 void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,

@@ -205,6 +205,31 @@ void silu_mul(uintptr_t out, uintptr_t gu, int tokens, int inter, uintptr_t stre
 }
 
 // ---------------------------------------------------------------------------
+// a <- a + b (bf16, 16-byte vectors): closes the residual stream at a stage boundary.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) add_inplace_kernel(bf16* __restrict__ a, const bf16* __restrict__ b,
+                                                          long nvec) {
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (long)gridDim.x * 256) {
+    bf16x8 x = reinterpret_cast<bf16x8*>(a)[v];
+    const bf16x8 y = reinterpret_cast<const bf16x8*>(b)[v];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = f2bf(bf2f(x[j]) + bf2f(y[j]));
+    reinterpret_cast<bf16x8*>(a)[v] = x;
+  }
+}
+
+void add_inplace(uintptr_t a, uintptr_t b, long n, uintptr_t stream) {
+  DLLM_HOST_CHECK(n % 8 == 0, "numel % 8");
+  const long nvec = n / 8;
+  if (nvec == 0) return;
+  long blocks = (nvec + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(add_inplace_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (bf16*)a, (const bf16*)b, nvec);
+  DLLM_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
 // K10 tail: greedy argmax over the vocabulary. One 1024-thread workgroup per row.
 // Ties resolve to the smallest index (matches torch.argmax on the fp32 values).
 // ---------------------------------------------------------------------------

@@ -1,0 +1,139 @@
+"""Host-side batch metadata construction and its (de)serialization.
+
+A :class:`HostBatch` is the numpy form of one step's metadata; it is what stage 0
+ships to the other pipeline stages (over the CPU control group) and what every stage
+uploads into its :class:`BatchMeta` device tensors.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..models.stage import BatchMeta
+from .scheduler import Step
+
+_FIELDS = ("ids", "positions", "slots", "seq_lens", "cu_seqlens", "block_tables", "logits_idx")
+
+
+@dataclass
+class HostBatch:
+    is_prefill: bool
+    ids: np.ndarray           # [T] int32
+    positions: np.ndarray     # [T] int32
+    slots: np.ndarray         # [T] int32
+    seq_lens: np.ndarray      # [B] int32
+    cu_seqlens: np.ndarray    # [B+1] int32
+    block_tables: np.ndarray  # [B, MB] int32
+    logits_idx: np.ndarray    # [B] int32
+    max_q_len: int
+    max_ctx: int
+    slot: int = 0
+    step_id: int = 0
+
+    @property
+    def num_tokens(self) -> int:
+        return int(self.ids.shape[0])
+
+    @property
+    def num_seqs(self) -> int:
+        return int(self.seq_lens.shape[0])
+
+    # ------------------------------------------------------ wire format
+    def pack(self) -> np.ndarray:
+        """Flatten to one int32 array: [header(16) | fields...]."""
+        b, t = self.num_seqs, self.num_tokens
+        mb = self.block_tables.shape[1] if self.block_tables.ndim == 2 else 0
+        hdr = np.array([1 if self.is_prefill else 0, t, b, mb, self.max_q_len, self.max_ctx, self.slot,
+                        self.step_id] + [0] * 8, dtype=np.int32)
+        parts = [hdr, self.ids, self.positions, self.slots, self.seq_lens, self.cu_seqlens,
+                 self.block_tables.reshape(-1), self.logits_idx]
+        return np.concatenate([p.astype(np.int32, copy=False).reshape(-1) for p in parts])
+
+    @staticmethod
+    def unpack(arr: np.ndarray) -> "HostBatch":
+        hdr = arr[:16]
+        pf, t, b, mb, mq, mc, slot, sid = (int(x) for x in hdr[:8])
+        o = 16
+        def take(n):
+            nonlocal o
+            v = arr[o:o + n]
+            o += n
+            return v
+        ids, pos, slots = take(t), take(t), take(t)
+        seq_lens, cu = take(b), take(b + 1)
+        bt = take(b * mb).reshape(b, mb)
+        lidx = take(b)
+        return HostBatch(bool(pf), ids, pos, slots, seq_lens, cu, bt, lidx, mq, mc, slot, sid)
+
+
+def next_pow2(x: int, lo: int = 1) -> int:
+    p = lo
+    while p < x:
+        p *= 2
+    return p
+
+
+def build_host_batch(step: Step, bm, block_size: int, max_blocks: Optional[int] = None,
+                     step_id: int = 0) -> HostBatch:
+    seqs = step.seqs
+    b = len(seqs)
+    seq_ids = np.fromiter((s.seq_id for s in seqs), dtype=np.int64, count=b)
+    seq_lens = np.fromiter((s.total_len for s in seqs), dtype=np.int32, count=b)
+    if step.is_prefill:
+        starts = np.fromiter((s.num_cached for s in seqs), dtype=np.int32, count=b)
+        qlens = seq_lens - starts
+        cu = np.zeros(b + 1, dtype=np.int32)
+        np.cumsum(qlens, out=cu[1:])
+        t = int(cu[-1])
+        ids = np.empty(t, dtype=np.int32)
+        positions = np.empty(t, dtype=np.int32)
+        for i, s in enumerate(seqs):
+            toks = s.all_tokens()
+            ids[cu[i]:cu[i + 1]] = toks[s.num_cached:]
+            positions[cu[i]:cu[i + 1]] = np.arange(s.num_cached, s.total_len, dtype=np.int32)
+        logits_idx = (cu[1:] - 1).astype(np.int32)
+        max_q_len = int(qlens.max()) if b else 0
+    else:
+        starts = seq_lens - 1
+        qlens = np.ones(b, dtype=np.int32)
+        cu = np.arange(b + 1, dtype=np.int32)
+        ids = np.fromiter((s.last_token() for s in seqs), dtype=np.int32, count=b)
+        positions = starts.astype(np.int32)
+        logits_idx = np.arange(b, dtype=np.int32)
+        max_q_len = 1
+    t = ids.shape[0]
+    slots = np.empty(t, dtype=np.int32)
+    n = bm.fill_slots(seq_ids, starts.astype(np.int32), qlens.astype(np.int32), slots)
+    assert n == t
+    need_blocks = int(-(-int(seq_lens.max()) // block_size)) if b else 1
+    mb = max_blocks if max_blocks is not None else need_blocks
+    if mb < need_blocks:
+        raise ValueError("max_blocks too small for batch")
+    bt = np.zeros((b, mb), dtype=np.int32)
+    bm.fill_block_tables(seq_ids, bt, 0)
+    max_ctx = int(seq_lens.max()) if b else 0
+    return HostBatch(step.is_prefill, ids, positions, slots, seq_lens, cu, bt, logits_idx, max_q_len,
+                     max_ctx, step.slot, step_id)
+
+
+def to_device_meta(hb: HostBatch, device, pad_ctx_to: Optional[int] = None) -> (torch.Tensor, BatchMeta):
+    """Upload a HostBatch; returns (ids tensor, BatchMeta)."""
+    dev = torch.device(device)
+    nb = dev.type == "cuda"
+    def up(a, dtype=torch.int32):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if nb:
+            t = t.pin_memory()
+        return t.to(dev, dtype=dtype, non_blocking=nb)
+    ids = up(hb.ids)
+    meta = BatchMeta(
+        is_prefill=hb.is_prefill, positions=up(hb.positions), slot_mapping=up(hb.slots),
+        block_tables=up(hb.block_tables), seq_lens=up(hb.seq_lens),
+        cu_seqlens_q=up(hb.cu_seqlens) if hb.is_prefill else None,
+        logits_idx=up(hb.logits_idx, torch.int64) if hb.is_prefill else None,
+        max_q_len=hb.max_q_len, max_ctx=pad_ctx_to or hb.max_ctx, num_seqs=hb.num_seqs,
+        num_tokens=hb.num_tokens)
+    return ids, meta

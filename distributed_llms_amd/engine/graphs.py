@@ -1,0 +1,124 @@
+"""HIP-graph capture/replay of the per-stage decode step (N5 in SURVEY §2.2).
+
+A decode step of an 8B model is ~300 kernel launches; eager launch costs ~3-4 us
+each on the host, so the step is captured once per (batch bucket, context bucket) and
+replayed.  Inputs are copied into persistent device buffers; padded rows of a bucket
+write their K/V into the reserved scratch block 0 (slot 0) and attend to one token,
+so they never touch a live sequence.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from .. import ops
+from ..models.stage import BatchMeta, ModelStage
+from .batch import HostBatch, next_pow2
+
+SCRATCH_SEQ_ID = -1      # owns block 0 in the BlockManager
+
+
+class DecodeGraphRunner:
+    def __init__(self, stage: ModelStage, max_batch: int, max_blocks: int, batch_sizes,
+                 min_ctx_bucket: int = 256):
+        self.stage = stage
+        self.dev = stage.device
+        self.max_batch = max(batch_sizes) if batch_sizes else max_batch
+        self.max_batch = max(self.max_batch, 1)
+        self.max_blocks = max_blocks
+        self.block_size = stage.kv.block_size
+        self.batch_sizes = sorted(set(b for b in batch_sizes if b <= self.max_batch)) or [self.max_batch]
+        self.min_ctx_bucket = min_ctx_bucket
+        cfg = stage.cfg
+        mb, dev = self.max_batch, self.dev
+        self.ids = torch.zeros(mb, dtype=torch.int32, device=dev)
+        self.hidden = None if stage.is_first else torch.zeros(mb, cfg.hidden_size, dtype=stage.dtype, device=dev)
+        self.positions = torch.zeros(mb, dtype=torch.int32, device=dev)
+        self.slots = torch.zeros(mb, dtype=torch.int32, device=dev)
+        self.seq_lens = torch.ones(mb, dtype=torch.int32, device=dev)
+        self.block_tables = torch.zeros(mb, max_blocks, dtype=torch.int32, device=dev)
+        max_splits = 64
+        self.ws = (torch.empty(mb * cfg.num_heads * max_splits * cfg.head_dim, dtype=torch.float32, device=dev),
+                   torch.empty(mb * cfg.num_heads * max_splits * 2, dtype=torch.float32, device=dev))
+        self.pinned = torch.empty(4 * mb + mb * max_blocks, dtype=torch.int32).pin_memory()
+        self.graphs: Dict[Tuple[int, int], Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
+        self.pool = None
+        self.copy_done: Optional[torch.cuda.Event] = None
+
+    def bucket(self, b: int, max_ctx: int) -> Tuple[int, int]:
+        bb = next(x for x in self.batch_sizes if x >= b)
+        cb = min(next_pow2(max_ctx, self.min_ctx_bucket), self.max_blocks * self.block_size)
+        return bb, cb
+
+    def can_run(self, b: int, max_ctx: int) -> bool:
+        return b <= self.max_batch and max_ctx <= self.max_blocks * self.block_size
+
+    def _meta(self, bb: int, cb: int) -> BatchMeta:
+        return BatchMeta(is_prefill=False, positions=self.positions[:bb], slot_mapping=self.slots[:bb],
+                         block_tables=self.block_tables[:bb], seq_lens=self.seq_lens[:bb], max_q_len=1,
+                         max_ctx=cb, num_seqs=bb, num_tokens=bb, attn_workspace=self.ws)
+
+    def _inp(self, bb: int) -> torch.Tensor:
+        return self.ids[:bb] if self.stage.is_first else self.hidden[:bb]
+
+    def capture(self, bb: int, cb: int):
+        meta = self._meta(bb, cb)
+        # warm up outside capture (allocator, lazy module init)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.stage.forward(self._inp(bb), meta)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g, pool=self.pool):
+            out = self.stage.forward(self._inp(bb), meta)
+        self.graphs[(bb, cb)] = (g, out)
+        return g, out
+
+    def load_inputs(self, hb: HostBatch, bb: int, hidden: Optional[torch.Tensor] = None):
+        b = hb.num_seqs
+        mbk = hb.block_tables.shape[1]
+        if mbk > self.max_blocks:
+            raise ValueError("block table wider than graph buffers")
+        p = self.pinned
+        if self.copy_done is not None:
+            self.copy_done.synchronize()   # previous step's H2D may still read the pinned buffer
+        n = bb
+        pv = p[: 4 * n].view(4, n)
+        pv.zero_()
+        pv[3].fill_(1)                                  # seq_lens of padded rows = 1
+        pv[0, :b] = torch.from_numpy(hb.ids)
+        pv[1, :b] = torch.from_numpy(hb.positions)
+        pv[2, :b] = torch.from_numpy(hb.slots)
+        pv[3, :b] = torch.from_numpy(hb.seq_lens)
+        bt = p[4 * n: 4 * n + n * self.max_blocks].view(n, self.max_blocks)
+        bt.zero_()
+        bt[:b, :mbk] = torch.from_numpy(hb.block_tables)
+        self.ids[:n].copy_(pv[0], non_blocking=True)
+        self.positions[:n].copy_(pv[1], non_blocking=True)
+        self.slots[:n].copy_(pv[2], non_blocking=True)
+        self.seq_lens[:n].copy_(pv[3], non_blocking=True)
+        self.block_tables[:n].copy_(bt, non_blocking=True)
+        if self.copy_done is None:
+            self.copy_done = torch.cuda.Event()
+        self.copy_done.record()
+        if hidden is not None:
+            self.hidden[:b].copy_(hidden[:b])
+            if bb > b:
+                self.hidden[b:bb].zero_()
+
+    def run(self, hb: HostBatch, hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Replay the bucket's graph; returns the (static) output truncated to the real batch."""
+        b = hb.num_seqs
+        bb, cb = self.bucket(b, hb.max_ctx)
+        self.load_inputs(hb, bb, hidden)
+        entry = self.graphs.get((bb, cb))
+        if entry is None:
+            entry = self.capture(bb, cb)
+        g, out = entry
+        g.replay()
+        return out[:b]

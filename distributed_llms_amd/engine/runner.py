@@ -1,0 +1,75 @@
+"""Stage executor: a ModelStage + its paged KV pool + decode-graph runner.
+
+Used by the single-GPU engine and by every pipeline worker.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Optional
+
+import torch
+
+from ..config import EngineConfig, ModelConfig
+from ..models.stage import KVCache, ModelStage
+from .batch import HostBatch, to_device_meta
+from .graphs import DecodeGraphRunner
+
+log = logging.getLogger("dllm.runner")
+
+
+def plan_kv_blocks(mcfg: ModelConfig, num_layers: int, ecfg: EngineConfig, device) -> int:
+    """KV blocks for a stage: enough for max_batch x max_seq_len (+ scratch), capped by free HBM."""
+    bs = ecfg.kv_block_size
+    if ecfg.num_kv_blocks > 0:
+        return ecfg.num_kv_blocks
+    per_seq = -(-ecfg.max_seq_len // bs)
+    slots = max(1, ecfg.microbatches or ecfg.num_workers)
+    want = ecfg.max_batch * slots * per_seq + 2
+    per_block = KVCache.bytes_per_block(num_layers, mcfg.num_kv_heads, mcfg.head_dim, bs)
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        free, _total = torch.cuda.mem_get_info(dev)
+        cap = int(free * ecfg.kv_cache_fraction) // per_block
+    else:
+        cap = max(64, (2 << 30) // per_block)     # CPU: at most ~2 GiB of KV
+    n = min(want, cap)
+    if n < 2:
+        raise RuntimeError("not enough memory for the KV cache")
+    return n
+
+
+class StageRunner:
+    def __init__(self, stage: ModelStage, ecfg: EngineConfig, num_blocks: Optional[int] = None):
+        self.stage = stage
+        self.ecfg = ecfg
+        self.block_size = ecfg.kv_block_size
+        nb = num_blocks or plan_kv_blocks(stage.cfg, stage.num_layers, ecfg, stage.device)
+        stage.allocate_kv(nb, self.block_size)
+        self.num_blocks = nb
+        self.max_blocks = -(-ecfg.max_seq_len // self.block_size)
+        self.graphs: Optional[DecodeGraphRunner] = None
+        if ecfg.use_graphs and stage.device.type == "cuda":
+            sizes = [b for b in ecfg.graph_batch_sizes if b <= ecfg.max_batch] or [ecfg.max_batch]
+            if max(sizes) < ecfg.max_batch:
+                sizes.append(ecfg.max_batch)
+            self.graphs = DecodeGraphRunner(stage, ecfg.max_batch, self.max_blocks, sizes)
+        log.info("stage [%d,%d) kv blocks=%d (%.1f GiB) weights=%.2f GiB", stage.layer_start, stage.layer_end,
+                 nb, stage.kv.nbytes / 2**30, stage.weight_bytes() / 2**30)
+
+    @torch.inference_mode()
+    def execute(self, hb: HostBatch, hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+        st = self.stage
+        if (not hb.is_prefill) and self.graphs is not None and self.graphs.can_run(hb.num_seqs, hb.max_ctx):
+            return self.graphs.run(hb, hidden)
+        ids, meta = to_device_meta(hb, st.device)
+        return st.forward(ids if st.is_first else hidden, meta)
+
+    def warmup_graphs(self, batch_sizes=None, ctx_buckets=(256,)):
+        """Pre-capture decode graphs (keeps capture cost out of timed regions)."""
+        if self.graphs is None:
+            return
+        for b in (batch_sizes or self.graphs.batch_sizes):
+            for c in ctx_buckets:
+                bb, cb = self.graphs.bucket(b, c)
+                if (bb, cb) not in self.graphs.graphs:
+                    self.graphs.capture(bb, cb)

@@ -1,0 +1,215 @@
+"""A pipeline stage of a decoder-only transformer: the layer slice one worker owns.
+
+Realizes what the reference's ``ModelShard`` only pretends to do
+(``src/worker/node.py:13-32``: a placeholder ``inputs[key] @ param``): a contiguous
+block range ``[layer_start, layer_end)`` with its paged KV cache, plus the token
+embedding on the first stage and final norm + LM head on the last.
+
+Stage I/O:
+  first stage  input: token ids [T] int32
+  other stages input: hidden [T, H] (the closed residual stream of the previous stage)
+  last stage  output: logits [n, V] for the rows in ``meta.logits_idx``
+  other stages output: hidden [T, H]
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+from .. import ops
+from ..config import ModelConfig
+from ..ops import reference as ref
+from . import weights as W
+
+
+@dataclass
+class BatchMeta:
+    """Per-step attention metadata (device tensors) + host-side scalars."""
+    is_prefill: bool
+    positions: torch.Tensor          # [T] int32
+    slot_mapping: torch.Tensor       # [T] int32
+    block_tables: torch.Tensor       # [B, max_blocks] int32
+    seq_lens: torch.Tensor           # [B] int32 context length after this step
+    cu_seqlens_q: Optional[torch.Tensor] = None   # [B+1] int32 (prefill)
+    logits_idx: Optional[torch.Tensor] = None     # [B] int64 rows that produce logits (prefill)
+    max_q_len: int = 1
+    max_ctx: int = 0
+    num_seqs: int = 0
+    num_tokens: int = 0
+    attn_workspace: Optional[tuple] = None
+
+
+class KVCache:
+    """Paged KV for the stage's layers: k [L, NB, Hkv, BS, D], v [L, NB, Hkv, D, BS]."""
+
+    def __init__(self, num_layers: int, num_blocks: int, num_kv_heads: int, head_dim: int,
+                 block_size: int, dtype, device):
+        self.num_layers, self.num_blocks, self.block_size = num_layers, num_blocks, block_size
+        self.k = torch.zeros(num_layers, num_blocks, num_kv_heads, block_size, head_dim, dtype=dtype, device=device)
+        self.v = torch.zeros(num_layers, num_blocks, num_kv_heads, head_dim, block_size, dtype=dtype, device=device)
+
+    def layer(self, i: int):
+        return self.k[i], self.v[i]
+
+    @property
+    def nbytes(self) -> int:
+        return self.k.numel() * self.k.element_size() * 2
+
+    @staticmethod
+    def bytes_per_block(num_layers, num_kv_heads, head_dim, block_size, dtype_bytes=2) -> int:
+        return 2 * num_layers * num_kv_heads * head_dim * block_size * dtype_bytes
+
+
+class ModelStage:
+    def __init__(self, cfg: ModelConfig, layer_start: int, layer_end: int, device="cpu",
+                 dtype=torch.bfloat16):
+        if not (0 <= layer_start < layer_end <= cfg.num_layers):
+            raise ValueError(f"bad layer range [{layer_start}, {layer_end}) for {cfg.num_layers} layers")
+        self.cfg = cfg
+        self.layer_start, self.layer_end = layer_start, layer_end
+        self.is_first = layer_start == 0
+        self.is_last = layer_end == cfg.num_layers
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.layers: List[Dict[str, torch.Tensor]] = []
+        self.embed: Dict[str, torch.Tensor] = {}
+        self.head: Dict[str, torch.Tensor] = {}
+        self.kv: Optional[KVCache] = None
+        self.cos_sin = None
+        if cfg.arch != "gpt2":
+            self.cos_sin = ref.rope_cos_sin(cfg.head_dim, cfg.max_position, cfg.rope_theta, cfg.rope_scaling,
+                                            device=self.device)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    # --------------------------------------------------------------- weights
+    @property
+    def num_layers(self) -> int:
+        return self.layer_end - self.layer_start
+
+    def needs_embed(self) -> bool:
+        return self.is_first or (self.is_last and self.cfg.tie_embeddings)
+
+    def init_synthetic(self, seed: int = 0) -> "ModelStage":
+        """Seeded random-init weights generated directly on the stage's device."""
+        cfg = self.cfg
+        self.layers = [W.synth_block(cfg, l, seed, self.dtype, self.device)
+                       for l in range(self.layer_start, self.layer_end)]
+        if self.needs_embed():
+            self.embed = W.synth_embed(cfg, seed, self.dtype, self.device)
+        if self.is_last:
+            self.head = W.synth_head(cfg, seed, self.dtype, self.device)
+        return self
+
+    def load_hf_state(self, sd: Dict[str, torch.Tensor]) -> "ModelStage":
+        """Load from HF-named tensors (a shard file's dict); fuses q|k|v and gate|up."""
+        cfg = self.cfg
+        conv = lambda t: t.to(device=self.device, dtype=self.dtype).contiguous()
+        self.layers = [{k: conv(v) for k, v in W.hf_to_block(cfg, l, sd).items()}
+                       for l in range(self.layer_start, self.layer_end)]
+        if self.needs_embed():
+            self.embed = {k: conv(sd[n]) for k, n in W.hf_embed_names(cfg).items()}
+        if self.is_last:
+            self.head = {k: conv(sd[n]) for k, n in W.hf_head_names(cfg).items()}
+        return self
+
+    def weight_bytes(self) -> int:
+        n = sum(t.numel() * t.element_size() for d in self.layers for t in d.values())
+        n += sum(t.numel() * t.element_size() for t in self.embed.values())
+        n += sum(t.numel() * t.element_size() for t in self.head.values())
+        return n
+
+    def allocate_kv(self, num_blocks: int, block_size: int) -> KVCache:
+        cfg = self.cfg
+        self.kv = KVCache(self.num_layers, num_blocks, cfg.num_kv_heads, cfg.head_dim, block_size,
+                          self.dtype, self.device)
+        return self.kv
+
+    def lm_head_weight(self) -> torch.Tensor:
+        return self.embed["embed"] if self.cfg.tie_embeddings else self.head["lm_head"]
+
+    # --------------------------------------------------------------- forward
+    @torch.inference_mode()
+    def forward(self, inp: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
+        if self.kv is None:
+            raise RuntimeError("allocate_kv() before forward()")
+        if self.cfg.arch == "gpt2":
+            return self._forward_gpt2(inp, meta)
+        return self._forward_llama(inp, meta)
+
+    def _attention(self, qkv: torch.Tensor, li: int, meta: BatchMeta) -> torch.Tensor:
+        cfg = self.cfg
+        k_cache, v_cache = self.kv.layer(li)
+        q = ops.rope_cache_append(qkv, meta.positions, self.cos_sin, k_cache, v_cache, meta.slot_mapping,
+                                  cfg.num_heads, cfg.num_kv_heads, cfg.head_dim)
+        if meta.is_prefill:
+            o = ops.paged_attention_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_seqlens_q,
+                                            meta.seq_lens, self.scale, max_q_len=meta.max_q_len)
+        else:
+            o = ops.paged_attention_decode(q, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.scale,
+                                           max_ctx=meta.max_ctx or None, workspace=meta.attn_workspace)
+        return o.view(o.shape[0], cfg.q_size)
+
+    def _mlp(self, h: torch.Tensor, lw: Dict[str, torch.Tensor]) -> torch.Tensor:
+        if self.cfg.is_moe:
+            router_logits = ops.linear(h, lw["router"])
+            tw, tid = ops.moe_route(router_logits, self.cfg.experts_per_token)
+            return ops.moe_mlp(h, lw["experts_gate_up"], lw["experts_down"], tw, tid)
+        gu = ops.linear(h, lw["w_gate_up"])
+        return ops.linear(ops.silu_mul(gu), lw["w_down"])
+
+    def _forward_llama(self, inp: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
+        cfg = self.cfg
+        eps = cfg.norm_eps
+        residual = ops.embedding(inp, self.embed["embed"]) if self.is_first else inp.clone()
+        h = None
+        for li, lw in enumerate(self.layers):
+            if h is None:
+                h = ops.rms_norm(residual, lw["attn_norm"], eps)
+            else:
+                h, residual = ops.fused_add_rms_norm(h, residual, lw["attn_norm"], eps)
+            qkv = ops.linear(h, lw["wqkv"])
+            a = self._attention(qkv, li, meta)
+            o = ops.linear(a, lw["wo"])
+            h, residual = ops.fused_add_rms_norm(o, residual, lw["mlp_norm"], eps)
+            h = self._mlp(h, lw)
+        if not self.is_last:
+            return ops.add_(residual, h)
+        return self._logits(h, residual, meta)
+
+    def _logits(self, h: torch.Tensor, residual: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
+        cfg = self.cfg
+        if meta.logits_idx is not None:
+            h = h.index_select(0, meta.logits_idx)
+            residual = residual.index_select(0, meta.logits_idx)
+        if cfg.arch == "gpt2":
+            x = ops.layer_norm(h, self.head["final_norm"], self.head["final_norm_b"], cfg.norm_eps)
+        else:
+            x, _ = ops.fused_add_rms_norm(h, residual, self.head["final_norm"], cfg.norm_eps)
+        return ops.linear(x, self.lm_head_weight())
+
+    def _forward_gpt2(self, inp: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
+        cfg = self.cfg
+        eps = cfg.norm_eps
+        if self.is_first:
+            x = ops.embedding(inp, self.embed["embed"])
+            pe = ops.embedding(meta.positions, self.embed["pos_embed"])
+            x = ops.add_(x, pe)
+        else:
+            x = inp.clone()
+        for li, lw in enumerate(self.layers):
+            h = ops.layer_norm(x, lw["ln1_w"], lw["ln1_b"], eps)
+            qkv = ops.linear(h, lw["wqkv"], lw["bqkv"])
+            a = self._attention(qkv, li, meta)
+            x = ops.add_(x, ops.linear(a, lw["wo"], lw["bo"]))
+            h = ops.layer_norm(x, lw["ln2_w"], lw["ln2_b"], eps)
+            f = ops.gelu_tanh(ops.linear(h, lw["w_fc"], lw["b_fc"]))
+            x = ops.add_(x, ops.linear(f, lw["w_proj"], lw["b_proj"]))
+        if not self.is_last:
+            return x
+        if meta.logits_idx is not None:
+            x = x.index_select(0, meta.logits_idx)
+        x = ops.layer_norm(x, self.head["final_norm"], self.head["final_norm_b"], eps)
+        return ops.linear(x, self.lm_head_weight())

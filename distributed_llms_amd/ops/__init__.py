@@ -21,7 +21,7 @@ from . import reference as ref
 __all__ = [
     "embedding", "rms_norm", "fused_add_rms_norm", "layer_norm", "linear", "silu_mul",
     "gelu_tanh", "rope_cache_append", "paged_attention_decode", "paged_attention_prefill",
-    "argmax", "moe_route", "moe_mlp", "decode_split_plan",
+    "argmax", "add_", "moe_route", "moe_mlp", "decode_split_plan",
 ]
 
 
@@ -97,6 +97,19 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         return ref.linear(x, w, bias)
     from . import gemm
     return gemm.linear(x, w, bias)
+
+
+def add_(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a <- a + b (in place)."""
+    if not _gpu(a):
+        a.copy_((a.float() + b.float()).to(a.dtype))
+        return a
+    _ck(a, "add_.a")
+    _ck(b, "add_.b")
+    if a.shape != b.shape:
+        raise ValueError("add_: shape mismatch")
+    _ext.kernels().add_inplace(a.data_ptr(), b.data_ptr(), a.numel(), _stream())
+    return a
 
 
 # ------------------------------------------------------------ SwiGLU

@@ -170,8 +170,8 @@ def paged_attention_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: tor
         k, v = _gather_kv(k_cache, v_cache, block_tables[i], n)
         qi = q[s0:s1].float().permute(1, 0, 2).reshape(hkv, hq // hkv, ql, d)
         s = torch.einsum("hgqd,hnd->hgqn", qi, k.float()) * scale
-        qpos = torch.arange(n - ql, n).view(ql, 1)
-        kpos = torch.arange(n).view(1, n)
+        qpos = torch.arange(n - ql, n, device=q.device).view(ql, 1)
+        kpos = torch.arange(n, device=q.device).view(1, n)
         s = s.masked_fill(kpos > qpos, float("-inf"))
         p = torch.softmax(s, dim=-1)
         o = torch.einsum("hgqn,hnd->hgqd", p, v.float())
