@@ -1,0 +1,128 @@
+#!/usr/bin/env python
+"""Headline benchmark: output tokens/s (whole node) + p50 request latency, Llama-3-8B bf16.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...        (driver form for N > 1)
+
+One *step* = one serving round: ``batch x N`` fresh requests (synthetic prompt ids of
+``--prompt-len`` tokens) are submitted at once and the engine runs until every one of
+them has produced ``--gen-len`` new tokens (prefill + continuous-batched decode, greedy,
+EOS ignored).  W untimed rounds, then K timed rounds bracketed by a barrier +
+torch.cuda.synchronize() on every rank; the max over ranks is reported.
+
+  value       = K * batch * N * gen_len / elapsed      (output tokens/s, whole job)
+  p50 latency = median request latency (submit -> last token) over the timed rounds
+
+Parallelism: ``pp`` (default, BASELINE config 3: N workers each own a contiguous slice
+of layers; activations hop stage->stage over RCCL/xGMI with N microbatches in flight)
+or ``dp`` (N independent replicas).  Per-GPU batch is fixed, so scaling is weak.
+Weights are random-init (seeded, generated on device); prompts are synthetic ids.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "output tokens/sec (whole node) + p50 latency, Llama-3-8B across 1/2/4/8 workers"
+BASELINE_VALUE = None   # reference publishes no number; comparator measured separately
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--batch", type=int, default=64, help="sequences per GPU per round")
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--gen-len", type=int, default=128)
+    ap.add_argument("--parallelism", choices=["pp", "dp"], default="pp")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def make_prompts(n, plen, vocab, seed):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    return rng.integers(100, min(vocab, 30000), size=(n, plen)).tolist()
+
+
+def emit(args, world, elapsed, lat, extra):
+    tokens = args.steps * args.batch * world * args.gen_len
+    value = tokens / elapsed
+    rec = {
+        "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+        "dtype": "bf16", "data": "synthetic (random-init weights, random prompt ids)",
+        "p50_latency_ms": round(1000 * statistics.median(lat), 3) if lat else None,
+        "config": {"model": args.model, "global_batch": args.batch * world, "seq_len": args.prompt_len + args.gen_len,
+                   "prompt_len": args.prompt_len, "gen_len": args.gen_len,
+                   "parallelism": f"{args.parallelism}{world}"},
+    }
+    rec.update(extra)
+    line = json.dumps(rec)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(line + "\n")
+
+
+def run_single(args):
+    import torch
+    from distributed_llms_amd.config import EngineConfig
+    from distributed_llms_amd.engine.llm_engine import LLMEngine
+    from distributed_llms_amd.engine.sequence import SamplingParams
+
+    ecfg = EngineConfig(model=f"synthetic:{args.model}", max_batch=args.batch,
+                        max_prefill_tokens=max(16384, args.batch * args.prompt_len),
+                        max_seq_len=args.prompt_len + args.gen_len + 32, use_graphs=not args.no_graphs,
+                        seed=args.seed)
+    t0 = time.perf_counter()
+    eng = LLMEngine(ecfg)
+    torch.cuda.synchronize()
+    load_s = time.perf_counter() - t0
+    params = SamplingParams(max_new_tokens=args.gen_len, ignore_eos=True)
+    vocab = eng.mcfg.vocab_size
+
+    def round_(r):
+        seqs = [eng.add_request(p, params) for p in make_prompts(args.batch, args.prompt_len, vocab, r)]
+        eng.run_until_done()
+        return seqs
+
+    for r in range(args.warmup):
+        round_(10_000 + r)
+    torch.cuda.synchronize()
+    lat = []
+    t0 = time.perf_counter()
+    for r in range(args.steps):
+        seqs = round_(r)
+        lat.extend(s.latency() for s in seqs)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    assert all(len(s.output) == args.gen_len for s in seqs)
+    emit(args, 1, elapsed, lat, {"load_s": round(load_s, 1)})
+
+
+def main(argv=None):
+    args = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or args.gpus > 1:
+        from distributed_llms_amd.parallel.bench_dist import run_distributed
+        return run_distributed(args, emit, make_prompts)
+    run_single(args)
+
+
+if __name__ == "__main__":
+    main()
