@@ -18,6 +18,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("silu_mul", &dllm::silu_mul);
   m.def("argmax", &dllm::argmax);
   m.def("add_inplace", &dllm::add_inplace);
+  m.def("gemm_skinny", &dllm::gemm_skinny);
   m.def("paged_attention_decode", &dllm::paged_attention_decode);
   m.def("paged_attention_prefill", &dllm::paged_attention_prefill);
 }

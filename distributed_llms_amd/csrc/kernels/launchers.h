@@ -18,6 +18,9 @@ void silu_mul(uintptr_t out, uintptr_t gu, int tokens, int inter, uintptr_t stre
 void add_inplace(uintptr_t a, uintptr_t b, long n, uintptr_t stream);
 void argmax(uintptr_t out, uintptr_t logits, int rows, int vocab, long row_stride, uintptr_t stream);
 
+void gemm_skinny(uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t bias, int M, int N, int K, int mode,
+                 uintptr_t stream);
+
 void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
                             uintptr_t block_tables, uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml,
                             int batch, int hq, int hkv, int d, int block_size, int max_blocks, int num_splits,

@@ -32,6 +32,7 @@ class HostBatch:
     max_ctx: int
     slot: int = 0
     step_id: int = 0
+    sampling: Optional[np.ndarray] = None   # [B, 3] int32: temperature*1e4, top_k, top_p*1e4 (None = greedy)
 
     @property
     def num_tokens(self) -> int:
@@ -46,16 +47,26 @@ class HostBatch:
         """Flatten to one int32 array: [header(16) | fields...]."""
         b, t = self.num_seqs, self.num_tokens
         mb = self.block_tables.shape[1] if self.block_tables.ndim == 2 else 0
+        has_s = 1 if self.sampling is not None else 0
         hdr = np.array([1 if self.is_prefill else 0, t, b, mb, self.max_q_len, self.max_ctx, self.slot,
-                        self.step_id] + [0] * 8, dtype=np.int32)
+                        self.step_id, has_s] + [0] * 7, dtype=np.int32)
         parts = [hdr, self.ids, self.positions, self.slots, self.seq_lens, self.cu_seqlens,
                  self.block_tables.reshape(-1), self.logits_idx]
+        if has_s:
+            parts.append(self.sampling.reshape(-1))
         return np.concatenate([p.astype(np.int32, copy=False).reshape(-1) for p in parts])
+
+    def sampling_args(self) -> dict:
+        if self.sampling is None:
+            return {}
+        s = self.sampling
+        return {"temperatures": (s[:, 0] / 1e4).tolist(), "top_k": s[:, 1].tolist(),
+                "top_p": (s[:, 2] / 1e4).tolist()}
 
     @staticmethod
     def unpack(arr: np.ndarray) -> "HostBatch":
         hdr = arr[:16]
-        pf, t, b, mb, mq, mc, slot, sid = (int(x) for x in hdr[:8])
+        pf, t, b, mb, mq, mc, slot, sid, has_s = (int(x) for x in hdr[:9])
         o = 16
         def take(n):
             nonlocal o
@@ -66,7 +77,8 @@ class HostBatch:
         seq_lens, cu = take(b), take(b + 1)
         bt = take(b * mb).reshape(b, mb)
         lidx = take(b)
-        return HostBatch(bool(pf), ids, pos, slots, seq_lens, cu, bt, lidx, mq, mc, slot, sid)
+        samp = take(3 * b).reshape(b, 3) if has_s else None
+        return HostBatch(bool(pf), ids, pos, slots, seq_lens, cu, bt, lidx, mq, mc, slot, sid, samp)
 
 
 def next_pow2(x: int, lo: int = 1) -> int:
@@ -115,8 +127,12 @@ def build_host_batch(step: Step, bm, block_size: int, max_blocks: Optional[int] 
     bt = np.zeros((b, mb), dtype=np.int32)
     bm.fill_block_tables(seq_ids, bt, 0)
     max_ctx = int(seq_lens.max()) if b else 0
+    sampling = None
+    if any(s.params.temperature > 0 for s in seqs):
+        sampling = np.array([[int(round(s.params.temperature * 1e4)), int(s.params.top_k),
+                              int(round(s.params.top_p * 1e4))] for s in seqs], dtype=np.int32)
     return HostBatch(step.is_prefill, ids, positions, slots, seq_lens, cu, bt, logits_idx, max_q_len,
-                     max_ctx, step.slot, step_id)
+                     max_ctx, step.slot, step_id, sampling)
 
 
 def to_device_meta(hb: HostBatch, device, pad_ctx_to: Optional[int] = None) -> (torch.Tensor, BatchMeta):

@@ -45,6 +45,7 @@ class DecodeGraphRunner:
         self.graphs: Dict[Tuple[int, int], Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
         self.pool = None
         self.copy_done: Optional[torch.cuda.Event] = None
+        self.capture_stream: Optional[torch.cuda.Stream] = None
 
     def bucket(self, b: int, max_ctx: int) -> Tuple[int, int]:
         bb = next(x for x in self.batch_sizes if x >= b)
@@ -65,7 +66,9 @@ class DecodeGraphRunner:
     def capture(self, bb: int, cb: int):
         meta = self._meta(bb, cb)
         # warm up outside capture (allocator, lazy module init)
-        s = torch.cuda.Stream()
+        if self.capture_stream is None:
+            self.capture_stream = torch.cuda.Stream(self.dev)
+        s = self.capture_stream
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
@@ -74,7 +77,9 @@ class DecodeGraphRunner:
         g = torch.cuda.CUDAGraph()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(g, pool=self.pool):
+        # own capture stream: per-stream GEMM workspaces stay private to this runner's graphs;
+        # thread_local mode: RCCL/gloo threads of this process may keep calling HIP meanwhile
+        with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
             out = self.stage.forward(self._inp(bb), meta)
         self.graphs[(bb, cb)] = (g, out)
         return g, out

@@ -157,8 +157,7 @@ class ModelStage:
             router_logits = ops.linear(h, lw["router"])
             tw, tid = ops.moe_route(router_logits, self.cfg.experts_per_token)
             return ops.moe_mlp(h, lw["experts_gate_up"], lw["experts_down"], tw, tid)
-        gu = ops.linear(h, lw["w_gate_up"])
-        return ops.linear(ops.silu_mul(gu), lw["w_down"])
+        return ops.linear(ops.linear_swiglu(h, lw["w_gate_up"]), lw["w_down"])
 
     def _forward_llama(self, inp: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
         cfg = self.cfg

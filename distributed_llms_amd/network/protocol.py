@@ -1,0 +1,226 @@
+"""Control-plane wire protocol (master <-> worker, client <-> worker).
+
+Keeps the reference's command vocabulary and call shapes
+(``src/network/protocol.py:12-20`` MESSAGE_TYPES, ``send_message(sock, command,
+payload=None, metadata=None) -> bool``, ``receive_message(sock, timeout=60) ->
+(header, payload)``) but replaces its framing:
+
+* reference: 10 ASCII bytes of header length + ``pickle(header)`` + payload, received in
+  4 KiB chunks with ``payload += chunk`` (O(n^2), D18) and unpickled from the socket
+  (arbitrary code execution on untrusted input);
+* here: a 24-byte binary prefix (magic, version, command id, header length, payload
+  length, header CRC-32 -- encoded/validated by the native codec in ``_C_runtime``), a
+  JSON header, and the raw payload read with ``recv_into`` straight into one
+  preallocated buffer (O(n), no copies).  Nothing received is ever unpickled.
+
+``send_message``/``receive_message`` are static, so both ``MessageProtocol.send_message(sock,
+...)`` (how the reference's tests call it, D2) and instance calls work.
+"""
+from __future__ import annotations
+
+import json
+import socket
+import struct
+import threading
+import zlib
+from typing import Any, Dict, Optional, Tuple
+
+HEADER_SIZE = 24                      # fixed frame prefix (the reference's was a 10-byte length field)
+MAX_PAYLOAD = 1 << 40
+
+# Command ids are the wire encoding; names are the API (superset of the reference's).
+COMMANDS = [
+    "REGISTER", "LOAD_SHARD", "RUN_INFERENCE", "RESULT", "HEARTBEAT", "SHARD_REQUEST", "TASK_ASSIGN",
+    "SHARD_LOADED", "UNLOAD_SHARD", "SHARD_UNLOADED", "SCHEDULE_COMPUTATION", "ERROR",
+    "REGISTER_ACK", "PLAN", "STATUS", "STATUS_REPLY", "SHUTDOWN", "TOKENS", "ABORT", "PING", "PONG",
+]
+_CMD_ID = {c: i for i, c in enumerate(COMMANDS)}
+EXTENDED_ID = 0xFFFF                  # unknown command names travel in the header
+
+
+def _codec():
+    try:
+        from .. import _ext
+        return _ext.runtime()
+    except Exception:   # pragma: no cover - pure-Python fallback only when the runtime is unbuilt
+        return None
+
+
+class _PyCodec:
+    """Bit-identical pure-Python twin of csrc/runtime/frame_codec.cpp (used if unbuilt)."""
+    _fmt = struct.Struct("<IBBHIQI")
+    MAGIC = 0x4D4C4C44
+
+    def encode_frame_head(self, cid, flags, header, plen):
+        return self._fmt.pack(self.MAGIC, 1, flags, cid, len(header), plen, zlib.crc32(header)) + header
+
+    def decode_frame_prefix(self, prefix):
+        magic, ver, flags, cid, hl, pl, crc = self._fmt.unpack(prefix)
+        if magic != self.MAGIC:
+            raise ValueError("bad frame magic")
+        if ver != 1:
+            raise ValueError("unsupported frame version")
+        if hl > (16 << 20) or pl > MAX_PAYLOAD:
+            raise ValueError("frame length out of bounds")
+        return cid, flags, hl, pl, crc
+
+    def check_header_crc(self, header, crc):
+        return zlib.crc32(header) == crc
+
+
+def _get_codec():
+    c = _codec()
+    return c if c is not None else _PyCodec()
+
+
+def _recv_exact_into(sock: socket.socket, view: memoryview) -> int:
+    got = 0
+    n = len(view)
+    while got < n:
+        k = sock.recv_into(view[got:], n - got)
+        if k == 0:
+            return got
+        got += k
+    return got
+
+
+class MessageProtocol:
+    """Framed messages over a stream socket.  Instances are cheap; methods are static."""
+
+    MESSAGE_TYPES = {
+        "REGISTER": "Worker registration (capabilities: device, HBM bytes, arch)",
+        "LOAD_SHARD": "Load a model shard / layer range (by path, or file bytes as payload)",
+        "RUN_INFERENCE": "Submit a generation request (token ids payload)",
+        "RESULT": "Generated token ids for a request",
+        "HEARTBEAT": "Health check",
+        "SHARD_REQUEST": "Request a shard re-load (recovery / migration)",
+        "TASK_ASSIGN": "Assign a computation task",
+        "SHARD_LOADED": "Shard load acknowledgement",
+        "UNLOAD_SHARD": "Free a shard",
+        "SHARD_UNLOADED": "Shard unload acknowledgement",
+        "SCHEDULE_COMPUTATION": "Run a stateless forward over loaded shards",
+        "ERROR": "Error report",
+        "REGISTER_ACK": "Registration accepted (worker id, config)",
+        "STATUS": "Status query",
+        "STATUS_REPLY": "Status response",
+        "SHUTDOWN": "Stop the worker",
+        "TOKENS": "Streamed tokens for a request",
+        "ABORT": "Cancel a request",
+    }
+    _send_locks: Dict[int, threading.Lock] = {}
+    _locks_guard = threading.Lock()
+
+    def __init__(self, zmq_context=None):
+        # the reference took a pyzmq context; the transport here is plain TCP
+        self.zmq_context = zmq_context
+
+    @staticmethod
+    def _lock_for(sock) -> threading.Lock:
+        key = id(sock)
+        with MessageProtocol._locks_guard:
+            lk = MessageProtocol._send_locks.get(key)
+            if lk is None:
+                lk = MessageProtocol._send_locks[key] = threading.Lock()
+            return lk
+
+    @staticmethod
+    def encode(command: str, payload: Optional[bytes] = None, metadata: Optional[Dict[str, Any]] = None) -> bytes:
+        header = {"command": command}
+        if metadata:
+            header.update(metadata)
+        if payload is not None:
+            header["payload_size"] = len(payload)
+        hb = json.dumps(header, separators=(",", ":"), default=_json_default).encode()
+        cid = _CMD_ID.get(command, EXTENDED_ID)
+        return _get_codec().encode_frame_head(cid, 0, hb, 0 if payload is None else len(payload))
+
+    @staticmethod
+    def send_message(sock, command: str, payload: Optional[bytes] = None,
+                     metadata: Optional[Dict[str, Any]] = None) -> bool:
+        """Send one frame; thread-safe per socket (heartbeat and replies may interleave)."""
+        try:
+            head = MessageProtocol.encode(command, payload, metadata)
+            with MessageProtocol._lock_for(sock):
+                sock.sendall(head)
+                if payload is not None and len(payload):
+                    sock.sendall(payload)
+            return True
+        except socket.timeout:
+            return False
+        except (OSError, ValueError, TypeError):
+            return False
+
+    @staticmethod
+    def receive_message(sock, timeout: Optional[float] = 60) -> Tuple[Dict[str, Any], Optional[bytes]]:
+        """Receive one frame. ({}, None) on orderly close before a frame starts;
+        TimeoutError on timeout; ConnectionError on close mid-frame; ValueError on a bad frame."""
+        try:
+            sock.settimeout(timeout)
+            prefix = bytearray(HEADER_SIZE)
+            got = _recv_exact_into(sock, memoryview(prefix))
+            if got == 0:
+                return {}, None
+            if got < HEADER_SIZE:
+                raise ConnectionError("connection closed while receiving frame prefix")
+            codec = _get_codec()
+            cid, _flags, hl, pl, crc = codec.decode_frame_prefix(bytes(prefix))
+            hbuf = bytearray(hl)
+            if _recv_exact_into(sock, memoryview(hbuf)) < hl:
+                raise ConnectionError("connection closed while receiving header")
+            hbytes = bytes(hbuf)
+            if not codec.check_header_crc(hbytes, crc):
+                raise ValueError("frame header CRC mismatch")
+            header = json.loads(hbytes.decode("utf-8"))
+            if not isinstance(header, dict) or "command" not in header:
+                raise ValueError("frame header must be a JSON object with a command")
+            if cid != EXTENDED_ID and (cid >= len(COMMANDS) or COMMANDS[cid] != header["command"]):
+                raise ValueError("command id / header mismatch")
+            payload = None
+            if "payload_size" in header:
+                if int(header["payload_size"]) != pl:
+                    raise ValueError("payload_size mismatch")
+                payload = bytearray(pl)
+                if pl and _recv_exact_into(sock, memoryview(payload)) < pl:
+                    raise ConnectionError("connection closed while receiving payload")
+                payload = bytes(payload)
+            return header, payload
+        except socket.timeout:
+            raise TimeoutError("timeout while receiving message")
+
+
+def _json_default(o):
+    try:
+        import numpy as np
+        if isinstance(o, np.integer):
+            return int(o)
+        if isinstance(o, np.floating):
+            return float(o)
+        if isinstance(o, np.ndarray):
+            return o.tolist()
+    except ImportError:  # pragma: no cover
+        pass
+    raise TypeError(f"not JSON serialisable: {type(o)}")
+
+
+# -------------------------------------------------------------- payload helpers
+def pack_ids(ids) -> bytes:
+    import numpy as np
+    return np.asarray(ids, dtype=np.int32).tobytes()
+
+
+def unpack_ids(b: Optional[bytes]):
+    import numpy as np
+    if not b:
+        return []
+    return np.frombuffer(b, dtype=np.int32).tolist()
+
+
+def pack_tensors(tensors: Dict[str, "torch.Tensor"]) -> bytes:
+    """Tensors -> safetensors bytes (no pickle on the wire)."""
+    from safetensors.torch import save
+    return save({k: v.detach().contiguous().cpu() for k, v in tensors.items()})
+
+
+def unpack_tensors(b: bytes) -> Dict[str, "torch.Tensor"]:
+    from safetensors.torch import load
+    return load(b)

@@ -99,6 +99,16 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return gemm.linear(x, w, bias)
 
 
+def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
+    """silu(x @ Wg^T) * (x @ Wu^T), W = [Wg; Wu]; fused into the GEMM epilogue on the GPU (decode)."""
+    if _gpu(x):
+        from . import gemm
+        y = gemm.linear_swiglu(x, w_gate_up)
+        if y is not None:
+            return y
+    return silu_mul(linear(x, w_gate_up))
+
+
 def add_(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a <- a + b (in place)."""
     if not _gpu(a):
@@ -151,7 +161,7 @@ def rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, n
 
 # ---------------------------------------------------------- K6 / K7
 def decode_split_plan(batch: int, num_kv_heads: int, max_ctx: int, block_size: int = 32,
-                      target_wgs: int = 1024) -> Tuple[int, int]:
+                      target_wgs: int = 512) -> Tuple[int, int]:
     """(num_splits, split_len) for the decode kernel.
 
     Enough workgroups to fill 256 CUs several times over, each split a multiple of

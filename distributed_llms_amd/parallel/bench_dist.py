@@ -1,0 +1,70 @@
+"""Multi-rank body of bench.py (torchrun, one process per GPU)."""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..config import EngineConfig
+from ..engine.sequence import SamplingParams
+from .dist_engine import RankRole, agree_max, init_distributed
+
+
+def _sync(ctx):
+    if torch.cuda.is_available() and ctx.device != "cpu":
+        torch.cuda.synchronize()
+    dist.barrier(group=ctx.ctrl_group)
+
+
+def run_distributed(args, emit, make_prompts):
+    pp = None if args.parallelism == "pp" else 1
+    ctx = init_distributed(pp=pp)
+    world = ctx.world
+    ecfg = EngineConfig(model=f"synthetic:{args.model}", max_batch=args.batch,
+                        max_prefill_tokens=max(16384, args.batch * args.prompt_len),
+                        max_seq_len=args.prompt_len + args.gen_len + 32, use_graphs=not args.no_graphs,
+                        num_workers=ctx.pp, seed=args.seed)
+    t0 = time.perf_counter()
+    role = RankRole(ctx, ecfg)
+    _sync(ctx)
+    load_s = time.perf_counter() - t0
+    params = SamplingParams(max_new_tokens=args.gen_len, ignore_eos=True)
+    vocab = ecfg.model_config().vocab_size
+    # requests per pipeline per round: batch x pp (each of the pp microbatch slots holds `batch`)
+    per_pipe = args.batch * ctx.pp
+
+    def one_round(r):
+        seqs = []
+        if role.is_driver:
+            prompts = make_prompts(per_pipe, args.prompt_len, vocab, r * 1000 + ctx.pipeline_id)
+            seqs = [role.add_request(p, params) for p in prompts]
+        role.run_round()
+        return seqs
+
+    for r in range(args.warmup):
+        one_round(10_000 + r)
+    _sync(ctx)
+    lat = []
+    t0 = time.perf_counter()
+    for r in range(args.steps):
+        seqs = one_round(r)
+        lat.extend(s.latency() for s in seqs)
+    _sync(ctx)
+    elapsed = agree_max(ctx, time.perf_counter() - t0)
+    if role.is_driver:
+        assert all(len(s.output) == args.gen_len for s in seqs), "incomplete generations"
+    # gather latencies to rank 0
+    obj = [None] * world
+    dist.all_gather_object(obj, lat, group=ctx.ctrl_group)
+    all_lat = [x for part in obj for x in part]
+    if ctx.rank == 0:
+        extra = {"load_s": round(load_s, 1), "stage_ranges": role.plan.to_json()["ranges"],
+                 "backend": dist.get_backend()}
+        if role.driver is not None:
+            extra["driver_stall_s"] = round(role.driver.stall_s, 3)
+        emit(args, world, elapsed, all_lat, extra)
+    role.shutdown()
+    _sync(ctx)
+    dist.destroy_process_group()

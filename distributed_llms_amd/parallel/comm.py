@@ -97,7 +97,9 @@ class DistTransport(Transport):
 
     # ---- data plane (RCCL on GPU, gloo on CPU)
     def send_hidden(self, t: torch.Tensor):
-        t = t.contiguous()
+        # copy: `t` may be a graph's static output that the next replay overwrites while the
+        # send (on the comm stream) is still reading it
+        t = t.clone(memory_format=torch.contiguous_format)
         w = dist.isend(t, self.next, group=self.data)
         self._pending.append((w, t))
         self._reap()

@@ -1,0 +1,137 @@
+"""One process per GPU: bootstrap torch.distributed and build this rank's pipeline role.
+
+World layout: ``world = dp * pp``; ranks ``[p*pp, (p+1)*pp)`` form pipeline ``p`` and
+rank ``p*pp + s`` runs stage ``s``.  Backend "nccl" is RCCL on ROCm (activations over
+xGMI); a gloo group carries the small CPU control messages (batch metadata, tokens).
+"""
+from __future__ import annotations
+
+import datetime
+import logging
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..config import EngineConfig
+from ..engine.llm_engine import LLMEngine, build_stage, make_block_manager
+from ..engine.runner import StageRunner, plan_kv_blocks
+from .comm import DistTransport
+from .pipeline import PipelineDriver, stage_worker_loop
+from .planner import plan_stages
+
+log = logging.getLogger("dllm.dist")
+
+
+@dataclass
+class DistContext:
+    rank: int
+    world: int
+    local_rank: int
+    dp: int
+    pp: int
+    ctrl_group: object
+    device: str
+
+    @property
+    def pipeline_id(self) -> int:
+        return self.rank // self.pp
+
+    @property
+    def stage(self) -> int:
+        return self.rank % self.pp
+
+    @property
+    def pipeline_ranks(self):
+        p = self.pipeline_id
+        return list(range(p * self.pp, (p + 1) * self.pp))
+
+
+def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
+                     timeout_s: float = 1800) -> DistContext:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if use_gpu:
+        torch.cuda.set_device(local_rank)
+    backend = backend or ("nccl" if use_gpu else "gloo")
+    if not dist.is_initialized():
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local_rank)
+        dist.init_process_group(**kw)
+    ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s)) if backend != "gloo" \
+        else dist.group.WORLD
+    pp = pp or world
+    if world % pp:
+        raise ValueError(f"world {world} not divisible by pp {pp}")
+    return DistContext(rank, world, local_rank, world // pp, pp, ctrl,
+                       f"cuda:{local_rank}" if use_gpu else "cpu")
+
+
+def agree_min(ctx: DistContext, value: int) -> int:
+    t = torch.tensor([value], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctx.ctrl_group)
+    return int(t.item())
+
+
+def agree_max(ctx: DistContext, value: float) -> float:
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctx.ctrl_group)
+    return float(t.item())
+
+
+class RankRole:
+    """What this rank runs: a full engine (pp == 1), a pipeline driver (stage 0), or a follower."""
+
+    def __init__(self, ctx: DistContext, ecfg: EngineConfig, hf_state=None):
+        self.ctx = ctx
+        self.ecfg = ecfg
+        mcfg = ecfg.model_config()
+        self.plan = plan_stages(mcfg, ctx.pp)
+        a, b = self.plan.ranges[ctx.stage]
+        stage = build_stage(ecfg, a, b, device=ctx.device, shard_state=hf_state)
+        nb = plan_kv_blocks(mcfg, b - a, ecfg, stage.device)
+        nb = agree_min(ctx, nb)        # every stage of a pipeline must hold the same block ids
+        self.engine = None
+        self.driver = None
+        self.runner = None
+        if ctx.pp == 1:
+            ecfg1 = ecfg.apply_overrides(num_kv_blocks=nb)
+            self.engine = LLMEngine(ecfg1, stage)
+        else:
+            self.runner = StageRunner(stage, ecfg, num_blocks=nb)
+            self.transport = DistTransport(ctx.pipeline_ranks, ctx.stage, ctrl_group=ctx.ctrl_group)
+            if ctx.stage == 0:
+                bm = make_block_manager(nb, ecfg.kv_block_size)
+                self.driver = PipelineDriver(self.runner, self.transport, ecfg, bm)
+        log.info("rank %d: pipeline %d stage %d layers [%d,%d) kv_blocks=%d", ctx.rank, ctx.pipeline_id,
+                 ctx.stage, a, b, nb)
+
+    @property
+    def is_driver(self) -> bool:
+        return self.engine is not None or self.driver is not None
+
+    def add_request(self, prompt, params):
+        return (self.engine or self.driver).add_request(prompt, params)
+
+    def run_round(self):
+        """Drivers: run all queued requests to completion, then release followers.
+        Followers: serve microbatches until the driver's ROUND_END."""
+        if self.engine is not None:
+            return self.engine.run_until_done()
+        if self.driver is not None:
+            done = self.driver.run_until_done()
+            self.driver.end_round()
+            return done
+        stage_worker_loop(self.runner, self.transport, stop_on_round_end=True)
+        return []
+
+    def shutdown(self):
+        if self.driver is not None:
+            self.driver.shutdown()
+        elif self.runner is not None:
+            stage_worker_loop(self.runner, self.transport, stop_on_round_end=False)

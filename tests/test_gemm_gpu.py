@@ -1,0 +1,61 @@
+"""Skinny-M MFMA GEMM (decode) vs a plain fp32 PyTorch GEMM of the same operands."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_llms_amd import ops
+from distributed_llms_amd.ops import gemm
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(*s, scale=1.0):
+    return (torch.randn(*s, device="cuda") * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("m", [1, 5, 32, 33, 64])
+@pytest.mark.parametrize("n,k", [(6144, 4096), (4096, 4096), (4096, 14336), (128, 768), (2304, 768)])
+def test_skinny_linear(cuda, m, n, k):
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear(x, w, force_skinny=True)
+    ref = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+def test_skinny_bias(cuda):
+    x, w, b = _bf(9, 768), _bf(2304, 768, scale=0.05), _bf(2304)
+    y = gemm.linear(x, w, b, force_skinny=True)
+    ref = x.float() @ w.float().t() + b.float()
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [1, 16, 64])
+@pytest.mark.parametrize("inter,k", [(14336, 4096), (512, 256), (1024, 512)])
+def test_skinny_swiglu(cuda, m, inter, k):
+    x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
+    y = gemm.linear_swiglu(x, w, force_skinny=True)
+    gu = x.float() @ w.float().t()
+    ref = F.silu(gu[:, :inter]) * gu[:, inter:]
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+def test_large_m_uses_library_gemm(cuda):
+    x, w = _bf(300, 512), _bf(256, 512, scale=0.05)
+    y = ops.linear(x, w)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
+def test_skinny_graph_replay(cuda):
+    x, w = _bf(64, 4096), _bf(4096, 4096, scale=0.05)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gemm.linear(x, w, force_skinny=True)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        y = gemm.linear(x, w, force_skinny=True)
+    for _ in range(3):
+        x.copy_(_bf(64, 4096))
+        g.replay()
+        torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
