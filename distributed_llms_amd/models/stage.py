@@ -99,6 +99,8 @@ class ModelStage:
                        for l in range(self.layer_start, self.layer_end)]
         if self.needs_embed():
             self.embed = W.synth_embed(cfg, seed, self.dtype, self.device)
+            if not self.is_first:
+                self.embed.pop("pos_embed", None)
         if self.is_last:
             self.head = W.synth_head(cfg, seed, self.dtype, self.device)
         return self
@@ -110,7 +112,10 @@ class ModelStage:
         self.layers = [{k: conv(v) for k, v in W.hf_to_block(cfg, l, sd).items()}
                        for l in range(self.layer_start, self.layer_end)]
         if self.needs_embed():
-            self.embed = {k: conv(sd[n]) for k, n in W.hf_embed_names(cfg).items()}
+            names = W.hf_embed_names(cfg)
+            if not self.is_first:           # tied LM head on the last stage: token table only
+                names = {"embed": names["embed"]}
+            self.embed = {k: conv(sd[n]) for k, n in names.items()}
         if self.is_last:
             self.head = {k: conv(sd[n]) for k, n in W.hf_head_names(cfg).items()}
         return self

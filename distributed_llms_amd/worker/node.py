@@ -1,0 +1,554 @@
+"""Worker node: owns one pipeline stage (a contiguous layer slice resident in HBM).
+
+Reference: ``src/worker/node.py`` (``WorkerNode`` with a raw-TCP server, a pyzmq REQ link to
+the master that never worked (D3-D6), heartbeat every 5 s, ``ModelShard`` whose ``compute``
+was a placeholder matmul (D22)).  Same public surface here, working end to end:
+
+* master link: plain TCP + the framed protocol; REGISTER (device, HBM bytes, arch, peers)
+  -> REGISTER_ACK (worker id); reconnect with exponential backoff (not recursion);
+  one send lock per socket so heartbeats and replies never interleave mid-frame (D6);
+* LOAD_SHARD from the master carries the stage plan: layer range, model spec / shard path,
+  torch.distributed rendezvous (rank, world, addr, port).  The worker builds its
+  ModelStage, joins the RCCL (GPU) / gloo (CPU) group, sizes its paged KV pool and acks
+  SHARD_LOADED.  Stage 0 then runs the request scheduler (PipelineDriver / LLMEngine) and
+  answers RUN_INFERENCE with RESULT; other stages serve microbatches;
+* the reference's peer server path (client -> worker raw TCP: LOAD_SHARD with shard bytes,
+  RUN_INFERENCE / SCHEDULE_COMPUTATION with tensors) is kept, with safetensors payloads
+  instead of pickle (D9/D10/D24);
+* fault injection for tests: ``fail_after_steps`` kills the process after N engine steps.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import socket
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..config import EngineConfig, ModelConfig, get_model_config, resolve_device, torch_dtype
+from ..models import weights as W
+from ..models.stage import BatchMeta, KVCache, ModelStage
+from ..network.protocol import MessageProtocol, pack_ids, pack_tensors, unpack_ids, unpack_tensors
+
+log = logging.getLogger("dllm.worker")
+
+
+# ============================================================== ModelShard
+class ModelShard:
+    """A loaded shard: HF-named parameters of a contiguous block range (+ embed / head).
+
+    ``compute`` is a real stateless forward over the shard's layers (prefill of the given
+    tokens with a private scratch KV cache): ``{"input_ids": [T] or [B,T]}`` (first shard) or
+    ``{"hidden_states": [T,H] / [B,T,H]}`` in; ``{"hidden_states"}`` or, for the shard holding
+    the LM head, ``{"logits": [..., V]}`` out.  Chaining ``compute`` over all shards in order
+    equals a full-model forward.
+    """
+
+    def __init__(self, shard_id: int, parameters: Dict[str, torch.Tensor], config: Optional[ModelConfig] = None,
+                 layer_range=None, device: Optional[str] = None, dtype=None):
+        self.shard_id = shard_id
+        self.parameters = parameters
+        self.config = config
+        self.device = resolve_device(device or "auto")
+        self.dtype = dtype
+        self._stage: Optional[ModelStage] = None
+        if layer_range is None and config is not None:
+            layers = sorted({W.layer_of(k) for k in parameters if W.layer_of(k) is not None})
+            layer_range = (layers[0], layers[-1] + 1) if layers else None
+        self.layer_range = tuple(layer_range) if layer_range else None
+
+    def to_device(self):
+        for key in self.parameters:
+            self.parameters[key] = self.parameters[key].to(self.device)
+        self._stage = None
+        return self
+
+    @property
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.parameters.values())
+
+    def stage(self) -> ModelStage:
+        if self._stage is None:
+            if self.config is None or self.layer_range is None:
+                raise ValueError("ModelShard needs a ModelConfig and a layer range to compute")
+            dt = self.dtype or (torch.bfloat16 if str(self.device).startswith("cuda") else torch.float32)
+            st = ModelStage(self.config, self.layer_range[0], self.layer_range[1], device=self.device, dtype=dt)
+            self._stage = st.load_hf_state(self.parameters)
+        return self._stage
+
+    @torch.inference_mode()
+    def compute(self, inputs: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        st = self.stage()
+        if st.is_first:
+            x = inputs["input_ids"]
+            batched = x.dim() == 2
+            b, t = (x.shape if batched else (1, x.shape[0]))
+            inp = x.reshape(-1).to(st.device, torch.int32)
+        else:
+            x = inputs["hidden_states"]
+            batched = x.dim() == 3
+            b, t = (x.shape[0], x.shape[1]) if batched else (1, x.shape[0])
+            inp = x.reshape(b * t, -1).to(st.device, st.dtype)
+        bs = 32
+        nb = -(-t // bs)
+        st.allocate_kv(b * nb + 1, bs)
+        dev = st.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        pos = torch.arange(t, **i32).repeat(b)
+        bt = (torch.arange(b * nb, **i32).view(b, nb) + 1)
+        slots = (bt[:, :, None] * bs + torch.arange(bs, **i32)).view(b, -1)[:, :t].reshape(-1)
+        meta = BatchMeta(is_prefill=True, positions=pos, slot_mapping=slots, block_tables=bt,
+                         seq_lens=torch.full((b,), t, **i32), cu_seqlens_q=torch.arange(0, b * t + 1, t, **i32),
+                         logits_idx=torch.arange(b * t, dtype=torch.int64, device=dev), max_q_len=t, max_ctx=t,
+                         num_seqs=b, num_tokens=b * t)
+        out = st.forward(inp, meta)
+        st.kv = None
+        key = "logits" if st.is_last else "hidden_states"
+        out = out.view(b, t, -1) if batched else out
+        return {key: out}
+
+
+# ============================================================== WorkerNode
+class WorkerNode:
+    def __init__(self, host: str = "0.0.0.0", port: int = 65433, master_address: Optional[str] = None,
+                 device: Optional[str] = None, heartbeat_interval: float = 5.0, fail_after_steps: int = 0,
+                 serve_peers: bool = True):
+        self.host = host
+        self.port = port
+        self.master_address = master_address
+        self.device = resolve_device(device or os.environ.get("DLLM_DEVICE", "auto"))
+        self.heartbeat_interval = heartbeat_interval
+        self.fail_after_steps = fail_after_steps
+        self.serve_peers = serve_peers
+        self.shards: Dict[int, ModelShard] = {}
+        self.running = False
+        self.server_socket: Optional[socket.socket] = None
+        self.master_socket: Optional[socket.socket] = None
+        self.worker_id: Optional[str] = None
+        self.proto = MessageProtocol()
+        self._lock = threading.RLock()
+        self._threads: List[threading.Thread] = []
+        # pipeline role (set by a master LOAD_SHARD plan)
+        self.role = None                   # "driver" | "engine" | "follower"
+        self.stage_runner = None
+        self.driver = None
+        self.engine = None
+        self.plan: Dict[str, Any] = {}
+        self._req_cv = threading.Condition()
+        self._pending: List[tuple] = []
+        self._serve_thread: Optional[threading.Thread] = None
+        self._dist_ctx = None
+        self._steps = 0
+        self._stopped = threading.Event()
+
+    # ------------------------------------------------------------ lifecycle
+    def capabilities(self) -> Dict[str, Any]:
+        cap = {"device": self.device, "has_gpu": self.device.startswith("cuda"), "pid": os.getpid(),
+               "host": socket.gethostname(), "port": self.port}
+        if cap["has_gpu"]:
+            idx = torch.device(self.device).index or 0
+            props = torch.cuda.get_device_properties(idx)
+            cap.update(memory=int(props.total_memory), gpu_name=props.name,
+                       gfx_arch=getattr(props, "gcnArchName", ""), cu_count=props.multi_processor_count,
+                       device_index=idx)
+        else:
+            cap.update(memory=0)
+        return cap
+
+    def start(self, block: bool = True):
+        self.running = True
+        if self.serve_peers:
+            self._bind_server()
+            self._spawn(self._accept_connections)
+        if self.master_address:
+            self._connect_to_master()
+            self._spawn(self._send_heartbeat)
+        if block:
+            try:
+                while self.running and not self._stopped.wait(0.5):
+                    pass
+            except KeyboardInterrupt:
+                pass
+            finally:
+                self.stop()
+
+    def _spawn(self, fn, *args):
+        th = threading.Thread(target=fn, args=args, daemon=True)
+        th.start()
+        self._threads.append(th)
+        return th
+
+    def _bind_server(self):
+        self.server_socket = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        self.server_socket.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        last = None
+        for _ in range(16):    # reference: port+1 retry up to 5 times (src/worker/node.py:52-65)
+            try:
+                self.server_socket.bind((self.host, self.port))
+                break
+            except OSError as e:
+                last = e
+                self.port += 1
+        else:
+            raise RuntimeError(f"could not bind a worker port: {last}")
+        self.server_socket.listen(16)
+        self.port = self.server_socket.getsockname()[1]
+        log.info("worker listening on %s:%d", self.host, self.port)
+
+    def stop(self):
+        if not self.running and self._stopped.is_set():
+            return
+        self.running = False
+        self._stopped.set()
+        self._teardown_pipeline(send_stop=True)
+        for s in (self.server_socket, self.master_socket):
+            try:
+                if s:
+                    s.close()
+            except OSError:
+                pass
+
+    # ------------------------------------------------------------ master link
+    def _connect_to_master(self, max_wait: float = 300.0):
+        host, port = self.master_address.rsplit(":", 1)
+        delay, t0 = 0.2, time.time()
+        while self.running:
+            try:
+                s = socket.create_connection((host, int(port)), timeout=10)
+                s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                self.master_socket = s
+                if not self.proto.send_message(s, "REGISTER", metadata={"capabilities": self.capabilities()}):
+                    raise ConnectionError("REGISTER send failed")
+                hdr, _ = self.proto.receive_message(s, timeout=30)
+                if hdr.get("command") != "REGISTER_ACK":
+                    raise ConnectionError(f"unexpected reply {hdr}")
+                self.worker_id = hdr["worker_id"]
+                self.heartbeat_interval = float(hdr.get("heartbeat_interval", self.heartbeat_interval))
+                self._spawn(self._handle_master)
+                log.info("registered with master %s as %s", self.master_address, self.worker_id)
+                return
+            except (OSError, ConnectionError, TimeoutError, ValueError) as e:
+                if time.time() - t0 > max_wait:
+                    raise RuntimeError(f"cannot reach master {self.master_address}: {e}")
+                time.sleep(delay)
+                delay = min(delay * 2, 5.0)      # exponential backoff (plan.md:430-436)
+
+    def _send_heartbeat(self):
+        while self.running:
+            s = self.master_socket
+            if s is not None:
+                meta = {"timestamp": time.time(), "steps": self._steps}
+                if self.driver is not None:
+                    meta["running"] = self.driver.scheduler.num_running()
+                    meta["waiting"] = len(self.driver.scheduler.waiting)
+                self.proto.send_message(s, "HEARTBEAT", metadata=meta)
+            if self._stopped.wait(self.heartbeat_interval):
+                return
+
+    def _handle_master(self):
+        s = self.master_socket
+        try:
+            while self.running:
+                try:
+                    header, payload = self.proto.receive_message(s, timeout=None)
+                except TimeoutError:
+                    continue
+                if not header:
+                    break
+                self._handle_command(s, header.get("command", ""), header, payload)
+        except (OSError, ConnectionError, ValueError) as e:
+            if self.running:
+                log.warning("master link lost: %s", e)
+        finally:
+            if self.running:
+                # the master is gone: a worker without a control plane cannot serve
+                log.error("master connection closed; stopping worker")
+                self.stop()
+
+    # ------------------------------------------------------------ peer server (reference path)
+    def _accept_connections(self):
+        while self.running:
+            try:
+                c, addr = self.server_socket.accept()
+            except OSError:
+                break
+            self._spawn(self._handle_client, c, addr)
+
+    def _handle_client(self, c, addr):
+        try:
+            while self.running:
+                try:
+                    header, payload = self.proto.receive_message(c, timeout=None)
+                except TimeoutError:
+                    continue
+                if not header:
+                    break
+                self._handle_command(c, header.get("command", ""), header, payload)
+        except (OSError, ConnectionError, ValueError) as e:
+            log.debug("client %s: %s", addr, e)
+        finally:
+            try:
+                c.close()
+            except OSError:
+                pass
+
+    # ------------------------------------------------------------ command dispatch
+    def _handle_command(self, sock, command: str, header: Dict[str, Any], payload: Optional[bytes]):
+        try:
+            if command == "LOAD_SHARD":
+                if "plan" in header:
+                    info = self._load_plan(header["plan"], payload)
+                    self.proto.send_message(sock, "SHARD_LOADED", metadata=info)
+                else:
+                    sid = int(header["shard_id"])
+                    ok = self.load_shard(sid, payload, config=header.get("config"),
+                                         layer_range=header.get("layer_range"))
+                    self.proto.send_message(sock, "SHARD_LOADED" if ok else "ERROR",
+                                            metadata={"shard_id": sid, "ok": ok})
+            elif command == "UNLOAD_SHARD":
+                if header.get("pipeline"):
+                    self._teardown_pipeline(send_stop=True)
+                sid = header.get("shard_id")
+                if sid is not None:
+                    self.unload_shard(int(sid))
+                self.proto.send_message(sock, "SHARD_UNLOADED", metadata={"shard_id": sid})
+            elif command == "RUN_INFERENCE":
+                if self.role in ("driver", "engine"):
+                    self._enqueue_request(sock, header, payload)
+                else:
+                    self._run_stateless(sock, header, payload)
+            elif command == "SCHEDULE_COMPUTATION":
+                self._run_stateless(sock, header, payload)
+            elif command == "ABORT":
+                self._abort(header.get("task_id"))
+            elif command == "STATUS":
+                self.proto.send_message(sock, "STATUS_REPLY", metadata={"status": self.status(),
+                                                                        "req": header.get("req")})
+            elif command == "PING":
+                self.proto.send_message(sock, "PONG", metadata={"t": time.time()})
+            elif command == "SHUTDOWN":
+                self.proto.send_message(sock, "SHARD_UNLOADED", metadata={"shutdown": True})
+                self._stopped.set()
+                self.running = False
+            else:
+                self.proto.send_message(sock, "ERROR", metadata={"error": f"unknown command {command}"})
+        except Exception as e:   # report, never kill the connection thread silently
+            log.exception("command %s failed", command)
+            self.proto.send_message(sock, "ERROR", metadata={"error": repr(e), "failed_command": command,
+                                                             "task_id": header.get("task_id")})
+
+    # ------------------------------------------------------------ in-process shard API
+    def load_shard(self, shard_id: int, shard_data, config=None, layer_range=None) -> bool:
+        """Load a shard from bytes (safetensors or torch.save zip), a path, or a dict of tensors."""
+        from ..checkpoint.shard_manager import load_shard_bytes, load_shard_file
+        try:
+            if isinstance(shard_data, dict):
+                params = shard_data
+            elif isinstance(shard_data, (bytes, bytearray)):
+                params = load_shard_bytes(bytes(shard_data))
+            elif isinstance(shard_data, str):
+                params = load_shard_file(shard_data)
+            else:
+                raise TypeError(f"unsupported shard data {type(shard_data)}")
+            cfg = None
+            if isinstance(config, dict):
+                cfg = ModelConfig.from_hf_config(config)
+            elif isinstance(config, ModelConfig):
+                cfg = config
+            elif isinstance(config, str):
+                cfg = get_model_config(config)
+            shard = ModelShard(shard_id, params, cfg, layer_range, device=self.device)
+            shard.to_device()
+            with self._lock:
+                self.shards[shard_id] = shard
+            return True
+        except Exception as e:
+            log.error("error loading shard %s: %s", shard_id, e)
+            return False
+
+    def unload_shard(self, shard_id: int) -> bool:
+        with self._lock:
+            return self.shards.pop(shard_id, None) is not None
+
+    def schedule_computation(self, inputs: Dict[str, torch.Tensor], shard_ids: List[int]) -> Dict[str, torch.Tensor]:
+        """Chain ``compute`` over the given shards in order (missing shard -> KeyError)."""
+        out = dict(inputs)
+        for sid in shard_ids:
+            with self._lock:
+                shard = self.shards[sid]
+            out = shard.compute(out)
+        return out
+
+    def _run_stateless(self, sock, header, payload):
+        inputs = unpack_tensors(payload) if payload else {}
+        res = self.schedule_computation(inputs, [int(s) for s in header.get("shard_ids", [])])
+        self.proto.send_message(sock, "RESULT", payload=pack_tensors(res), metadata={"task_id": header.get("task_id")})
+
+    # ------------------------------------------------------------ pipeline role
+    def _load_plan(self, plan: Dict[str, Any], payload: Optional[bytes]) -> Dict[str, Any]:
+        from ..checkpoint.shard_manager import load_shard_bytes, load_shard_file
+        from ..engine.llm_engine import LLMEngine, build_stage, make_block_manager
+        from ..engine.runner import StageRunner, plan_kv_blocks
+        from ..parallel.comm import DistTransport
+        from ..parallel.pipeline import PipelineDriver, stage_worker_loop
+
+        self._teardown_pipeline(send_stop=False)
+        ecfg = EngineConfig.from_dict(plan["engine_config"])
+        stage_idx, world = int(plan["stage"]), int(plan["num_stages"])
+        a, b = plan["layer_range"]
+        t0 = time.time()
+        state = None
+        if payload:
+            state = load_shard_bytes(payload)
+        elif plan.get("shard_path"):
+            state = load_shard_file(plan["shard_path"])
+        if state is not None and ecfg.model_config().arch == "gpt2":
+            state.pop("lm_head.weight", None)
+        stage = build_stage(ecfg, a, b, device=self.device, shard_state=state)
+        del state
+        ctx = None
+        if world > 1:
+            ctx = self._init_dist(plan["dist"], stage_idx, world)
+        nb = plan_kv_blocks(stage.cfg, b - a, ecfg, stage.device)
+        if ctx is not None:
+            from ..parallel.dist_engine import agree_min
+            nb = agree_min(ctx, nb)
+        self.plan = plan
+        if world == 1:
+            self.engine = LLMEngine(ecfg.apply_overrides(num_kv_blocks=nb), stage)
+            self.role = "engine"
+            self._serve_thread = self._spawn(self._serve_loop)
+        else:
+            self.stage_runner = StageRunner(stage, ecfg, num_blocks=nb)
+            transport = DistTransport(list(range(world)), stage_idx, ctrl_group=ctx.ctrl_group)
+            if stage_idx == 0:
+                bm = make_block_manager(nb, ecfg.kv_block_size)
+                self.driver = PipelineDriver(self.stage_runner, transport, ecfg, bm)
+                self.role = "driver"
+                self._serve_thread = self._spawn(self._serve_loop)
+            else:
+                self.role = "follower"
+                self._follower_transport = transport
+                self._serve_thread = self._spawn(self._follower_loop, stage_worker_loop, transport)
+        self._instrument(self.engine.runner if self.engine is not None else self.stage_runner)
+        return {"shard_id": int(plan.get("shard_id", stage_idx)), "stage": stage_idx, "layer_range": [a, b],
+                "weight_bytes": stage.weight_bytes(), "kv_blocks": nb, "load_s": round(time.time() - t0, 3),
+                "role": self.role}
+
+    def _instrument(self, runner):
+        """Count executed microbatches (heartbeat load report) and inject a crash if asked to."""
+        inner = runner.execute
+
+        def execute(hb, hidden=None):
+            self._steps += 1
+            if self.fail_after_steps and self._steps > self.fail_after_steps:
+                log.error("fault injection: worker exiting after %d steps", self._steps - 1)
+                os._exit(17)
+            return inner(hb, hidden)
+
+        runner.execute = execute
+
+    def _init_dist(self, d: Dict[str, Any], rank: int, world: int):
+        from ..parallel.dist_engine import init_distributed
+        os.environ.update(MASTER_ADDR=str(d["master_addr"]), MASTER_PORT=str(d["master_port"]), RANK=str(rank),
+                          WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(torch.device(self.device).index or 0) if self.device.startswith("cuda")
+                          else str(rank))
+        backend = "gloo" if not self.device.startswith("cuda") else None
+        self._dist_ctx = init_distributed(pp=world, backend=backend)
+        return self._dist_ctx
+
+    def _follower_loop(self, loop_fn, transport):
+        try:
+            loop_fn(self.stage_runner, transport, stop_on_round_end=False)
+        except Exception as e:  # pragma: no cover
+            if self.running:
+                log.exception("stage loop failed: %s", e)
+
+    def _enqueue_request(self, sock, header, payload):
+        from ..engine.sequence import SamplingParams
+        ids = unpack_ids(payload) if payload else list(header.get("input_ids", []))
+        params = SamplingParams.from_dict(header.get("params"))
+        with self._req_cv:
+            self._pending.append((sock, header.get("task_id"), ids, params))
+            self._req_cv.notify()
+
+    def _abort(self, task_id):
+        target = self.driver or self.engine
+        if target is None or task_id is None:
+            return
+        sch = target.scheduler
+        for s in list(sch.waiting) + [x for r in sch.running for x in r]:
+            if s.request_id == task_id:
+                sch.abort(s.seq_id)
+
+    def _serve_loop(self):
+        """Stage 0: admit requests, step the pipeline, return finished sequences as RESULT."""
+        target = self.driver or self.engine
+        owners: Dict[str, Any] = {}
+        last_activity = time.time()
+        keepalive_s = 60.0     # idle pipelines ping their followers so gloo/RCCL receives never time out
+        while self.running and target is (self.driver or self.engine):
+            with self._req_cv:
+                while self.running and not self._pending and not target.has_work():
+                    self._req_cv.wait(timeout=0.5)
+                    if self.driver is not None and time.time() - last_activity > keepalive_s:
+                        self.driver.end_round()
+                        last_activity = time.time()
+                batch, self._pending = self._pending, []
+            last_activity = time.time()
+            for sock, task_id, ids, params in batch:
+                seq = target.add_request(ids, params, request_id=task_id)
+                owners[task_id] = sock
+            if not target.has_work():
+                continue
+            done = target.poll() if self.driver is not None else target.step()
+            for s in done:
+                sock = owners.pop(s.request_id, None)
+                if sock is None:
+                    continue
+                meta = {"task_id": s.request_id, "finish_reason": s.finish_reason, "num_tokens": len(s.output),
+                        "ttft_s": s.ttft(), "latency_s": s.latency(), "prompt_tokens": len(s.prompt)}
+                self.proto.send_message(sock, "RESULT", payload=pack_ids(s.output), metadata=meta)
+
+    def _teardown_pipeline(self, send_stop: bool):
+        if self.driver is not None and send_stop:
+            try:
+                self.driver.shutdown()
+            except Exception:
+                pass
+        th = self._serve_thread
+        self.driver = self.engine = None
+        self.role = None
+        if th is not None and th is not threading.current_thread():
+            with self._req_cv:
+                self._req_cv.notify_all()
+            th.join(timeout=5)
+        self._serve_thread = None
+        self.stage_runner = None
+        if self._dist_ctx is not None:
+            try:
+                import torch.distributed as dist
+                if dist.is_initialized():
+                    dist.destroy_process_group()
+            except Exception:
+                pass
+            self._dist_ctx = None
+
+    def status(self) -> Dict[str, Any]:
+        st = {"worker_id": self.worker_id, "role": self.role, "device": self.device, "steps": self._steps,
+              "shards": sorted(self.shards), "plan": {k: v for k, v in self.plan.items() if k != "engine_config"}}
+        if self.device.startswith("cuda"):
+            free, total = torch.cuda.mem_get_info(torch.device(self.device))
+            st["hbm_used_bytes"] = int(total - free)
+            st["hbm_total_bytes"] = int(total)
+        t = self.driver or self.engine
+        if t is not None:
+            st["running"] = t.scheduler.num_running()
+            st["waiting"] = len(t.scheduler.waiting)
+            st["kv_free_blocks"] = t.bm.num_free()
+        return st

@@ -1,0 +1,122 @@
+"""Master + workers over localhost sockets on CPU (BASELINE config 1 plumbing), with real
+``run_worker.py`` processes: registration, contiguous stage plan, torch.distributed (gloo)
+pipeline, request routing, heartbeat eviction and recovery."""
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from distributed_llms_amd.config import EngineConfig
+from distributed_llms_amd.engine.llm_engine import LLMEngine
+from distributed_llms_amd.engine.sequence import SamplingParams
+from distributed_llms_amd.master.node import MasterNode, WorkerFailure
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROMPTS = [[3, 5, 7, 9, 11], [20, 21, 22], [100, 4, 4, 4, 4, 4, 4, 4, 9]]
+
+pytestmark = pytest.mark.slow
+
+
+def _cfg(model):
+    return EngineConfig(model=model, dtype="float32", device="cpu", max_batch=8, max_seq_len=128,
+                        use_graphs=False, num_kv_blocks=128, heartbeat_interval=0.5, heartbeat_timeout=4.0)
+
+
+def _spawn_worker(port, extra=()):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    return subprocess.Popen([sys.executable, os.path.join(ROOT, "run_worker.py"), "--master", f"127.0.0.1:{port}",
+                             "--device", "cpu", "--port", "0", "--heartbeat", "0.5", "--log-level", "WARNING",
+                             *extra], env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+
+
+@pytest.fixture
+def cluster():
+    procs = []
+    masters = []
+
+    def make(model, n, auto_recover=False, extra=None):
+        m = MasterNode("127.0.0.1", 0, _cfg(model), auto_recover=auto_recover).start()
+        masters.append(m)
+        m.initialize_model(model, num_shards=n)
+        for i in range(n):
+            procs.append(_spawn_worker(m.port, (extra or {}).get(i, ())))
+        m.wait_for_workers(n, timeout=120)
+        return m
+
+    yield make, procs
+    for m in masters:
+        m.stop()
+    for p in procs:
+        try:
+            p.wait(timeout=15)
+        except subprocess.TimeoutExpired:
+            p.kill()
+
+
+@pytest.mark.parametrize("model", ["synthetic:tiny-gpt2", "synthetic:tiny-llama"])
+def test_two_worker_pipeline_matches_single_process(cluster, model):
+    make, _ = cluster
+    m = make(model, 2)
+    assert m.assign_shards() == {"w0": [0], "w1": [1]}
+    acks = m.distribute_shards(timeout=300)
+    assert [acks[w]["layer_range"] for w in ("w0", "w1")] == [[0, 2], [2, 4]]
+    res = m.generate(PROMPTS, max_new_tokens=6, ignore_eos=True, timeout=120)
+    ref = LLMEngine(_cfg(model)).generate(PROMPTS, SamplingParams(max_new_tokens=6, ignore_eos=True))
+    assert [r["tokens"] for r in res] == ref
+    text = m.run_inference("hello", max_new_tokens=4, timeout=60, ignore_eos=True)
+    assert len(text["tokens"]) == 4 and isinstance(text["text"], str)
+    st = m.status()
+    assert st["state"] == "ready" and st["metrics"]["requests"] == 4
+    assert {w["remote"]["role"] for w in st["workers"].values()} == {"driver", "follower"}
+
+
+def test_single_worker_engine(cluster):
+    make, _ = cluster
+    m = make("synthetic:tiny-llama", 1)
+    m.assign_shards()
+    m.distribute_shards(timeout=300)
+    res = m.generate(PROMPTS, max_new_tokens=5, ignore_eos=True, timeout=120)
+    ref = LLMEngine(_cfg("synthetic:tiny-llama")).generate(PROMPTS, SamplingParams(max_new_tokens=5, ignore_eos=True))
+    assert [r["tokens"] for r in res] == ref
+
+
+def test_worker_failure_eviction_and_recovery(cluster):
+    make, procs = cluster
+    # stage-0 worker dies after 3 engine steps (fault injection)
+    m = make("synthetic:tiny-llama", 2, auto_recover=True, extra={0: ("--fail-after", "3")})
+    m.assign_shards()
+    m.distribute_shards(timeout=300)
+    with pytest.raises((WorkerFailure, RuntimeError, TimeoutError)):
+        m.generate(PROMPTS, max_new_tokens=50, ignore_eos=True, timeout=60)
+    t0 = time.time()
+    while m.state != "degraded" and time.time() - t0 < 30:
+        time.sleep(0.2)
+    assert m.state == "degraded"
+    assert m.running                                    # the master survives
+    procs.append(_spawn_worker(m.port))                 # a replacement worker joins
+    t0 = time.time()
+    while m.state != "ready" and time.time() - t0 < 120:
+        time.sleep(0.5)
+    assert m.state == "ready"
+    res = m.generate(PROMPTS[:2], max_new_tokens=4, ignore_eos=True, timeout=120)
+    ref = LLMEngine(_cfg("synthetic:tiny-llama")).generate(PROMPTS[:2], SamplingParams(max_new_tokens=4, ignore_eos=True))
+    assert [r["tokens"] for r in res] == ref
+
+
+def test_checkpoint_shards_distributed_by_path(cluster, tmp_path):
+    from distributed_llms_amd.checkpoint.shard_manager import write_synthetic_checkpoint
+    d = write_synthetic_checkpoint("tiny-gpt2", str(tmp_path / "ckpt"), seed=7)
+    make, _ = cluster
+    m = make(d, 2)
+    m.assign_shards()
+    m.distribute_shards(timeout=300)
+    res = m.generate(PROMPTS, max_new_tokens=5, ignore_eos=True, timeout=120)
+    from distributed_llms_amd.checkpoint.shard_manager import iter_checkpoint
+    from distributed_llms_amd.models.stage import ModelStage
+    from distributed_llms_amd.config import get_model_config
+    cfg = get_model_config(d)
+    st = ModelStage(cfg, 0, cfg.num_layers, "cpu", __import__("torch").float32).load_hf_state(dict(iter_checkpoint(d)))
+    ref = LLMEngine(_cfg(d), st).generate(PROMPTS, SamplingParams(max_new_tokens=5, ignore_eos=True))
+    assert [r["tokens"] for r in res] == ref
