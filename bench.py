@@ -41,7 +41,7 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--batch", type=int, default=64, help="sequences per GPU per round")
+    ap.add_argument("--batch", type=int, default=256, help="sequences per GPU per round")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--parallelism", choices=["pp", "dp"], default="pp")

@@ -17,42 +17,13 @@
 //  * waves combine their partial tiles with LDS float atomics (ds_add_f32) into one
 //    [M_pad x BN] f32 tile; the epilogue writes bf16 (+bias), or SwiGLU: the workgroup's two
 //    column tiles are the gate rows n and the up rows I+n of the fused [2I, K] weight.
-#include "common.h"
+#include "skinny_common.h"
 #include "launchers.h"
 
 namespace dllm {
 
-constexpr int kSkWaves = 8;
 constexpr int EPI_STORE = 0;
 constexpr int EPI_SWIGLU = 1;
-
-template <int MT, int NT>
-__device__ __forceinline__ void sk_load(bf16x8 (&xa)[MT][4], bf16x8 (&wb)[NT][4], const bf16* const (&xrow)[MT],
-                                        const bf16* const (&wrow)[NT], int k) {
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const bf16x8* p = reinterpret_cast<const bf16x8*>(wrow[nt] + k);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) wb[nt][i] = __builtin_nontemporal_load(p + i);
-  }
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const bf16x8* p = reinterpret_cast<const bf16x8*>(xrow[mt] + k);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xa[mt][i] = p[i];
-  }
-}
-
-template <int MT, int NT>
-__device__ __forceinline__ void sk_mma(f32x4 (&acc)[MT][NT], const bf16x8 (&xa)[MT][4], const bf16x8 (&wb)[NT][4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[mt][i], wb[nt][i], acc[mt][nt], 0, 0, 0);
-}
 
 template <int MT, int NT, int EPI>
 __global__ void __launch_bounds__(512, 1) gemm_skinny_kernel(bf16* __restrict__ y, const bf16* __restrict__ x,
@@ -82,30 +53,9 @@ __global__ void __launch_bounds__(512, 1) gemm_skinny_kernel(bf16* __restrict__ 
   const int g0 = wv * per, g1 = min(ngroups, g0 + per);
 
   f32x4 acc[MT][NT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (g0 < g1) {
-    bf16x8 xa0[MT][4], wb0[NT][4], xa1[MT][4], wb1[NT][4];
-    int gg = g0;
-    sk_load<MT, NT>(xa0, wb0, xrow, wrow, gg * 128);
-    for (; gg + 1 < g1; gg += 2) {
-      sk_load<MT, NT>(xa1, wb1, xrow, wrow, (gg + 1) * 128);
-      sk_mma<MT, NT>(acc, xa0, wb0);
-      if (gg + 2 < g1) sk_load<MT, NT>(xa0, wb0, xrow, wrow, (gg + 2) * 128);
-      sk_mma<MT, NT>(acc, xa1, wb1);
-    }
-    if (gg < g1) sk_mma<MT, NT>(acc, xa0, wb0);
-  }
+  sk_mainloop<MT, NT>(acc, xrow, wrow, g0, g1);
   __syncthreads();   // LDS zero-fill visible
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(&red[(mt * 16 + 4 * g + i) * BN + nt * 16 + r], acc[mt][nt][i]);
+  sk_reduce_lds<MT, NT>(red, acc, lane);
   __syncthreads();
 
   if (EPI == EPI_SWIGLU) {

@@ -21,6 +21,13 @@ void argmax(uintptr_t out, uintptr_t logits, int rows, int vocab, long row_strid
 void gemm_skinny(uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t bias, int M, int N, int K, int mode,
                  uintptr_t stream);
 
+void moe_route(uintptr_t logits, int T, int E, int k, uintptr_t topk_w, uintptr_t topk_ids, uintptr_t counts,
+               uintptr_t offsets, uintptr_t sorted_tok, uintptr_t inv, uintptr_t stream);
+void moe_grouped_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets,
+                      int E, int N, int K, int mode, uintptr_t stream);
+void moe_combine(uintptr_t out, uintptr_t ysorted, uintptr_t topk_w, uintptr_t inv, int T, int H, int k,
+                 uintptr_t stream);
+
 void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
                             uintptr_t block_tables, uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml,
                             int batch, int hq, int hkv, int d, int block_size, int max_blocks, int num_splits,

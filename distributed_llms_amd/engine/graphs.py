@@ -8,6 +8,7 @@ so they never touch a live sequence.
 """
 from __future__ import annotations
 
+import threading
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -17,6 +18,7 @@ from ..models.stage import BatchMeta, ModelStage
 from .batch import HostBatch, next_pow2
 
 SCRATCH_SEQ_ID = -1      # owns block 0 in the BlockManager
+_CAPTURE_LOCK = threading.Lock()   # one graph capture at a time per process
 
 
 class DecodeGraphRunner:
@@ -64,6 +66,10 @@ class DecodeGraphRunner:
         return self.ids[:bb] if self.stage.is_first else self.hidden[:bb]
 
     def capture(self, bb: int, cb: int):
+        with _CAPTURE_LOCK:
+            return self._capture(bb, cb)
+
+    def _capture(self, bb: int, cb: int):
         meta = self._meta(bb, cb)
         # warm up outside capture (allocator, lazy module init)
         if self.capture_stream is None:

@@ -159,9 +159,8 @@ class ModelStage:
 
     def _mlp(self, h: torch.Tensor, lw: Dict[str, torch.Tensor]) -> torch.Tensor:
         if self.cfg.is_moe:
-            router_logits = ops.linear(h, lw["router"])
-            tw, tid = ops.moe_route(router_logits, self.cfg.experts_per_token)
-            return ops.moe_mlp(h, lw["experts_gate_up"], lw["experts_down"], tw, tid)
+            return ops.moe_forward(h, lw["router"], lw["experts_gate_up"], lw["experts_down"],
+                                   self.cfg.experts_per_token)
         return ops.linear(ops.linear_swiglu(h, lw["w_gate_up"]), lw["w_down"])
 
     def _forward_llama(self, inp: torch.Tensor, meta: BatchMeta) -> torch.Tensor:

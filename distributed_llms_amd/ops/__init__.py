@@ -256,3 +256,9 @@ def moe_route(router_logits: torch.Tensor, top_k: int):
 def moe_mlp(x, w_gate_up, w_down, topk_w, topk_ids):
     from . import moe
     return moe.mlp(x, w_gate_up, w_down, topk_w, topk_ids)
+
+
+def moe_forward(x, w_router, w_gate_up, w_down, top_k: int):
+    """Full Mixtral sparse MLP: route + expert SwiGLU MLPs + weighted combine."""
+    from . import moe
+    return moe.forward(x, w_router, w_gate_up, w_down, top_k)

@@ -1,9 +1,23 @@
-"""Mixtral MoE: router (K11) and expert MLPs (K12)."""
+"""Mixtral MoE: router (K11) and expert MLPs (K12).
+
+GPU path (bf16):
+  router logits  = linear(x, W_router)                                   [T, E]
+  moe_route      : softmax -> top-k -> renormalise, expert-sorted slots    (HIP, one launch)
+  decode-sized T : grouped weight-streaming GEMMs on the sorted slots (gate|up + SwiGLU, then down)
+                   entirely on device -- no host sync, so the decode step stays graph-capturable
+  prefill-sized T: per-expert library GEMMs over the gathered rows (needs the counts on the host)
+  moe_combine    : weighted sum of each token's top-k expert outputs        (HIP)
+CPU path: the PyTorch reference (ops/reference.py).
+"""
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 
+from .. import _ext
 from . import reference as ref
+
+GROUPED_MAX_TOKENS = 256      # beyond this the per-expert row count makes library GEMMs cheaper
 
 
 def route(router_logits: torch.Tensor, top_k: int):
@@ -12,3 +26,45 @@ def route(router_logits: torch.Tensor, top_k: int):
 
 def mlp(x, w_gate_up, w_down, topk_w, topk_ids):
     return ref.moe_mlp(x, w_gate_up, w_down, topk_w, topk_ids)
+
+
+def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor,
+            top_k: int) -> torch.Tensor:
+    if not x.is_cuda:
+        tw, tid = ref.moe_route(ref.linear(x, w_router), top_k)
+        return ref.moe_mlp(x, w_gate_up, w_down, tw, tid)
+    from . import linear, silu_mul
+    k = _ext.kernels()
+    st = torch.cuda.current_stream().cuda_stream
+    t, h = x.shape
+    e, two_i, _ = w_gate_up.shape
+    inter = two_i // 2
+    if not (x.is_contiguous() and w_gate_up.is_contiguous() and w_down.is_contiguous()):
+        raise ValueError("moe: operands must be contiguous")
+    logits = linear(x, w_router)
+    dev = x.device
+    topk_w = torch.empty(t, top_k, dtype=torch.float32, device=dev)
+    topk_ids = torch.empty(t, top_k, dtype=torch.int32, device=dev)
+    counts = torch.empty(e, dtype=torch.int32, device=dev)
+    offsets = torch.empty(e + 1, dtype=torch.int32, device=dev)
+    sorted_tok = torch.empty(t * top_k, dtype=torch.int32, device=dev)
+    inv = torch.empty(t * top_k, dtype=torch.int32, device=dev)
+    k.moe_route(logits.data_ptr(), t, e, top_k, topk_w.data_ptr(), topk_ids.data_ptr(), counts.data_ptr(),
+                offsets.data_ptr(), sorted_tok.data_ptr(), inv.data_ptr(), st)
+    ys = torch.empty(t * top_k, h, dtype=x.dtype, device=dev)
+    if t <= GROUPED_MAX_TOKENS:
+        act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
+        k.moe_grouped_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
+                           counts.data_ptr(), offsets.data_ptr(), e, two_i, h, 1, st)
+        k.moe_grouped_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), counts.data_ptr(),
+                           offsets.data_ptr(), e, h, inter, 0, st)
+    else:
+        xs = x.index_select(0, sorted_tok.long())
+        off = offsets.cpu().tolist()          # prefill only: eager, host sync is fine here
+        for ex in range(e):
+            a, b = off[ex], off[ex + 1]
+            if b > a:
+                ys[a:b] = F.linear(silu_mul(F.linear(xs[a:b], w_gate_up[ex])), w_down[ex])
+    out = torch.empty_like(x)
+    k.moe_combine(out.data_ptr(), ys.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), t, h, top_k, st)
+    return out

@@ -153,7 +153,11 @@ class LoopbackTransport(Transport):
     def recv_hidden(self, rows, hidden, dtype, device):
         t, ev = self.hub.hidden[self.stage].get()
         if ev is not None:
-            torch.cuda.current_stream().wait_event(ev)
+            cur = torch.cuda.current_stream()
+            cur.wait_event(ev)
+            # the producer thread drops its reference: without this the caching allocator may
+            # hand the block to the producer's stream again while this stream still reads it
+            t.record_stream(cur)
         assert t.shape == (rows, hidden), (t.shape, rows, hidden)
         return t
 

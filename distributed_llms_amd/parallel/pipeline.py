@@ -174,6 +174,10 @@ def run_loopback_pipeline(ecfg: EngineConfig, num_stages: int, prompts, params: 
         stage = build_stage(ecfg, a, b, device=device, shard_state=hf_state)
         runners.append(StageRunner(stage, ecfg, num_blocks=ecfg.num_kv_blocks or 512))
     errors = []
+    # capture every stage's decode graphs up front, one at a time: concurrent captures from
+    # several threads of one process are not something to rely on
+    for r in runners:
+        r.warmup_graphs(ctx_buckets=(min(256, ecfg.max_seq_len),))
 
     def follower(s):
         try:
@@ -194,6 +198,10 @@ def run_loopback_pipeline(ecfg: EngineConfig, num_stages: int, prompts, params: 
     drv = PipelineDriver(runners[0], hub.transport(0), ecfg, bm)
     try:
         outs = drv.generate(prompts, params)
+    except RuntimeError as e:
+        if errors:
+            raise errors[0] from e
+        raise
     finally:
         drv.shutdown()
         for th in threads:

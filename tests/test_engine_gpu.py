@@ -26,7 +26,7 @@ def _engines(name, graphs=True, max_batch=8):
     return e_cpu, e_gpu
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama-d128", "tiny-gpt2"])
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama-d128", "tiny-gpt2", "tiny-mixtral"])
 def test_prefill_logits_gpu_vs_cpu(cuda, name):
     e_cpu, e_gpu = _engines(name, graphs=False)
     prompts = [[1, 5, 9, 200, 37, 44, 45, 46, 47, 48], [3, 4], list(range(10, 80))]
@@ -40,9 +40,10 @@ def test_prefill_logits_gpu_vs_cpu(cuda, name):
     torch.testing.assert_close(outs[1], outs[0], atol=5e-2, rtol=5e-2)
 
 
-def test_graph_decode_matches_eager(cuda):
-    _, e_eager = _engines("tiny-llama", graphs=False)
-    _, e_graph = _engines("tiny-llama", graphs=True)
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
+def test_graph_decode_matches_eager(cuda, name):
+    _, e_eager = _engines(name, graphs=False)
+    _, e_graph = _engines(name, graphs=True)
     prompts = [[1, 5, 9, 200], [3, 4, 7], list(range(10, 70)), [8] * 33, [9, 9, 9]]
     p = SamplingParams(max_new_tokens=24, ignore_eos=True)
     a = e_eager.generate(prompts, p)
