@@ -7,6 +7,7 @@ scheduler and stage executor split across processes.
 """
 from __future__ import annotations
 
+import collections
 import logging
 import time
 from typing import Iterable, List, Optional
@@ -56,12 +57,25 @@ class LLMEngine:
         if not (self.stage.is_first and self.stage.is_last):
             raise ValueError("LLMEngine needs a stage owning every layer")
         self.mcfg = self.stage.cfg
-        self.runner = StageRunner(self.stage, ecfg)
+        gpu = self.stage.device.type == "cuda"
+        self.num_slots = max(1, ecfg.streams) if gpu else 1
+        self.runner = StageRunner(self.stage, ecfg, num_slots=self.num_slots)
         self.bm = make_block_manager(self.runner.num_blocks, ecfg.kv_block_size)
-        self.scheduler = Scheduler(self.bm, 1, ecfg.max_batch, ecfg.max_prefill_tokens, ecfg.max_seq_len)
+        # max_batch is the engine's total decode batch, split evenly over the slots
+        per_slot = -(-ecfg.max_batch // self.num_slots)
+        self.scheduler = Scheduler(self.bm, self.num_slots, per_slot, ecfg.max_prefill_tokens, ecfg.max_seq_len)
         self.step_id = 0
         self.num_prefill_tokens = 0
         self.num_decode_tokens = 0
+        # async slots: each has its own stream, pinned token buffer and completion event
+        self.inflight = collections.deque()
+        self.busy = [False] * self.num_slots
+        if gpu:
+            dev = self.stage.device
+            self.streams = [torch.cuda.Stream(dev) for _ in range(self.num_slots)]
+            self.tok_host = [torch.empty(max(ecfg.max_batch, 1), dtype=torch.int32).pin_memory()
+                             for _ in range(self.num_slots)]
+            self.events = [torch.cuda.Event() for _ in range(self.num_slots)]
 
     # ------------------------------------------------------------ requests
     def add_request(self, prompt: List[int], params: Optional[SamplingParams] = None,
@@ -72,28 +86,65 @@ class LLMEngine:
         return seq
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work()
+        return self.scheduler.has_work() or bool(self.inflight)
 
     # ------------------------------------------------------------ stepping
-    def execute_step(self, step: Step) -> List[int]:
+    def _host_batch(self, step: Step):
         hb = build_host_batch(step, self.bm, self.ecfg.kv_block_size,
                               None if step.is_prefill else self.runner.max_blocks, self.step_id)
         self.step_id += 1
-        logits = self.runner.execute(hb)
-        ids = sample(logits, **step_sampling_args(step.seqs))
         if step.is_prefill:
             self.num_prefill_tokens += hb.num_tokens
         else:
             self.num_decode_tokens += hb.num_tokens
+        return hb
+
+    def execute_step(self, step: Step) -> List[int]:
+        """Synchronous execution of one step (CPU path / tests)."""
+        hb = self._host_batch(step)
+        logits = self.runner.execute(hb, slot=step.slot)
+        ids = sample(logits, **step_sampling_args(step.seqs))
         return ids.cpu().tolist()
 
+    def _issue(self, slot: int) -> bool:
+        step = self.scheduler.schedule(slot)
+        if step is None:
+            return False
+        hb = self._host_batch(step)
+        s = self.streams[slot]
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            logits = self.runner.execute(hb, slot=slot)
+            ids = sample(logits, **step_sampling_args(step.seqs))
+            n = ids.shape[0]
+            self.tok_host[slot][:n].copy_(ids, non_blocking=True)
+            self.events[slot].record(s)
+        self.inflight.append((step, slot, n))
+        self.busy[slot] = True
+        return True
+
+    def _complete_oldest(self):
+        step, slot, n = self.inflight.popleft()
+        self.events[slot].synchronize()
+        self.scheduler.complete(step, self.tok_host[slot][:n].tolist(), time.perf_counter())
+        self.busy[slot] = False
+
     def step(self) -> List[Sequence]:
-        """One scheduler iteration; returns sequences that finished in it."""
-        st = self.scheduler.schedule(0)
-        if st is None:
+        """One pass over the microbatch slots; returns sequences that finished."""
+        if self.stage.device.type != "cuda":
+            st = self.scheduler.schedule(0)
+            if st is not None:
+                toks = self.execute_step(st)
+                self.scheduler.complete(st, toks, time.perf_counter())
             return self.scheduler.pop_finished()
-        toks = self.execute_step(st)
-        self.scheduler.complete(st, toks, time.perf_counter())
+        issued = False
+        for slot in range(self.num_slots):
+            while self.busy[slot]:
+                self._complete_oldest()
+            if self._issue(slot):
+                issued = True
+        if not issued and self.inflight:
+            self._complete_oldest()
         return self.scheduler.pop_finished()
 
     def run_until_done(self) -> List[Sequence]:

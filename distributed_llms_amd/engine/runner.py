@@ -39,7 +39,11 @@ def plan_kv_blocks(mcfg: ModelConfig, num_layers: int, ecfg: EngineConfig, devic
 
 
 class StageRunner:
-    def __init__(self, stage: ModelStage, ecfg: EngineConfig, num_blocks: Optional[int] = None):
+    """``num_slots`` > 1 gives every microbatch slot its own decode-graph set (static buffers,
+    graph pool, attention workspace), so slots can be replayed concurrently on separate streams."""
+
+    def __init__(self, stage: ModelStage, ecfg: EngineConfig, num_blocks: Optional[int] = None,
+                 num_slots: int = 1):
         self.stage = stage
         self.ecfg = ecfg
         self.block_size = ecfg.kv_block_size
@@ -47,29 +51,34 @@ class StageRunner:
         stage.allocate_kv(nb, self.block_size)
         self.num_blocks = nb
         self.max_blocks = -(-ecfg.max_seq_len // self.block_size)
-        self.graphs: Optional[DecodeGraphRunner] = None
+        self.graph_sets = []
         if ecfg.use_graphs and stage.device.type == "cuda":
             sizes = [b for b in ecfg.graph_batch_sizes if b <= ecfg.max_batch] or [ecfg.max_batch]
             if max(sizes) < ecfg.max_batch:
                 sizes.append(ecfg.max_batch)
-            self.graphs = DecodeGraphRunner(stage, ecfg.max_batch, self.max_blocks, sizes)
+            self.graph_sets = [DecodeGraphRunner(stage, ecfg.max_batch, self.max_blocks, sizes)
+                               for _ in range(max(1, num_slots))]
         log.info("stage [%d,%d) kv blocks=%d (%.1f GiB) weights=%.2f GiB", stage.layer_start, stage.layer_end,
                  nb, stage.kv.nbytes / 2**30, stage.weight_bytes() / 2**30)
 
+    @property
+    def graphs(self) -> Optional[DecodeGraphRunner]:
+        return self.graph_sets[0] if self.graph_sets else None
+
     @torch.inference_mode()
-    def execute(self, hb: HostBatch, hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def execute(self, hb: HostBatch, hidden: Optional[torch.Tensor] = None, slot: int = 0) -> torch.Tensor:
         st = self.stage
-        if (not hb.is_prefill) and self.graphs is not None and self.graphs.can_run(hb.num_seqs, hb.max_ctx):
-            return self.graphs.run(hb, hidden)
+        gr = self.graph_sets[slot % len(self.graph_sets)] if self.graph_sets else None
+        if (not hb.is_prefill) and gr is not None and gr.can_run(hb.num_seqs, hb.max_ctx):
+            return gr.run(hb, hidden)
         ids, meta = to_device_meta(hb, st.device)
         return st.forward(ids if st.is_first else hidden, meta)
 
     def warmup_graphs(self, batch_sizes=None, ctx_buckets=(256,)):
         """Pre-capture decode graphs (keeps capture cost out of timed regions)."""
-        if self.graphs is None:
-            return
-        for b in (batch_sizes or self.graphs.batch_sizes):
-            for c in ctx_buckets:
-                bb, cb = self.graphs.bucket(b, c)
-                if (bb, cb) not in self.graphs.graphs:
-                    self.graphs.capture(bb, cb)
+        for gr in self.graph_sets:
+            for b in (batch_sizes or gr.batch_sizes):
+                for c in ctx_buckets:
+                    bb, cb = gr.bucket(b, c)
+                    if (bb, cb) not in gr.graphs:
+                        gr.capture(bb, cb)

@@ -443,12 +443,12 @@ class WorkerNode:
         """Count executed microbatches (heartbeat load report) and inject a crash if asked to."""
         inner = runner.execute
 
-        def execute(hb, hidden=None):
+        def execute(hb, hidden=None, slot=0):
             self._steps += 1
             if self.fail_after_steps and self._steps > self.fail_after_steps:
                 log.error("fault injection: worker exiting after %d steps", self._steps - 1)
                 os._exit(17)
-            return inner(hb, hidden)
+            return inner(hb, hidden, slot)
 
         runner.execute = execute
 
