@@ -46,6 +46,7 @@ def parse(argv=None):
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--parallelism", choices=["pp", "dp"], default="pp")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--streams", type=int, default=1, help="1-GPU engine: microbatch slots on separate streams")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
@@ -88,7 +89,7 @@ def run_single(args):
     ecfg = EngineConfig(model=f"synthetic:{args.model}", max_batch=args.batch,
                         max_prefill_tokens=max(16384, args.batch * args.prompt_len),
                         max_seq_len=args.prompt_len + args.gen_len + 32, use_graphs=not args.no_graphs,
-                        seed=args.seed)
+                        seed=args.seed, streams=args.streams)
     t0 = time.perf_counter()
     eng = LLMEngine(ecfg)
     torch.cuda.synchronize()

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--m", type=int, nargs="+", default=[1, 16, 64])
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
+    ap.add_argument("--tiled", action="store_true", help="compare the split-K tiled kernel instead")
     a = ap.parse_args()
     # a scratch buffer larger than the 256 MiB Infinity Cache to flush it between calls
     flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
@@ -50,7 +51,10 @@ def main():
         w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
         for m in a.m:
             x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
-            if sw:
+            if a.tiled:
+                ours = lambda: (flush.zero_(), gemm.linear_tiled(x, w, swiglu=sw))
+                blas = (lambda: (flush.zero_(), ops.silu_mul(F.linear(x, w)))) if sw else (lambda: (flush.zero_(), F.linear(x, w)))
+            elif sw:
                 ours = lambda: (flush.zero_(), gemm.linear_swiglu(x, w, force_skinny=True))
                 blas = lambda: (flush.zero_(), ops.silu_mul(F.linear(x, w)))
             else:

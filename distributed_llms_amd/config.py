@@ -225,7 +225,10 @@ class EngineConfig:
     num_workers: int = 1               # pipeline stages (one process / GPU each)
     dp_replicas: int = 1               # data-parallel replica groups (dp x pp = world)
     microbatches: int = 0              # 0 -> = number of stages
-    streams: int = 2                   # single-GPU engine: microbatch slots interleaved on HIP streams
+    # single-GPU engine: microbatch slots interleaved on HIP streams.  1 by default: decode GEMMs
+    # are weight-streaming, and two half-batches stream every weight twice (measured 16.2k vs
+    # 21.0k tok/s at batch 256, profiles/dual_stream.txt)
+    streams: int = 1
     max_batch: int = 256               # max sequences decoded per step (per replica)
     max_prefill_tokens: int = 16384    # max prompt tokens per prefill step
     max_seq_len: int = 4096

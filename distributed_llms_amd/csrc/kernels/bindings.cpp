@@ -19,6 +19,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("argmax", &dllm::argmax);
   m.def("add_inplace", &dllm::add_inplace);
   m.def("gemm_skinny", &dllm::gemm_skinny);
+  m.def("gemm_tiled", &dllm::gemm_tiled);
   m.def("moe_route", &dllm::moe_route);
   m.def("moe_grouped_gemm", &dllm::moe_grouped_gemm);
   m.def("moe_combine", &dllm::moe_combine);

@@ -1,0 +1,182 @@
+// Large-batch decode GEMM (M = 64..512): C[M,N] = A[M,K] . B[N,K]^T, bf16 in, f32 accumulate.
+//
+// Why: at these M hipBLASLt's tiles leave most of the 256 CUs idle for N <= 6144
+// (qkv / o / down run at 1.1-2 TB/s and 0.3-0.5 PF, bench/blas_graph_probe.py).  This kernel
+// splits K across workgroups so (N/128) x (M/128) x S fills the chip, and reduces the S f32
+// partial slabs in a second, fully parallel pass (optionally with the SwiGLU epilogue).
+//
+// Structure (the guide's minimum 2-phase LDS pipeline, gfx950):
+//  * tile 128 x 128 x 64, 256 threads = 4 waves in 2 x 2, wave tile 64 x 64 = 4 x 4
+//    v_mfma_f32_16x16x32_bf16 accumulators (64 VGPRs);
+//  * global -> LDS with global_load_lds_dwordx4 (16 B per lane, lane-linear 1 KiB per
+//    wave-instruction = 8 rows x 128 B); the bank-conflict swizzle (16-B chunk c of row r
+//    stored at c ^ ((r >> 1) & 7)) is applied on the per-lane SOURCE address and on the
+//    ds_read address (guide rule 21), which makes the 16-lane ds_read_b128 groups
+//    conflict-free;
+//  * double-buffered LDS (64 KiB): stage tile t+1 before the MFMAs of tile t, one
+//    vmcnt(0) + barrier per K-tile.
+#include "common.h"
+#include "launchers.h"
+
+namespace dllm {
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* glb_vptr;
+
+constexpr int TBM = 128, TBN = 128, TBK = 64;
+constexpr int TILE_ELEMS = TBM * TBK;   // 8192 bf16 = 16 KiB
+
+__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <bool SPLIT>
+__global__ void __launch_bounds__(256, 2) gemm_tiled_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                            bf16* __restrict__ C, float* __restrict__ P, int M, int N,
+                                                            int K, int k_per_split) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE_ELEMS];   // [buf][A|B][128][64]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int n0 = blockIdx.x * TBN, m0 = blockIdx.y * TBM, split = blockIdx.z;
+  const int kb = split * k_per_split;
+  const int ke = min(K, kb + k_per_split);
+  const int nt = max(0, (ke - kb) / TBK);
+
+  // staging addresses (per lane): instruction i = wv*4 + j covers tile rows 8i .. 8i+7
+  const bf16* srcA[4];
+  const bf16* srcB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = wv * 4 + j;
+    const int r = 8 * i + (lane >> 3);
+    const int c = swz_chunk(r, lane & 7);
+    srcA[j] = A + (size_t)min(m0 + r, M - 1) * K + c * 8;
+    srcB[j] = B + (size_t)(n0 + r) * K + c * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = wv * 4 + j;
+      __builtin_amdgcn_global_load_lds((glb_vptr)(srcA[j] + k0), (lds_vptr)(smem + (buf * 2 + 0) * TILE_ELEMS + i * 512),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_vptr)(srcB[j] + k0), (lds_vptr)(smem + (buf * 2 + 1) * TILE_ELEMS + i * 512),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  if (nt > 0) {
+    stage(0, kb);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const int cur = t & 1;
+      if (t + 1 < nt) stage(cur ^ 1, kb + (t + 1) * TBK);
+      const bf16* sa = smem + (cur * 2 + 0) * TILE_ELEMS;
+      const bf16* sb = smem + (cur * 2 + 1) * TILE_ELEMS;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 fa[4], fb[4];
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+          const int row = wm * 64 + rt * 16 + fr;
+          fa[rt] = *reinterpret_cast<const bf16x8*>(sa + row * TBK + swz_chunk(row, 4 * s + fq) * 8);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const int row = wn * 64 + ct * 16 + fr;
+          fb[ct] = *reinterpret_cast<const bf16x8*>(sb + row * TBK + swz_chunk(row, 4 * s + fq) * 8);
+        }
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct)
+            acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt], fb[ct], acc[rt][ct], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // epilogue: lane holds col (lane&15), rows 4*(lane>>4)+i of each 16x16 tile
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + rt * 16 + 4 * fq + i;
+      if (m >= M) continue;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int n = n0 + wn * 64 + ct * 16 + fr;
+        if (SPLIT) P[((size_t)split * M + m) * N + n] = acc[rt][ct][i];
+        else C[(size_t)m * N + n] = f2bf(acc[rt][ct][i]);
+      }
+    }
+  }
+}
+
+// out[m, n] = sum_s P[s, m, n] (+ bias[n]);  swiglu: out[m, j] = silu(sum P[m, j]) * sum P[m, I + j]
+template <bool SWIGLU>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16* __restrict__ out, const float* __restrict__ P,
+                                                            const bf16* __restrict__ bias, int S, int M, int N) {
+  const int ncols = SWIGLU ? N / 2 : N;
+  const long total = (long)M * ncols / 4;
+  const size_t slab = (size_t)M * N;
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
+    const long e = v * 4;
+    const int m = (int)(e / ncols), c = (int)(e % ncols);
+    f32x4 a = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      a += *reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + c);
+      if (SWIGLU) u += *reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + ncols + c);
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float x = a[j];
+      if (SWIGLU) x = silu_f(x) * u[j];
+      else if (bias) x += bf2f(bias[c + j]);
+      o[j] = f2bf(x);
+    }
+    *reinterpret_cast<bf16x4*>(out + (size_t)m * ncols + c) = o;
+  }
+}
+
+// mode 0: C[M,N] = A B^T (+bias);  mode 1 (SwiGLU): C[M, N/2] = silu(A Bg^T) * (A Bu^T), B = [Bg; Bu]
+void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t ws, long ws_floats, int M, int N,
+                int K, int splits, int mode, uintptr_t stream) {
+  DLLM_HOST_CHECK(M >= 1, "M >= 1");
+  DLLM_HOST_CHECK(N % TBN == 0, "N must be a multiple of 128");
+  DLLM_HOST_CHECK(K % TBK == 0, "K must be a multiple of 64");
+  DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int kps = (K / TBK + splits - 1) / splits * TBK;
+  const int S = (K + kps - 1) / kps;
+  dim3 grid(N / TBN, (M + TBM - 1) / TBM, S);
+  if (S == 1 && mode == 0 && bias == 0) {
+    hipLaunchKernelGGL(gemm_tiled_kernel<false>, grid, dim3(256), 0, s, (const bf16*)a, (const bf16*)b, (bf16*)c,
+                       (float*)nullptr, M, N, K, kps);
+    DLLM_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
+  hipLaunchKernelGGL(gemm_tiled_kernel<true>, grid, dim3(256), 0, s, (const bf16*)a, (const bf16*)b, (bf16*)nullptr,
+                     (float*)ws, M, N, K, kps);
+  DLLM_HIP_CHECK(hipGetLastError());
+  const int ncols = mode == 1 ? N / 2 : N;
+  long blocks = ((long)M * ncols / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (mode == 1)
+    hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, (bf16*)c,
+                       (const float*)ws, (const bf16*)nullptr, S, M, N);
+  else
+    hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, (bf16*)c,
+                       (const float*)ws, (const bf16*)bias, S, M, N);
+  DLLM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dllm

@@ -21,6 +21,9 @@ void argmax(uintptr_t out, uintptr_t logits, int rows, int vocab, long row_strid
 void gemm_skinny(uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t bias, int M, int N, int K, int mode,
                  uintptr_t stream);
 
+void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t ws, long ws_floats, int M, int N,
+                int K, int splits, int mode, uintptr_t stream);
+
 void moe_route(uintptr_t logits, int T, int E, int k, uintptr_t topk_w, uintptr_t topk_ids, uintptr_t counts,
                uintptr_t offsets, uintptr_t sorted_tok, uintptr_t inv, uintptr_t stream);
 void moe_grouped_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets,

@@ -7,6 +7,7 @@
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -33,6 +34,22 @@ def _launch(x, w, bias, y, m, n, k, mode):
                                m, n, k, mode, torch.cuda.current_stream().cuda_stream)
 
 
+# Which GEMM serves decode-sized M (64 <= M <= 512):
+#   DLLM_GEMM=auto  (default) tiled split-K kernel for long-K projections (K >= 8192: the MLP down
+#                   projection), where it measured 1.24-2.0x hipBLASLt (profiles/gemm_tiled_vs_hipblaslt.txt);
+#                   hipBLASLt elsewhere (ties or wins there)
+#   DLLM_GEMM=tiled / blas  force one implementation (A/B experiments)
+GEMM_MODE = os.environ.get("DLLM_GEMM", "auto")
+
+
+def _use_tiled(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool:
+    if GEMM_MODE == "blas" or not (64 <= m <= 512) or n % 128 or k % 64:
+        return False
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        return False
+    return GEMM_MODE == "tiled" or k >= 8192
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
            force_skinny: bool = False) -> torch.Tensor:
     k = x.shape[-1]
@@ -44,7 +61,49 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         y = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
         _launch(x, w, bias, y, m, n, k, 0)
         return y
+    if _use_tiled(m, n, k, x, w) and (bias is None or bias.dtype == torch.bfloat16):
+        return linear_tiled(x, w, bias)
     return F.linear(x, w, bias)
+
+
+_ws = {}
+_WS_FLOATS = 32 << 20          # 128 MiB of split-K partials per (device, stream)
+
+
+def _workspace(device: torch.device) -> torch.Tensor:
+    key = (device.index or 0, torch.cuda.current_stream().cuda_stream)
+    t = _ws.get(key)
+    if t is None:
+        t = _ws[key] = torch.empty(_WS_FLOATS, dtype=torch.float32, device=device)
+    return t
+
+
+def tiled_splits(m: int, n: int, k: int, target_wgs: int = 512) -> int:
+    tiles = (n // 128) * (-(-m // 128))
+    s = max(1, -(-target_wgs // tiles))
+    return max(1, min(s, k // 512, 16))
+
+
+def linear_tiled(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, splits: int = 0,
+                 swiglu: bool = False) -> torch.Tensor:
+    """Split-K LDS-tiled MFMA GEMM (csrc/kernels/gemm_tiled.hip) for decode-sized M."""
+    k = x.shape[-1]
+    n = w.shape[0]
+    m = x.numel() // k
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        raise ValueError("linear_tiled: bf16 contiguous operands")
+    if n % 128 or k % 64:
+        raise ValueError("linear_tiled: N % 128 and K % 64")
+    s = splits or tiled_splits(m, n, k)
+    ncols = n // 2 if swiglu else n
+    y = torch.empty(*x.shape[:-1], ncols, dtype=x.dtype, device=x.device)
+    ws = _workspace(x.device)
+    if s * m * n > ws.numel():
+        s = max(1, ws.numel() // (m * n))
+    _ext.kernels().gemm_tiled(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0 if bias is None else bias.data_ptr(),
+                              ws.data_ptr(), ws.numel(), m, n, k, s, 1 if swiglu else 0,
+                              torch.cuda.current_stream().cuda_stream)
+    return y
 
 
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor, force_skinny: bool = False) -> Optional[torch.Tensor]:

@@ -59,3 +59,22 @@ def test_skinny_graph_replay(cuda):
         x.copy_(_bf(64, 4096))
         g.replay()
         torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [1, 50, 128, 256, 300])
+@pytest.mark.parametrize("n,k,splits", [(6144, 4096, 0), (4096, 14336, 0), (256, 512, 1), (384, 1024, 3)])
+def test_tiled_linear(cuda, m, n, k, splits):
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear_tiled(x, w, splits=splits)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [7, 256])
+def test_tiled_swiglu_and_bias(cuda, m):
+    x, w = _bf(m, 1024), _bf(2 * 512, 1024, scale=0.05)
+    gu = x.float() @ w.float().t()
+    y = gemm.linear_tiled(x, w, swiglu=True, splits=2)
+    torch.testing.assert_close(y.float(), F.silu(gu[:, :512]) * gu[:, 512:], atol=3e-2, rtol=3e-2)
+    b = _bf(1024)
+    y2 = gemm.linear_tiled(x, w, bias=b, splits=2)
+    torch.testing.assert_close(y2.float(), gu + b.float(), atol=3e-2, rtol=3e-2)
