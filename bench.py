@@ -58,8 +58,10 @@ def make_prompts(n, plen, vocab, seed):
     return rng.integers(100, min(vocab, 30000), size=(n, plen)).tolist()
 
 
-def emit(args, world, elapsed, lat, extra):
-    tokens = args.steps * args.batch * world * args.gen_len
+def emit(args, world, elapsed, lat, extra, global_batch=None):
+    """global_batch = requests per round over the whole job (default batch x world)."""
+    global_batch = global_batch or args.batch * world
+    tokens = args.steps * global_batch * args.gen_len
     value = tokens / elapsed
     rec = {
         "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world,
@@ -68,7 +70,7 @@ def emit(args, world, elapsed, lat, extra):
         "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
         "dtype": "bf16", "data": "synthetic (random-init weights, random prompt ids)",
         "p50_latency_ms": round(1000 * statistics.median(lat), 3) if lat else None,
-        "config": {"model": args.model, "global_batch": args.batch * world, "seq_len": args.prompt_len + args.gen_len,
+        "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.prompt_len + args.gen_len,
                    "prompt_len": args.prompt_len, "gen_len": args.gen_len,
                    "parallelism": f"{args.parallelism}{world}"},
     }
@@ -90,9 +92,10 @@ def run_single(args):
                         max_prefill_tokens=max(16384, args.batch * args.prompt_len),
                         max_seq_len=args.prompt_len + args.gen_len + 32, use_graphs=not args.no_graphs,
                         seed=args.seed, streams=args.streams)
+    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
     t0 = time.perf_counter()
     eng = LLMEngine(ecfg)
-    torch.cuda.synchronize()
+    sync()
     load_s = time.perf_counter() - t0
     params = SamplingParams(max_new_tokens=args.gen_len, ignore_eos=True)
     vocab = eng.mcfg.vocab_size
@@ -104,13 +107,13 @@ def run_single(args):
 
     for r in range(args.warmup):
         round_(10_000 + r)
-    torch.cuda.synchronize()
+    sync()
     lat = []
     t0 = time.perf_counter()
     for r in range(args.steps):
         seqs = round_(r)
         lat.extend(s.latency() for s in seqs)
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     assert all(len(s.output) == args.gen_len for s in seqs)
     emit(args, 1, elapsed, lat, {"load_s": round(load_s, 1)})

@@ -32,8 +32,10 @@ def run_distributed(args, emit, make_prompts):
     load_s = time.perf_counter() - t0
     params = SamplingParams(max_new_tokens=args.gen_len, ignore_eos=True)
     vocab = ecfg.model_config().vocab_size
-    # requests per pipeline per round: batch x pp (each of the pp microbatch slots holds `batch`)
-    per_pipe = args.batch * ctx.pp
+    # requests per pipeline per round: `batch` per microbatch slot (pp=1: the engine's batch)
+    slots = role.driver.num_slots if role.driver is not None else 1
+    slots = int(agree_max(ctx, slots))
+    per_pipe = args.batch * slots
 
     def one_round(r):
         seqs = []
@@ -64,7 +66,8 @@ def run_distributed(args, emit, make_prompts):
                  "backend": dist.get_backend()}
         if role.driver is not None:
             extra["driver_stall_s"] = round(role.driver.stall_s, 3)
-        emit(args, world, elapsed, all_lat, extra)
+        extra["microbatch_slots"] = slots
+        emit(args, world, elapsed, all_lat, extra, global_batch=per_pipe * ctx.dp)
     role.shutdown()
     _sync(ctx)
     dist.destroy_process_group()

@@ -34,10 +34,51 @@ from .comm import STOP, Transport
 log = logging.getLogger("dllm.pipeline")
 
 ROUND_END = -2     # control marker: followers return to their caller (bench round barrier)
+FLUSH = -3         # control marker: the last stage must hand back the tokens it still holds
+_MARKERS = (STOP, ROUND_END, FLUSH)
 
 
 def _marker(code: int) -> np.ndarray:
     return np.array([code], dtype=np.int32)
+
+
+class _TokenReturn:
+    """Last stage: sampled ids go D2H asynchronously; a microbatch's tokens are sent only after
+    the NEXT microbatch has been launched, so the GPU never idles on the host's sync + send."""
+
+    def __init__(self, transport: Transport, max_rows: int, device):
+        self.t = transport
+        self.cuda = torch.device(device).type == "cuda"
+        self.bufs = [torch.empty(max_rows, dtype=torch.int32).pin_memory() if self.cuda else None for _ in range(2)]
+        self.events = [torch.cuda.Event() if self.cuda else None for _ in range(2)]
+        self.i = 0
+        self.pending = None
+
+    def push(self, step_id: int, ids: torch.Tensor):
+        n = ids.shape[0]
+        if self.cuda:
+            if n > self.bufs[self.i].shape[0]:
+                self.bufs[self.i] = torch.empty(n, dtype=torch.int32).pin_memory()
+            self.bufs[self.i][:n].copy_(ids, non_blocking=True)
+            self.events[self.i].record()
+            item = (step_id, n, self.i)
+            self.i ^= 1
+        else:
+            item = (step_id, n, ids.numpy().astype(np.int32))
+        self.flush()
+        self.pending = item
+
+    def flush(self):
+        if self.pending is None:
+            return
+        step_id, n, ref = self.pending
+        self.pending = None
+        if self.cuda:
+            self.events[ref].synchronize()
+            ids = self.bufs[ref][:n].numpy()
+        else:
+            ids = ref
+        self.t.send_tokens(np.concatenate([np.array([step_id, n], np.int32), ids.astype(np.int32)]))
 
 
 def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_end: bool = True) -> str:
@@ -45,14 +86,17 @@ def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_e
     st = runner.stage
     h = st.cfg.hidden_size
     last = transport.stage == transport.num_stages - 1
+    ret = _TokenReturn(transport, runner.ecfg.max_batch, st.device) if last else None
     while True:
         arr = transport.recv_meta()
-        if arr.shape[0] == 1 and arr[0] in (STOP, ROUND_END):
-            if not last:
-                transport.send_meta(arr) if arr[0] == ROUND_END else transport.send_stop()
+        if arr.shape[0] == 1 and arr[0] in _MARKERS:
+            if last:
+                ret.flush()
+            else:
+                transport.send_meta(arr) if arr[0] != STOP else transport.send_stop()
             if arr[0] == STOP:
                 return "stop"
-            if stop_on_round_end:
+            if arr[0] == ROUND_END and stop_on_round_end:
                 return "round"
             continue
         hb = HostBatch.unpack(arr)
@@ -61,9 +105,7 @@ def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_e
         hidden = transport.recv_hidden(hb.num_tokens, h, st.dtype, st.device)
         out = runner.execute(hb, hidden)
         if last:
-            ids = sample(out, **hb.sampling_args())
-            ids = ids.cpu().numpy().astype(np.int32)
-            transport.send_tokens(np.concatenate([np.array([hb.step_id, ids.shape[0]], np.int32), ids]))
+            ret.push(hb.step_id, sample(out, **hb.sampling_args()))
         else:
             transport.send_hidden(out)
 
@@ -78,7 +120,9 @@ class PipelineDriver:
         self.t = transport
         self.ecfg = ecfg
         self.bm = block_manager
-        self.num_slots = num_slots or max(ecfg.microbatches, transport.num_stages)
+        # one microbatch per stage keeps every stage busy only if the ring closure (last stage ->
+        # tokens -> stage 0 scheduling) were free; one spare slot hides that turnaround
+        self.num_slots = num_slots or (ecfg.microbatches if ecfg.microbatches > 0 else transport.num_stages + 1)
         self.scheduler = Scheduler(block_manager, self.num_slots, ecfg.max_batch, ecfg.max_prefill_tokens,
                                    ecfg.max_seq_len)
         self.mcfg = runner.stage.cfg
@@ -87,6 +131,7 @@ class PipelineDriver:
         self.step_id = 0
         self.num_steps = 0
         self.stall_s = 0.0
+        self._flushed = True
 
     def add_request(self, prompt: List[int], params: Optional[SamplingParams] = None,
                     request_id: Optional[str] = None) -> Sequence:
@@ -102,6 +147,7 @@ class PipelineDriver:
         hb = build_host_batch(step, self.bm, self.ecfg.kv_block_size,
                               None if step.is_prefill else self.runner.max_blocks, self.step_id)
         self.t.send_meta(hb.pack())
+        self._flushed = False
         out = self.runner.execute(hb)
         self.t.send_hidden(out)
         self.inflight.append((step, self.step_id))
@@ -111,6 +157,11 @@ class PipelineDriver:
         return True
 
     def _complete_oldest(self) -> List[Sequence]:
+        if len(self.inflight) == 1 and not self._flushed:
+            # the last stage holds the newest step's tokens until the next microbatch arrives;
+            # waiting on that step with nothing else to send would deadlock without a flush
+            self.t.send_meta(_marker(FLUSH))
+            self._flushed = True
         step, sid = self.inflight.popleft()
         t0 = time.perf_counter()
         arr = self.t.recv_tokens()

@@ -1,0 +1,55 @@
+"""bench.py driver contract on CPU: the exact `python -m torch.distributed.run ... bench.py --gpus N`
+form (gloo backend here), one JSON line from rank 0 with the required keys."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n,par", [(2, "pp"), (3, "pp"), (2, "dp")])
+def test_torchrun_bench_cpu(n, par):
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "1", "--warmup", "1", "--model", "tiny-llama", "--batch", "3",
+           "--prompt-len", "6", "--gen-len", "4", "--parallelism", par]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    rec = lines[0]
+    assert KEYS <= set(rec)
+    assert rec["n_gpus"] == n and rec["value"] > 0 and rec["config"]["parallelism"] == f"{par}{n}"
+    if par == "pp":
+        assert rec["microbatch_slots"] == n + 1
+        assert rec["config"]["global_batch"] == 3 * (n + 1)
+
+
+def test_single_process_bench_json_cpu():
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0", "--model",
+                        "tiny-llama", "--batch", "2", "--prompt-len", "5", "--gen-len", "3"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert KEYS <= set(rec) and rec["n_gpus"] == 1
