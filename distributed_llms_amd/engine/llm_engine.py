@@ -36,12 +36,12 @@ def make_block_manager(num_blocks: int, block_size: int):
 
 
 def build_stage(ecfg: EngineConfig, layer_start: int = 0, layer_end: Optional[int] = None,
-                device: Optional[str] = None, shard_state=None) -> ModelStage:
+                device: Optional[str] = None, shard_state=None, units=None) -> ModelStage:
     mcfg = ecfg.model_config()
     layer_end = mcfg.num_layers if layer_end is None else layer_end
     dev = resolve_device(device or ecfg.device)
     dtype = torch_dtype(ecfg.dtype)
-    stage = ModelStage(mcfg, layer_start, layer_end, device=dev, dtype=dtype)
+    stage = ModelStage(mcfg, layer_start, layer_end, device=dev, dtype=dtype, units=units)
     if shard_state is not None:
         stage.load_hf_state(shard_state)
     else:

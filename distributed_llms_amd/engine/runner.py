@@ -25,7 +25,7 @@ def plan_kv_blocks(mcfg: ModelConfig, num_layers: int, ecfg: EngineConfig, devic
     per_seq = -(-ecfg.max_seq_len // bs)
     slots = max(1, ecfg.microbatches or ecfg.num_workers)
     want = ecfg.max_batch * slots * per_seq + 2
-    per_block = KVCache.bytes_per_block(num_layers, mcfg.num_kv_heads, mcfg.head_dim, bs)
+    per_block = max(1, KVCache.bytes_per_block(num_layers, mcfg.num_kv_heads, mcfg.head_dim, bs))
     dev = torch.device(device)
     if dev.type == "cuda":
         free, _total = torch.cuda.mem_get_info(dev)

@@ -282,14 +282,17 @@ class MasterNode:
             return dict(self.shard_assignments)
 
     def _plans(self) -> List[Dict[str, Any]]:
-        from ..parallel.planner import plan_stages
+        from ..parallel.planner import plan_units
         cfg = self.model_config
         n = self.num_shards
         if self.shard_manager is not None:
             ranges = [tuple(r) for r in self.shard_manager.read_plan(self.shard_manager.shard_dir)["ranges"]]
+            unit_ranges = [(2 * a, 2 * b) for a, b in ranges]
             paths = self.shard_manager.get_shard_paths()
         else:
-            ranges = list(plan_stages(cfg, n).ranges)
+            up = plan_units(cfg, n, batch=self.config.max_batch, ctx=max(32, self.config.max_seq_len // 2))
+            ranges = list(up.ranges)
+            unit_ranges = list(up.units)
             paths = [None] * n
         ecfg = self.config.apply_overrides(model=self.model_spec, num_workers=n)
         ed = ecfg.to_dict()
@@ -299,6 +302,7 @@ class MasterNode:
         dist = {"master_addr": os.environ.get("DLLM_DIST_ADDR", "127.0.0.1" if master_addr == "0.0.0.0" else master_addr),
                 "master_port": _free_port()}
         return [{"shard_id": i, "stage": i, "num_stages": n, "layer_range": list(ranges[i]),
+                 "unit_range": list(unit_ranges[i]),
                  "shard_path": paths[i], "engine_config": ed, "dist": dist} for i in range(n)]
 
     def distribute_shards(self, timeout: float = 1800.0, ship_bytes: bool = False) -> Dict[str, Any]:

@@ -63,15 +63,30 @@ class KVCache:
         return 2 * num_layers * num_kv_heads * head_dim * block_size * dtype_bytes
 
 
+ATTN_KEYS = {"attn_norm", "wqkv", "wo", "ln1_w", "ln1_b", "bqkv", "bo"}
+
+
 class ModelStage:
+    """Layers ``[layer_start, layer_end)``, or -- finer -- half-layer *units* ``[u0, u1)``:
+    unit 2l is the attention half of layer l (norm, qkv, RoPE + KV append, attention, o-proj),
+    unit 2l+1 its MLP half.  Pipeline stages may start or end in the middle of a layer; the
+    stage hand-off is always the closed residual stream (one [T, H] tensor)."""
+
     def __init__(self, cfg: ModelConfig, layer_start: int, layer_end: int, device="cpu",
-                 dtype=torch.bfloat16):
-        if not (0 <= layer_start < layer_end <= cfg.num_layers):
-            raise ValueError(f"bad layer range [{layer_start}, {layer_end}) for {cfg.num_layers} layers")
+                 dtype=torch.bfloat16, units: Optional[tuple] = None):
+        if units is None:
+            units = (2 * layer_start, 2 * layer_end)
+        u0, u1 = int(units[0]), int(units[1])
+        if not (0 <= u0 < u1 <= 2 * cfg.num_layers):
+            raise ValueError(f"bad unit range [{u0}, {u1}) for {cfg.num_layers} layers")
         self.cfg = cfg
-        self.layer_start, self.layer_end = layer_start, layer_end
-        self.is_first = layer_start == 0
-        self.is_last = layer_end == cfg.num_layers
+        self.unit_start, self.unit_end = u0, u1
+        self.layer_start, self.layer_end = u0 // 2, (u1 + 1) // 2
+        self.is_first = u0 == 0
+        self.is_last = u1 == 2 * cfg.num_layers
+        # layers whose attention half (and therefore KV cache) lives on this stage
+        self.kv_layers = [l for l in range(self.layer_start, self.layer_end) if u0 <= 2 * l < u1]
+        self.kv_index = {l: i for i, l in enumerate(self.kv_layers)}
         self.device = torch.device(device)
         self.dtype = dtype
         self.layers: List[Dict[str, torch.Tensor]] = []
@@ -87,7 +102,13 @@ class ModelStage:
     # --------------------------------------------------------------- weights
     @property
     def num_layers(self) -> int:
-        return self.layer_end - self.layer_start
+        """Layers with KV on this stage (what the paged KV pool is sized for)."""
+        return len(self.kv_layers)
+
+    def _keep(self, layer: int, name: str) -> bool:
+        has_attn = self.unit_start <= 2 * layer < self.unit_end
+        has_mlp = self.unit_start <= 2 * layer + 1 < self.unit_end
+        return has_attn if name in ATTN_KEYS else has_mlp
 
     def needs_embed(self) -> bool:
         return self.is_first or (self.is_last and self.cfg.tie_embeddings)
@@ -95,8 +116,10 @@ class ModelStage:
     def init_synthetic(self, seed: int = 0) -> "ModelStage":
         """Seeded random-init weights generated directly on the stage's device."""
         cfg = self.cfg
-        self.layers = [W.synth_block(cfg, l, seed, self.dtype, self.device)
-                       for l in range(self.layer_start, self.layer_end)]
+        self.layers = []
+        for l in range(self.layer_start, self.layer_end):
+            shapes = {n: s for n, s in W.block_shapes(cfg).items() if self._keep(l, n)}
+            self.layers.append({n: W.synth_tensor(seed, l, n, s, self.dtype, self.device) for n, s in shapes.items()})
         if self.needs_embed():
             self.embed = W.synth_embed(cfg, seed, self.dtype, self.device)
             if not self.is_first:
@@ -109,7 +132,7 @@ class ModelStage:
         """Load from HF-named tensors (a shard file's dict); fuses q|k|v and gate|up."""
         cfg = self.cfg
         conv = lambda t: t.to(device=self.device, dtype=self.dtype).contiguous()
-        self.layers = [{k: conv(v) for k, v in W.hf_to_block(cfg, l, sd).items()}
+        self.layers = [{k: conv(v) for k, v in W.hf_to_block(cfg, l, sd).items() if self._keep(l, k)}
                        for l in range(self.layer_start, self.layer_end)]
         if self.needs_embed():
             names = W.hf_embed_names(cfg)
@@ -163,21 +186,27 @@ class ModelStage:
                                    self.cfg.experts_per_token)
         return ops.linear(ops.linear_swiglu(h, lw["w_gate_up"]), lw["w_down"])
 
+    def _units(self):
+        for u in range(self.unit_start, self.unit_end):
+            l = u // 2
+            yield u % 2 == 0, l, self.layers[l - self.layer_start]
+
     def _forward_llama(self, inp: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
         cfg = self.cfg
         eps = cfg.norm_eps
         residual = ops.embedding(inp, self.embed["embed"]) if self.is_first else inp.clone()
-        h = None
-        for li, lw in enumerate(self.layers):
+        h = None   # output of the previous half, not yet added to the residual stream
+        for is_attn, l, lw in self._units():
+            norm_w = lw["attn_norm"] if is_attn else lw["mlp_norm"]
             if h is None:
-                h = ops.rms_norm(residual, lw["attn_norm"], eps)
+                x = ops.rms_norm(residual, norm_w, eps)
             else:
-                h, residual = ops.fused_add_rms_norm(h, residual, lw["attn_norm"], eps)
-            qkv = ops.linear(h, lw["wqkv"])
-            a = self._attention(qkv, li, meta)
-            o = ops.linear(a, lw["wo"])
-            h, residual = ops.fused_add_rms_norm(o, residual, lw["mlp_norm"], eps)
-            h = self._mlp(h, lw)
+                x, residual = ops.fused_add_rms_norm(h, residual, norm_w, eps)
+            if is_attn:
+                a = self._attention(ops.linear(x, lw["wqkv"]), self.kv_index[l], meta)
+                h = ops.linear(a, lw["wo"])
+            else:
+                h = self._mlp(x, lw)
         if not self.is_last:
             return ops.add_(residual, h)
         return self._logits(h, residual, meta)
@@ -202,14 +231,15 @@ class ModelStage:
             x = ops.add_(x, pe)
         else:
             x = inp.clone()
-        for li, lw in enumerate(self.layers):
-            h = ops.layer_norm(x, lw["ln1_w"], lw["ln1_b"], eps)
-            qkv = ops.linear(h, lw["wqkv"], lw["bqkv"])
-            a = self._attention(qkv, li, meta)
-            x = ops.add_(x, ops.linear(a, lw["wo"], lw["bo"]))
-            h = ops.layer_norm(x, lw["ln2_w"], lw["ln2_b"], eps)
-            f = ops.gelu_tanh(ops.linear(h, lw["w_fc"], lw["b_fc"]))
-            x = ops.add_(x, ops.linear(f, lw["w_proj"], lw["b_proj"]))
+        for is_attn, l, lw in self._units():
+            if is_attn:
+                h = ops.layer_norm(x, lw["ln1_w"], lw["ln1_b"], eps)
+                a = self._attention(ops.linear(h, lw["wqkv"], lw["bqkv"]), self.kv_index[l], meta)
+                x = ops.add_(x, ops.linear(a, lw["wo"], lw["bo"]))
+            else:
+                h = ops.layer_norm(x, lw["ln2_w"], lw["ln2_b"], eps)
+                f = ops.gelu_tanh(ops.linear(h, lw["w_fc"], lw["b_fc"]))
+                x = ops.add_(x, ops.linear(f, lw["w_proj"], lw["b_proj"]))
         if not self.is_last:
             return x
         if meta.logits_idx is not None:

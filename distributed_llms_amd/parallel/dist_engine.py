@@ -20,7 +20,7 @@ from ..engine.llm_engine import LLMEngine, build_stage, make_block_manager
 from ..engine.runner import StageRunner, plan_kv_blocks
 from .comm import DistTransport
 from .pipeline import PipelineDriver, stage_worker_loop
-from .planner import plan_stages
+from .planner import plan_units
 
 log = logging.getLogger("dllm.dist")
 
@@ -91,10 +91,11 @@ class RankRole:
         self.ctx = ctx
         self.ecfg = ecfg
         mcfg = ecfg.model_config()
-        self.plan = plan_stages(mcfg, ctx.pp)
+        self.plan = plan_units(mcfg, ctx.pp, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2))
         a, b = self.plan.ranges[ctx.stage]
-        stage = build_stage(ecfg, a, b, device=ctx.device, shard_state=hf_state)
-        nb = plan_kv_blocks(mcfg, b - a, ecfg, stage.device)
+        stage = build_stage(ecfg, a, b, device=ctx.device, shard_state=hf_state,
+                            units=self.plan.unit_range(ctx.stage))
+        nb = plan_kv_blocks(mcfg, stage.num_layers, ecfg, stage.device)
         nb = agree_min(ctx, nb)        # every stage of a pipeline must hold the same block ids
         self.engine = None
         self.driver = None

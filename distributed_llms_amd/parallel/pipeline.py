@@ -215,14 +215,14 @@ def run_loopback_pipeline(ecfg: EngineConfig, num_stages: int, prompts, params: 
 
     from ..engine.llm_engine import build_stage, make_block_manager
     from .comm import LoopbackHub
-    from .planner import plan_stages
+    from .planner import plan_units
 
     mcfg = ecfg.model_config()
-    plan = plan_stages(mcfg, num_stages)
+    plan = plan_units(mcfg, num_stages, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2))
     hub = LoopbackHub(num_stages)
     runners = []
     for s, (a, b) in enumerate(plan.ranges):
-        stage = build_stage(ecfg, a, b, device=device, shard_state=hf_state)
+        stage = build_stage(ecfg, a, b, device=device, shard_state=hf_state, units=plan.unit_range(s))
         runners.append(StageRunner(stage, ecfg, num_blocks=ecfg.num_kv_blocks or 512))
     errors = []
     # capture every stage's decode graphs up front, one at a time: concurrent captures from

@@ -1,16 +1,21 @@
-"""Stage planner: contiguous, cost-balanced layer ranges.
+"""Stage planner: contiguous, cost-balanced stage ranges.
 
-The reference groups parameters by ``key.split('.')[1]`` and greedily drops whole
-layers onto the currently smallest shard (``src/model/shard_manager.py:33-61``), which
-for equal-size layers is round-robin (shard0 = layers 0,2,4 -- D12) and useless for a
-pipeline.  Here each stage owns ONE contiguous block range, and the split minimises the
-most expensive stage under a decode cost model in bytes read per step:
+The reference groups parameters by ``key.split('.')[1]`` and greedily drops whole layers
+onto the currently smallest shard (``src/model/shard_manager.py:33-61``), which for
+equal-size layers is round-robin (shard0 = layers 0,2,4 -- D12) and useless for a
+pipeline.  Here each stage owns ONE contiguous range, chosen by dynamic programming to
+minimise the most expensive stage.
 
-  block    = its weight bytes (+ KV bytes of the expected context, optional)
-  stage 0  += one embedding row gather (negligible)
-  last     += final norm + LM head (the 8B head is ~2.4 blocks of bytes)
-
-Solved exactly by dynamic programming over (layers, stages) (L <= 80, stages <= 8).
+Two granularities:
+* whole layers (:func:`plan_stages`) -- checkpoint shards (``shards/shard_{i}.pt`` hold whole
+  blocks), cost = weight bytes (+ the LM head on the last stage);
+* half layers (:func:`plan_units`) -- runtime pipelines: unit 2l = attention half of layer l
+  (norm, qkv, RoPE + KV append, attention, o-proj), unit 2l+1 = its MLP half.  Llama-3-8B on 8
+  stages at batch 256 is capped at ~83 % balance by whole-layer cuts (32 layers + an LM head
+  worth ~1.2 layers of time) and at ~95 % by half-layer cuts.  Costs come from a decode time
+  model calibrated on MI355X kernel profiles (profiles/llama3_8b_b256_kernels.md): each GEMM
+  takes max(weight bytes / HBM rate, FLOPs / achieved MFMA rate), attention reads the KV of
+  ``ctx`` tokens per sequence, plus fixed per-half elementwise/norm time.
 """
 from __future__ import annotations
 
@@ -19,11 +24,21 @@ from typing import List, Optional, Sequence, Tuple
 
 from ..config import ModelConfig
 
+# ---- decode time model (MI355X, bf16, measured on Llama-3-8B at batch 256, ctx ~192)
+HBM_B_PER_US = 5.0e6          # weight streaming, bytes / us
+KV_B_PER_US = 4.5e6           # attention KV read, bytes / us
+ATTN_GEMM_FLOP_PER_US = 3.4e8 # qkv + o projections at decode M (0.34 PF achieved)
+MLP_GEMM_FLOP_PER_US = 6.9e8  # gate_up + down (0.69 PF)
+HEAD_FLOP_PER_US = 8.4e8      # LM head (0.84 PF)
+ATTN_FIXED_US = 21.0          # RoPE/KV-append + norm kernels
+MLP_FIXED_US = 17.0           # SwiGLU + norm kernels
+
 
 @dataclass(frozen=True)
 class StagePlan:
-    ranges: Tuple[Tuple[int, int], ...]     # [start, end) per stage
+    ranges: Tuple[Tuple[int, int], ...]     # [start, end) layers touched per stage
     costs: Tuple[float, ...]
+    units: Optional[Tuple[Tuple[int, int], ...]] = None   # [start, end) half-layer units per stage
 
     @property
     def num_stages(self) -> int:
@@ -35,33 +50,35 @@ class StagePlan:
                 return i
         raise KeyError(layer)
 
+    def unit_range(self, stage: int) -> Tuple[int, int]:
+        if self.units is not None:
+            return self.units[stage]
+        a, b = self.ranges[stage]
+        return 2 * a, 2 * b
+
     def imbalance(self) -> float:
         return max(self.costs) / (sum(self.costs) / len(self.costs))
 
     def to_json(self):
-        return {"ranges": [list(r) for r in self.ranges], "costs": list(self.costs)}
+        d = {"ranges": [list(r) for r in self.ranges], "costs": [round(c, 1) for c in self.costs]}
+        if self.units is not None:
+            d["units"] = [list(u) for u in self.units]
+        return d
 
 
-def layer_costs(cfg: ModelConfig, dtype_bytes: int = 2, active_experts_only: bool = True) -> List[float]:
-    per = cfg.layer_param_count()
-    if cfg.is_moe and active_experts_only:
-        # decode reads only the routed experts' weights for small batches; at large batches
-        # all experts are touched -- keep the full count, it is what HBM capacity needs anyway
-        pass
-    return [per * dtype_bytes] * cfg.num_layers
+def layer_costs(cfg: ModelConfig, dtype_bytes: int = 2) -> List[float]:
+    return [cfg.layer_param_count() * dtype_bytes] * cfg.num_layers
 
 
 def head_cost(cfg: ModelConfig, dtype_bytes: int = 2) -> float:
     return cfg.head_param_count() * dtype_bytes
 
 
-def plan_stages(cfg: ModelConfig, num_stages: int, costs: Optional[Sequence[float]] = None,
-                head: Optional[float] = None, first_extra: float = 0.0) -> StagePlan:
-    L = cfg.num_layers
-    if not 1 <= num_stages <= L:
-        raise ValueError(f"cannot split {L} layers into {num_stages} stages")
-    costs = list(costs) if costs is not None else layer_costs(cfg)
-    head = head_cost(cfg) if head is None else head
+def _partition(costs: Sequence[float], n: int, head: float, first_extra: float = 0.0) -> List[Tuple[int, int]]:
+    """Exact min-max contiguous partition of ``costs`` into ``n`` parts (head added to the last)."""
+    L = len(costs)
+    if not 1 <= n <= L:
+        raise ValueError(f"cannot split {L} units into {n} stages")
     pre = [0.0]
     for c in costs:
         pre.append(pre[-1] + c)
@@ -70,17 +87,16 @@ def plan_stages(cfg: ModelConfig, num_stages: int, costs: Optional[Sequence[floa
         c = pre[b] - pre[a]
         if s == 0:
             c += first_extra
-        if s == num_stages - 1:
+        if s == n - 1:
             c += head
         return c
 
     INF = float("inf")
-    # best[s][j]: min over splits of layers [0, j) into s+1 stages of the max stage cost
-    best = [[INF] * (L + 1) for _ in range(num_stages)]
-    arg = [[0] * (L + 1) for _ in range(num_stages)]
+    best = [[INF] * (L + 1) for _ in range(n)]
+    arg = [[0] * (L + 1) for _ in range(n)]
     for j in range(1, L + 1):
         best[0][j] = seg(0, j, 0)
-    for s in range(1, num_stages):
+    for s in range(1, n):
         for j in range(s + 1, L + 1):
             for i in range(s, j):
                 v = max(best[s - 1][i], seg(i, j, s))
@@ -88,11 +104,53 @@ def plan_stages(cfg: ModelConfig, num_stages: int, costs: Optional[Sequence[floa
                     best[s][j], arg[s][j] = v, i
     bounds = [L]
     j = L
-    for s in range(num_stages - 1, 0, -1):
+    for s in range(n - 1, 0, -1):
         j = arg[s][j]
         bounds.append(j)
     bounds.append(0)
     bounds.reverse()
-    ranges = tuple((bounds[i], bounds[i + 1]) for i in range(num_stages))
-    cs = tuple(seg(a, b, i) for i, (a, b) in enumerate(ranges))
-    return StagePlan(ranges, cs)
+    return [(bounds[i], bounds[i + 1]) for i in range(n)]
+
+
+def plan_stages(cfg: ModelConfig, num_stages: int, costs: Optional[Sequence[float]] = None,
+                head: Optional[float] = None, first_extra: float = 0.0) -> StagePlan:
+    """Whole-layer plan (checkpoint shards), cost = bytes."""
+    costs = list(costs) if costs is not None else layer_costs(cfg)
+    head = head_cost(cfg) if head is None else head
+    ranges = _partition(costs, num_stages, head, first_extra)
+    pre = [0.0]
+    for c in costs:
+        pre.append(pre[-1] + c)
+    cs = [pre[b] - pre[a] + (first_extra if i == 0 else 0) + (head if i == num_stages - 1 else 0)
+          for i, (a, b) in enumerate(ranges)]
+    return StagePlan(tuple(ranges), tuple(cs))
+
+
+def unit_costs_us(cfg: ModelConfig, batch: int = 256, ctx: int = 192) -> Tuple[List[float], float]:
+    """Per half-layer decode time estimates (us) and the LM head's."""
+    h, i = cfg.hidden_size, cfg.intermediate_size
+    attn_p = h * cfg.qkv_size + cfg.q_size * h
+    if cfg.is_moe:
+        mlp_p_read = cfg.num_experts * 3 * h * i           # every expert is read at decode batch sizes
+        mlp_p_flop = cfg.experts_per_token * 3 * h * i
+    else:
+        mlp_p_read = mlp_p_flop = 3 * h * i
+    kv_b = batch * ctx * 2 * cfg.kv_size * 2
+    attn = max(2 * attn_p / HBM_B_PER_US, 2 * batch * attn_p / ATTN_GEMM_FLOP_PER_US) + kv_b / KV_B_PER_US \
+        + ATTN_FIXED_US
+    mlp = max(2 * mlp_p_read / HBM_B_PER_US, 2 * batch * mlp_p_flop / MLP_GEMM_FLOP_PER_US) + MLP_FIXED_US
+    head_p = cfg.vocab_size * h
+    head = max(2 * head_p / HBM_B_PER_US, 2 * batch * head_p / HEAD_FLOP_PER_US)
+    return [attn, mlp] * cfg.num_layers, head
+
+
+def plan_units(cfg: ModelConfig, num_stages: int, batch: int = 256, ctx: int = 192) -> StagePlan:
+    """Half-layer plan for runtime pipelines (see module doc)."""
+    costs, head = unit_costs_us(cfg, batch, ctx)
+    units = _partition(costs, num_stages, head)
+    pre = [0.0]
+    for c in costs:
+        pre.append(pre[-1] + c)
+    cs = [pre[b] - pre[a] + (head if k == num_stages - 1 else 0) for k, (a, b) in enumerate(units)]
+    ranges = tuple((a // 2, (b + 1) // 2) for a, b in units)
+    return StagePlan(ranges, tuple(cs), tuple(units))

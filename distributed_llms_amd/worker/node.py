@@ -408,12 +408,12 @@ class WorkerNode:
             state = load_shard_file(plan["shard_path"])
         if state is not None and ecfg.model_config().arch == "gpt2":
             state.pop("lm_head.weight", None)
-        stage = build_stage(ecfg, a, b, device=self.device, shard_state=state)
+        stage = build_stage(ecfg, a, b, device=self.device, shard_state=state, units=plan.get("unit_range"))
         del state
         ctx = None
         if world > 1:
             ctx = self._init_dist(plan["dist"], stage_idx, world)
-        nb = plan_kv_blocks(stage.cfg, b - a, ecfg, stage.device)
+        nb = plan_kv_blocks(stage.cfg, stage.num_layers, ecfg, stage.device)
         if ctx is not None:
             from ..parallel.dist_engine import agree_min
             nb = agree_min(ctx, nb)

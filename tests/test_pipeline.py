@@ -100,3 +100,43 @@ def test_multiprocess_gloo_pipeline(expected, world, pp):
     for r in drivers:
         for rnd in results[r]:
             assert rnd == expected
+
+
+def test_half_layer_stage_chain_matches_full():
+    """Stages that start/end in the middle of a layer (attention | MLP halves) compose exactly."""
+    from distributed_llms_amd.engine.batch import build_host_batch, to_device_meta
+    from distributed_llms_amd.engine.llm_engine import make_block_manager
+    from distributed_llms_amd.engine.scheduler import Scheduler
+    from distributed_llms_amd.engine.sequence import Sequence
+    from distributed_llms_amd.models.stage import ModelStage
+    for name in ("tiny-llama", "tiny-gpt2", "tiny-mixtral"):
+        cfg = get_model_config(name)
+        full = ModelStage(cfg, 0, cfg.num_layers, "cpu", torch.float32).init_synthetic(5)
+        parts = [ModelStage(cfg, 0, 0, "cpu", torch.float32, units=u).init_synthetic(5)
+                 for u in ((0, 3), (3, 4), (4, 7), (7, 2 * cfg.num_layers))]
+        assert parts[1].num_layers == 0 and parts[0].num_layers == 2   # (3,4) is one MLP half, no KV
+        for st in [full] + parts:
+            st.allocate_kv(16, 32)
+        bm = make_block_manager(16, 32)
+        sch = Scheduler(bm, 1, 4, 1024, 128)
+        for p in ([3, 4, 5, 6], [9, 9]):
+            sch.add(Sequence(p))
+        step = sch.schedule(0)
+        ids, meta = to_device_meta(build_host_batch(step, bm, 32), "cpu")
+        ref = full.forward(ids, meta)
+        x = ids
+        for st in parts:
+            x = st.forward(x, meta)
+        torch.testing.assert_close(x, ref)
+
+
+def test_unit_planner_balances_better_than_layers():
+    from distributed_llms_amd.parallel.planner import plan_stages, plan_units, unit_costs_us
+    cfg = get_model_config("llama3-8b")
+    c, head = unit_costs_us(cfg, 256, 192)
+    for n in (4, 8):
+        u = plan_units(cfg, n, 256, 192)
+        l = plan_stages(cfg, n, costs=[c[0] + c[1]] * cfg.num_layers, head=head)
+        assert u.imbalance() < l.imbalance()
+        assert u.units[0][0] == 0 and u.units[-1][1] == 64
+        assert all(a[1] == b[0] for a, b in zip(u.units, u.units[1:]))
