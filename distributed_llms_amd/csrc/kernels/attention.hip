@@ -33,13 +33,26 @@ __device__ __forceinline__ void attend_chunk(WaveState<D>& st, const bf16x8 (&qf
                                              const bf16* __restrict__ kblk, const bf16* __restrict__ vblk,
                                              int t0, int kmax_col, float scale_log2, int lane) {
   const int r = lane & 15, g = lane >> 4;
+  // Issue every K and V load of the chunk before any math: V does not depend on the scores,
+  // so its HBM latency overlaps K's instead of following the softmax.
+  bf16x8 ka[D / 32], kb[D / 32];
+  bf16x4 vlo[D / 16], vhi[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    ka[ks] = *reinterpret_cast<const bf16x8*>(kblk + r * D + ks * 32 + 8 * g);
+    kb[ks] = *reinterpret_cast<const bf16x8*>(kblk + (16 + r) * D + ks * 32 + 8 * g);
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    const bf16* vr = vblk + (dt * 16 + r) * kBS;
+    vlo[dt] = *reinterpret_cast<const bf16x4*>(vr + 4 * g);
+    vhi[dt] = *reinterpret_cast<const bf16x4*>(vr + 16 + 4 * g);
+  }
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
-    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(kblk + r * D + ks * 32 + 8 * g);
-    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(kblk + (16 + r) * D + ks * 32 + 8 * g);
-    s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qf[ks], s0, 0, 0, 0);
-    s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qf[ks], s1, 0, 0, 0);
+    s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[ks], qf[ks], s0, 0, 0, 0);
+    s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[ks], qf[ks], s1, 0, 0, 0);
   }
   float p[8];
   float cm = -INFINITY;
@@ -71,9 +84,7 @@ __device__ __forceinline__ void attend_chunk(WaveState<D>& st, const bf16x8 (&qf
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt) {
     st.acc[dt] *= alpha;
-    const bf16* vr = vblk + (dt * 16 + r) * kBS;
-    const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vr + 4 * g);
-    const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vr + 16 + 4 * g);
+    const bf16x4 lo = vlo[dt], hi = vhi[dt];
     bf16x8 va;
     va[0] = lo[0]; va[1] = lo[1]; va[2] = lo[2]; va[3] = lo[3];
     va[4] = hi[0]; va[5] = hi[1]; va[6] = hi[2]; va[7] = hi[3];
