@@ -49,6 +49,9 @@ def parse(argv=None):
     ap.add_argument("--streams", type=int, default=1, help="1-GPU engine: microbatch slots on separate streams")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--trace", default=None, metavar="DIR",
+                    help="record a roctx/host/GPU timeline of the timed steps: DIR/trace_rank<r>.json "
+                         "(Chrome format) and per-stage device busy %% in the JSON line")
     return ap.parse_args(argv)
 
 
@@ -82,6 +85,24 @@ def emit(args, world, elapsed, lat, extra, global_batch=None):
             f.write(line + "\n")
 
 
+def start_trace(args):
+    if not args.trace:
+        return None
+    from distributed_llms_amd.utils.tracing import get_tracer
+    tr = get_tracer()
+    tr.clear()
+    return tr.enable(True)
+
+
+def finish_trace(args, tr, elapsed, rank):
+    """Export this rank's timeline; return its stage's device busy fraction over the timed steps."""
+    tr.enable(False)
+    os.makedirs(args.trace, exist_ok=True)
+    util = tr.utilization(elapsed, cat="stage")
+    tr.export_chrome(os.path.join(args.trace, f"trace_rank{rank}.json"), process_name=f"rank{rank}")
+    return round(util["busy_frac"], 4)
+
+
 def run_single(args):
     import torch
     from distributed_llms_amd.config import EngineConfig
@@ -108,6 +129,7 @@ def run_single(args):
     for r in range(args.warmup):
         round_(10_000 + r)
     sync()
+    tr = start_trace(args)
     lat = []
     t0 = time.perf_counter()
     for r in range(args.steps):
@@ -116,7 +138,10 @@ def run_single(args):
     sync()
     elapsed = time.perf_counter() - t0
     assert all(len(s.output) == args.gen_len for s in seqs)
-    emit(args, 1, elapsed, lat, {"load_s": round(load_s, 1)})
+    extra = {"load_s": round(load_s, 1)}
+    if tr is not None:
+        extra["stage_busy_frac"] = [finish_trace(args, tr, elapsed, 0)]
+    emit(args, 1, elapsed, lat, extra)
 
 
 def main(argv=None):
@@ -124,7 +149,7 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.gpus > 1:
         from distributed_llms_amd.parallel.bench_dist import run_distributed
-        return run_distributed(args, emit, make_prompts)
+        return run_distributed(args, emit, make_prompts, start_trace, finish_trace)
     run_single(args)
 
 

@@ -12,60 +12,53 @@ namespace dllm {
 // K2: RMSNorm, optionally fused with the residual add.
 //   residual == nullptr : y = rmsnorm(x) * w
 //   residual != nullptr : r = x + residual; residual <- r; y = rmsnorm(r) * w
-// One WAVE per row (4 rows per 256-thread workgroup): the sum of squares is a pure
-// wave reduction (no LDS, no barrier), and the row stays in registers between the
-// reduction and the scale pass (MAXV bf16x8 vectors per lane).  The first version used
-// one 256-thread workgroup per row with a block reduction: 6.7 us per call at 256 rows,
-// latency-bound (profiles/llama3_8b_b256_kernels.md).
+// One 256-thread workgroup per row; the row stays in registers between the
+// sum-of-squares pass and the scale pass (MAXV vectors of 8 per thread).
 // ---------------------------------------------------------------------------
 template <int MAXV>
 __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ y, const bf16* __restrict__ x,
                                                        bf16* __restrict__ residual,
-                                                       const bf16* __restrict__ w, int rows, int hidden,
+                                                       const bf16* __restrict__ w, int hidden,
                                                        float eps) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;   // wave-uniform
+  __shared__ float red[16];
+  const int row = blockIdx.x;
   const int nvec = hidden >> 3;
   const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * hidden);
   bf16x8* rr = residual ? reinterpret_cast<bf16x8*>(residual + (size_t)row * hidden) : nullptr;
-  bf16x8 a[MAXV], b[MAXV];
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {      // issue every load of the row before using any
-    const int idx = lane + i * 64;
-    if (idx < nvec) {
-      a[i] = xr[idx];
-      if (rr) b[i] = rr[idx];
-    }
-  }
+  float v[MAXV][8];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int idx = lane + i * 64;
+    const int idx = threadIdx.x + i * 256;
     if (idx < nvec) {
+      bf16x8 a = xr[idx];
       if (rr) {
+        bf16x8 b = rr[idx];
         bf16x8 s;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] = f2bf(bf2f(a[i][j]) + bf2f(b[i][j]));
+        for (int j = 0; j < 8; ++j) s[j] = f2bf(bf2f(a[j]) + bf2f(b[j]));
         rr[idx] = s;
-        a[i] = s;  // normalise the bf16-rounded residual, as the reference does
+        a = s;  // normalise the bf16-rounded residual, as the reference does
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ss += bf2f(a[i][j]) * bf2f(a[i][j]);
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = bf2f(a[j]);
+        ss += v[i][j] * v[i][j];
+      }
     }
   }
-  ss = wave_sum(ss);
+  ss = block_sum(ss, red);
   const float inv = rsqrtf(ss / (float)hidden + eps);
   const bf16x8* wv = reinterpret_cast<const bf16x8*>(w);
   bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)row * hidden);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int idx = lane + i * 64;
+    const int idx = threadIdx.x + i * 256;
     if (idx < nvec) {
-      const bf16x8 g = wv[idx];
+      bf16x8 g = wv[idx];
       bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(a[i][j]) * inv * bf2f(g[j]));
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(g[j]));
       yr[idx] = o;
     }
   }
@@ -73,20 +66,19 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ y, con
 
 void rms_norm(uintptr_t y, uintptr_t x, uintptr_t residual, uintptr_t w, int rows, int hidden,
               float eps, uintptr_t stream) {
-  DLLM_HOST_CHECK(hidden % 8 == 0 && hidden <= 64 * 16 * 8, "hidden must be a multiple of 8 and <= 8192");
+  DLLM_HOST_CHECK(hidden % 8 == 0 && hidden <= 8 * 256 * 8, "hidden must be a multiple of 8 and <= 16384");
   DLLM_HOST_CHECK(rows >= 0, "rows >= 0");
   if (rows == 0) return;
   const int nvec = hidden / 8;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   auto args = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((rows + 3) / 4), dim3(256), 0, s, (bf16*)y, (const bf16*)x, (bf16*)residual,
-                       (const bf16*)w, rows, hidden, eps);
+    hipLaunchKernelGGL(kern, dim3(rows), dim3(256), 0, s, (bf16*)y, (const bf16*)x, (bf16*)residual,
+                       (const bf16*)w, hidden, eps);
   };
-  if (nvec <= 64) args(rms_norm_kernel<1>);
-  else if (nvec <= 128) args(rms_norm_kernel<2>);
-  else if (nvec <= 256) args(rms_norm_kernel<4>);
-  else if (nvec <= 512) args(rms_norm_kernel<8>);
-  else args(rms_norm_kernel<16>);
+  if (nvec <= 256) args(rms_norm_kernel<1>);
+  else if (nvec <= 512) args(rms_norm_kernel<2>);
+  else if (nvec <= 1024) args(rms_norm_kernel<4>);
+  else args(rms_norm_kernel<8>);
   DLLM_HIP_CHECK(hipGetLastError());
 }
 
@@ -117,11 +109,7 @@ void embedding(uintptr_t out, uintptr_t ids, uintptr_t table, int tokens, int hi
 // qkv [T, (Hq + 2 Hkv) * D] -> q_out [T, Hq, D] (rotated)
 // k_cache [NB, Hkv, BS, D]; v_cache [NB, Hkv, D, BS] (transposed V).
 // cos_sin [max_pos, D] f32 (first half cos, second half sin); nullptr = no RoPE (GPT-2).
-// One WAVE per (token, head) -- grid (tokens, ceil(heads / 4)), 4 waves per workgroup:
-// lane i of a q/k head rotates pairs (i, i + D/2) (and (i + 32, i + 32 + D/2) when D = 128);
-// lane i of a v head scatters dims i (and i + 64) into the transposed V block.  The first
-// version used one 256-thread workgroup per token (13.6 us at 256 decode tokens,
-// latency-bound; profiles/llama3_8b_b256_kernels.md).
+// One workgroup per token; a thread owns 4 rotation pairs (8-byte vectors).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ q_out, const bf16* __restrict__ qkv,
                                                          const int32_t* __restrict__ positions,
@@ -130,43 +118,57 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ q_ou
                                                          const int32_t* __restrict__ slots, int hq, int hkv,
                                                          int d, int bs) {
   const int t = blockIdx.x;
-  const int h = blockIdx.y * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int nh = hq + 2 * hkv;
-  if (h >= nh) return;   // wave-uniform
   const int half = d >> 1;
+  const int qpr = half >> 2;  // threads per head (4 pairs each)
+  const int pos = positions[t];
   const int slot = slots[t];
   const int blk = slot / bs, off = slot % bs;
-  const bf16* src = qkv + ((size_t)t * nh + h) * d;
-  if (h < hq + hkv) {
-    const float* cs = cos_sin ? cos_sin + (size_t)positions[t] * d : nullptr;
-    bf16* dst = h < hq ? q_out + ((size_t)t * hq + h) * d
-                       : k_cache + (((size_t)blk * hkv + (h - hq)) * bs + off) * d;
-    for (int i = lane; i < half; i += 64) {
-      const float a = bf2f(src[i]), b = bf2f(src[i + half]);
-      if (cs) {
-        const float c = cs[i], s = cs[i + half];
-        dst[i] = f2bf(a * c - b * s);
-        dst[i + half] = f2bf(b * c + a * s);
-      } else {
-        dst[i] = src[i];
-        dst[i + half] = src[i + half];
+  const bf16* row = qkv + (size_t)t * (hq + 2 * hkv) * d;
+  const float* cs = cos_sin ? cos_sin + (size_t)pos * d : nullptr;
+  // q and k: rotate
+  for (int i = threadIdx.x; i < (hq + hkv) * qpr; i += blockDim.x) {
+    const int h = i / qpr, p = (i % qpr) * 4;
+    const bf16* src = row + h * d;
+    bf16x4 x1 = *reinterpret_cast<const bf16x4*>(src + p);
+    bf16x4 x2 = *reinterpret_cast<const bf16x4*>(src + half + p);
+    bf16x4 o1, o2;
+    if (cs) {
+      f32x4 c = *reinterpret_cast<const f32x4*>(cs + p);
+      f32x4 s = *reinterpret_cast<const f32x4*>(cs + half + p);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = bf2f(x1[j]), b = bf2f(x2[j]);
+        o1[j] = f2bf(a * c[j] - b * s[j]);
+        o2[j] = f2bf(b * c[j] + a * s[j]);
       }
+    } else {
+      o1 = x1;
+      o2 = x2;
     }
-  } else {
-    bf16* vdst = v_cache + ((size_t)blk * hkv + (h - hq - hkv)) * d * bs + off;   // [d][bs] block of this head
-    for (int e = lane; e < d; e += 64) vdst[(size_t)e * bs] = src[e];
+    bf16* dst;
+    if (h < hq) {
+      dst = q_out + ((size_t)t * hq + h) * d;
+    } else {
+      dst = k_cache + (((size_t)blk * hkv + (h - hq)) * bs + off) * d;
+    }
+    *reinterpret_cast<bf16x4*>(dst + p) = o1;
+    *reinterpret_cast<bf16x4*>(dst + half + p) = o2;
+  }
+  // v: transposed store into [blk][h][d][bs]
+  const bf16* vsrc = row + (hq + hkv) * d;
+  for (int i = threadIdx.x; i < hkv * d; i += blockDim.x) {
+    const int h = i / d, e = i % d;
+    v_cache[(((size_t)blk * hkv + h) * d + e) * bs + off] = vsrc[i];
   }
 }
 
 void rope_cache_append(uintptr_t q_out, uintptr_t qkv, uintptr_t positions, uintptr_t cos_sin,
                        uintptr_t k_cache, uintptr_t v_cache, uintptr_t slots, int tokens, int hq, int hkv,
                        int d, int bs, uintptr_t stream) {
-  DLLM_HOST_CHECK(d % 2 == 0 && d <= 256, "head_dim must be even, <= 256");
+  DLLM_HOST_CHECK(d % 8 == 0 && d <= 256, "head_dim must be a multiple of 8, <= 256");
   DLLM_HOST_CHECK(hq % hkv == 0, "Hq % Hkv");
   if (tokens == 0) return;
-  dim3 grid(tokens, (hq + 2 * hkv + 3) / 4);
-  hipLaunchKernelGGL(rope_cache_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(rope_cache_kernel, dim3(tokens), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      (bf16*)q_out, (const bf16*)qkv, (const int32_t*)positions, (const float*)cos_sin,
                      (bf16*)k_cache, (bf16*)v_cache, (const int32_t*)slots, hq, hkv, d, bs);
   DLLM_HIP_CHECK(hipGetLastError());

@@ -11,6 +11,7 @@ import torch
 
 from ..config import EngineConfig, ModelConfig
 from ..models.stage import KVCache, ModelStage
+from ..utils.tracing import get_tracer
 from .batch import HostBatch, to_device_meta
 from .graphs import DecodeGraphRunner
 
@@ -46,6 +47,7 @@ class StageRunner:
                  num_slots: int = 1):
         self.stage = stage
         self.ecfg = ecfg
+        self.tracer = get_tracer()
         self.block_size = ecfg.kv_block_size
         nb = num_blocks or plan_kv_blocks(stage.cfg, stage.num_layers, ecfg, stage.device)
         stage.allocate_kv(nb, self.block_size)
@@ -67,6 +69,15 @@ class StageRunner:
 
     @torch.inference_mode()
     def execute(self, hb: HostBatch, hidden: Optional[torch.Tensor] = None, slot: int = 0) -> torch.Tensor:
+        tr = self.tracer
+        if not tr.enabled:
+            return self._execute(hb, hidden, slot)
+        kind = "prefill" if hb.is_prefill else "decode"
+        gspan = tr.gpu_span(kind, cat="stage") if self.stage.device.type == "cuda" else tr.span(kind, cat="stage")
+        with tr.span(f"stage.{kind}", cat="host", rows=hb.num_tokens, seqs=hb.num_seqs, slot=slot), gspan:
+            return self._execute(hb, hidden, slot)
+
+    def _execute(self, hb: HostBatch, hidden: Optional[torch.Tensor], slot: int) -> torch.Tensor:
         st = self.stage
         gr = self.graph_sets[slot % len(self.graph_sets)] if self.graph_sets else None
         if (not hb.is_prefill) and gr is not None and gr.can_run(hb.num_seqs, hb.max_ctx):

@@ -18,7 +18,7 @@ def _sync(ctx):
     dist.barrier(group=ctx.ctrl_group)
 
 
-def run_distributed(args, emit, make_prompts):
+def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=None):
     pp = None if args.parallelism == "pp" else 1
     ctx = init_distributed(pp=pp)
     world = ctx.world
@@ -48,6 +48,7 @@ def run_distributed(args, emit, make_prompts):
     for r in range(args.warmup):
         one_round(10_000 + r)
     _sync(ctx)
+    tr = start_trace(args) if start_trace else None
     lat = []
     t0 = time.perf_counter()
     for r in range(args.steps):
@@ -61,12 +62,18 @@ def run_distributed(args, emit, make_prompts):
     obj = [None] * world
     dist.all_gather_object(obj, lat, group=ctx.ctrl_group)
     all_lat = [x for part in obj for x in part]
+    busy = None
+    if tr is not None:
+        busy = [None] * world
+        dist.all_gather_object(busy, finish_trace(args, tr, elapsed, ctx.rank), group=ctx.ctrl_group)
     if ctx.rank == 0:
         extra = {"load_s": round(load_s, 1), "stage_ranges": role.plan.to_json()["ranges"],
                  "backend": dist.get_backend()}
         if role.driver is not None:
             extra["driver_stall_s"] = round(role.driver.stall_s, 3)
         extra["microbatch_slots"] = slots
+        if busy is not None:
+            extra["stage_busy_frac"] = busy
         emit(args, world, elapsed, all_lat, extra, global_batch=per_pipe * ctx.dp)
     role.shutdown()
     _sync(ctx)

@@ -29,6 +29,7 @@ from ..engine.runner import StageRunner
 from ..engine.sampler import sample
 from ..engine.scheduler import Scheduler, Step
 from ..engine.sequence import SamplingParams, Sequence
+from ..utils.tracing import get_tracer
 from .comm import STOP, Transport
 
 log = logging.getLogger("dllm.pipeline")
@@ -87,6 +88,7 @@ def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_e
     h = st.cfg.hidden_size
     last = transport.stage == transport.num_stages - 1
     ret = _TokenReturn(transport, runner.ecfg.max_batch, st.device) if last else None
+    tr = get_tracer()
     while True:
         arr = transport.recv_meta()
         if arr.shape[0] == 1 and arr[0] in _MARKERS:
@@ -102,12 +104,14 @@ def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_e
         hb = HostBatch.unpack(arr)
         if not last:
             transport.send_meta(arr)          # let the next stage post its receive early
-        hidden = transport.recv_hidden(hb.num_tokens, h, st.dtype, st.device)
+        with tr.span("pp.recv_hidden", cat="comm", step=hb.step_id):
+            hidden = transport.recv_hidden(hb.num_tokens, h, st.dtype, st.device)
         out = runner.execute(hb, hidden)
         if last:
             ret.push(hb.step_id, sample(out, **hb.sampling_args()))
         else:
-            transport.send_hidden(out)
+            with tr.span("pp.send_hidden", cat="comm", step=hb.step_id):
+                transport.send_hidden(out)
 
 
 class PipelineDriver:
@@ -164,7 +168,8 @@ class PipelineDriver:
             self._flushed = True
         step, sid = self.inflight.popleft()
         t0 = time.perf_counter()
-        arr = self.t.recv_tokens()
+        with get_tracer().span("pp.wait_tokens", cat="comm", step=sid):
+            arr = self.t.recv_tokens()
         self.stall_s += time.perf_counter() - t0
         if int(arr[0]) != sid or int(arr[1]) != len(step.seqs):
             raise RuntimeError(f"pipeline out of order: got step {arr[0]} n={arr[1]}, expected {sid}")

@@ -164,6 +164,8 @@ class Tracer:
     def utilization(self, wall_s: float, cat: str = "gpu") -> Dict[str, float]:
         """Device busy fraction of a category over a wall-clock window; 1 - busy = bubble."""
         busy = self.gpu_busy_ms(cat) / 1e3
+        if busy == 0.0:   # CPU stages: host spans of that category are the busy time
+            busy = sum(e["dur"] for e in self.events() if e.get("cat") == cat and e.get("ph") == "X") / 1e6
         frac = busy / wall_s if wall_s > 0 else 0.0
         return {"busy_s": busy, "wall_s": wall_s, "busy_frac": frac, "bubble_frac": max(0.0, 1.0 - frac)}
 

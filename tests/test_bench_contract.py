@@ -26,13 +26,15 @@ def _json_lines(out):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("n,par", [(2, "pp"), (3, "pp"), (2, "dp")])
-def test_torchrun_bench_cpu(n, par):
+@pytest.mark.parametrize("n,par,trace", [(2, "pp", True), (3, "pp", False), (2, "dp", False)])
+def test_torchrun_bench_cpu(n, par, trace, tmp_path):
     env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(n), "--steps", "1", "--warmup", "1", "--model", "tiny-llama", "--batch", "3",
            "--prompt-len", "6", "--gen-len", "4", "--parallelism", par]
+    if trace:
+        cmd += ["--trace", str(tmp_path)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
@@ -43,6 +45,9 @@ def test_torchrun_bench_cpu(n, par):
     if par == "pp":
         assert rec["microbatch_slots"] == n + 1
         assert rec["config"]["global_batch"] == 3 * (n + 1)
+    if trace:   # every rank wrote a timeline; every stage reports its busy fraction
+        assert sorted(os.listdir(tmp_path)) == [f"trace_rank{r}.json" for r in range(n)]
+        assert len(rec["stage_busy_frac"]) == n and all(0 < b <= 1.0 for b in rec["stage_busy_frac"])
 
 
 def test_single_process_bench_json_cpu():
