@@ -42,11 +42,11 @@ __global__ void __launch_bounds__(512, 1) gemm_skinny_kernel(bf16* __restrict__ 
     int n0;
     if (EPI == EPI_SWIGLU) n0 = (nt < NT / 2 ? 0 : up_off) + blockIdx.x * (BN / 2) + (nt % (NT / 2)) * 16;
     else n0 = blockIdx.x * BN + nt * 16;
-    wrow[nt] = w + (size_t)(n0 + r) * K + 32 * g;
+    wrow[nt] = w + (size_t)(n0 + r) * K + 8 * g;
   }
   const bf16* xrow[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) xrow[mt] = x + (size_t)min(mt * 16 + r, M - 1) * K + 32 * g;
+  for (int mt = 0; mt < MT; ++mt) xrow[mt] = x + (size_t)min(mt * 16 + r, M - 1) * K + 8 * g;
 
   const int ngroups = K >> 7;   // 128-wide k-groups
   const int per = (ngroups + kSkWaves - 1) / kSkWaves;

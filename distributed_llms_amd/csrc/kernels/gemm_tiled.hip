@@ -35,7 +35,17 @@ __global__ void __launch_bounds__(256, 2) gemm_tiled_kernel(const bf16* __restri
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE_ELEMS];   // [buf][A|B][128][64]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
-  const int n0 = blockIdx.x * TBN, m0 = blockIdx.y * TBM, split = blockIdx.z;
+  // 1-D grid, XCD-aware: hardware dispatches block b to XCD b % 8, so logical tile
+  // (b % 8) * (total / 8) + b / 8 gives each XCD a contiguous run of logical ids; M is the
+  // fastest logical axis, so the M tiles that share a W tile run back-to-back on ONE XCD and
+  // the second reads W from that XCD's L2 instead of HBM.
+  const int mtiles = (M + TBM - 1) / TBM, total = gridDim.x;
+  int b = blockIdx.x;
+  if ((total & 7) == 0) b = (b & 7) * (total >> 3) + (b >> 3);
+  const int m_t = b % mtiles, rest = b / mtiles;
+  const int nsplit = total / (mtiles * (N / TBN));
+  const int split = rest % nsplit, n_t = rest / nsplit;
+  const int n0 = n_t * TBN, m0 = m_t * TBM;
   const int kb = split * k_per_split;
   const int ke = min(K, kb + k_per_split);
   const int nt = max(0, (ke - kb) / TBK);
@@ -156,7 +166,7 @@ void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int kps = (K / TBK + splits - 1) / splits * TBK;
   const int S = (K + kps - 1) / kps;
-  dim3 grid(N / TBN, (M + TBM - 1) / TBM, S);
+  dim3 grid((N / TBN) * ((M + TBM - 1) / TBM) * S);
   if (S == 1 && mode == 0 && bias == 0) {
     hipLaunchKernelGGL(gemm_tiled_kernel<false>, grid, dim3(256), 0, s, (const bf16*)a, (const bf16*)b, (bf16*)c,
                        (float*)nullptr, M, N, K, kps);

@@ -79,14 +79,58 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16* __restrict_
 constexpr int MOE_EPI_STORE = 0;
 constexpr int MOE_EPI_SWIGLU = 1;
 
-// y[slot, :] for the rows of expert blockIdx.y.  x rows: gather ? x[gather[slot]] : x[slot].
-template <int NT, int EPI>
-__global__ void __launch_bounds__(512, 1) moe_grouped_kernel(bf16* __restrict__ y, const bf16* __restrict__ x,
-                                                             const int* __restrict__ gather,
-                                                             const bf16* __restrict__ w, const int* __restrict__ counts,
-                                                             const int* __restrict__ offsets, int N, int K, int ldy) {
-  constexpr int MT = 4, BM = 64, BN = NT * 16;
-  __shared__ __attribute__((aligned(16))) float red[BM * BN];
+// Rows [0, cnt) of one expert in chunks of MT*16 rows; every chunk streams the WG's W column
+// tile once (K split over the WAVES waves, partial tiles summed through LDS).
+template <int MT, int NT, int WAVES, int EPI>
+__device__ __forceinline__ void moe_rows(float* red, bf16* __restrict__ y, const bf16* __restrict__ x,
+                                         const int* __restrict__ gather, const bf16* const (&wrow)[NT], int cnt,
+                                         int off, int K, int ldy, int g0, int g1, int lane) {
+  constexpr int BM = MT * 16, BN = NT * 16, NTHR = WAVES * 64;
+  const int r = lane & 15, g = lane >> 4;
+  for (int r0 = 0; r0 < cnt; r0 += BM) {
+    const int rows = min(BM, cnt - r0);
+    for (int i = threadIdx.x; i < BM * BN; i += NTHR) red[i] = 0.f;
+    const bf16* xrow[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int slot = off + r0 + min(mt * 16 + r, rows - 1);
+      const int src = gather ? gather[slot] : slot;
+      xrow[mt] = x + (size_t)src * K + 8 * g;
+    }
+    f32x4 acc[MT][NT];
+    sk_mainloop<MT, NT>(acc, xrow, wrow, g0, g1);
+    __syncthreads();
+    sk_reduce_lds<MT, NT>(red, acc, lane);
+    __syncthreads();
+    if (EPI == MOE_EPI_SWIGLU) {
+      constexpr int HB = BN / 2;
+      for (int q = threadIdx.x; q < rows * HB; q += NTHR) {
+        const int m = q / HB, c = q % HB;
+        y[(size_t)(off + r0 + m) * ldy + blockIdx.x * HB + c] = f2bf(silu_f(red[m * BN + c]) * red[m * BN + HB + c]);
+      }
+    } else {
+      for (int q = threadIdx.x; q < rows * BN; q += NTHR) {
+        const int m = q / BN, c = q % BN;
+        y[(size_t)(off + r0 + m) * ldy + blockIdx.x * BN + c] = f2bf(red[m * BN + c]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Grouped expert GEMM: grid (N / (NT*16), E).  The row tile is chosen PER EXPERT from its
+// actual count (a workgroup-uniform branch): 16-row tiles for <= 16 rows, 32 for <= 32, else
+// MTMAX*16-row chunks -- so routing imbalance never makes an expert re-stream its weights
+// while it fits one chunk, and a decode expert with 10 rows does not gather 64.
+template <int MTMAX, int NT, int WAVES, int EPI>
+__global__ void __launch_bounds__(WAVES * 64, 1) moe_grouped_kernel(bf16* __restrict__ y, const bf16* __restrict__ x,
+                                                                    const int* __restrict__ gather,
+                                                                    const bf16* __restrict__ w,
+                                                                    const int* __restrict__ counts,
+                                                                    const int* __restrict__ offsets, int N, int K,
+                                                                    int ldy) {
+  constexpr int BN = NT * 16;
+  __shared__ __attribute__((aligned(16))) float red[MTMAX * 16 * BN];
   const int e = blockIdx.y;
   const int cnt = counts[e];
   if (cnt == 0) return;                       // uniform across the workgroup
@@ -100,39 +144,16 @@ __global__ void __launch_bounds__(512, 1) moe_grouped_kernel(bf16* __restrict__ 
     int n0;
     if (EPI == MOE_EPI_SWIGLU) n0 = (nt < NT / 2 ? 0 : N / 2) + blockIdx.x * (BN / 2) + (nt % (NT / 2)) * 16;
     else n0 = blockIdx.x * BN + nt * 16;
-    wrow[nt] = we + (size_t)(n0 + r) * K + 32 * g;
+    wrow[nt] = we + (size_t)(n0 + r) * K + 8 * g;
   }
   const int ngroups = K >> 7;
-  const int per = (ngroups + kSkWaves - 1) / kSkWaves;
+  const int per = (ngroups + WAVES - 1) / WAVES;
   const int g0 = wv * per, g1 = min(ngroups, g0 + per);
-  for (int r0 = 0; r0 < cnt; r0 += BM) {
-    const int rows = min(BM, cnt - r0);
-    for (int i = threadIdx.x; i < BM * BN; i += 512) red[i] = 0.f;
-    const bf16* xrow[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int slot = off + r0 + min(mt * 16 + r, rows - 1);
-      const int src = gather ? gather[slot] : slot;
-      xrow[mt] = x + (size_t)src * K + 32 * g;
-    }
-    f32x4 acc[MT][NT];
-    sk_mainloop<MT, NT>(acc, xrow, wrow, g0, g1);
-    __syncthreads();
-    sk_reduce_lds<MT, NT>(red, acc, lane);
-    __syncthreads();
-    if (EPI == MOE_EPI_SWIGLU) {
-      constexpr int HB = BN / 2;
-      for (int q = threadIdx.x; q < rows * HB; q += 512) {
-        const int m = q / HB, c = q % HB;
-        y[(size_t)(off + r0 + m) * ldy + blockIdx.x * HB + c] = f2bf(silu_f(red[m * BN + c]) * red[m * BN + HB + c]);
-      }
-    } else {
-      for (int q = threadIdx.x; q < rows * BN; q += 512) {
-        const int m = q / BN, c = q % BN;
-        y[(size_t)(off + r0 + m) * ldy + blockIdx.x * BN + c] = f2bf(red[m * BN + c]);
-      }
-    }
-    __syncthreads();
+  if (MTMAX == 1 || cnt <= 16) {
+    moe_rows<1, NT, WAVES, EPI>(red, y, x, gather, wrow, cnt, off, K, ldy, g0, g1, lane);
+  } else if constexpr (MTMAX >= 2) {
+    if (MTMAX == 2 || cnt <= 32) moe_rows<2, NT, WAVES, EPI>(red, y, x, gather, wrow, cnt, off, K, ldy, g0, g1, lane);
+    else if constexpr (MTMAX >= 4) moe_rows<4, NT, WAVES, EPI>(red, y, x, gather, wrow, cnt, off, K, ldy, g0, g1, lane);
   }
 }
 
@@ -166,20 +187,46 @@ void moe_route(uintptr_t logits, int T, int E, int k, uintptr_t topk_w, uintptr_
   DLLM_HIP_CHECK(hipGetLastError());
 }
 
-// mode 1 (SwiGLU): w [E, 2I, K] -> y [T*k, I]; mode 0: w [E, N, K] -> y [T*k, N]
-void moe_grouped_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets,
-                      int E, int N, int K, int mode, uintptr_t stream) {
-  DLLM_HOST_CHECK(K % 128 == 0, "K % 128");
-  DLLM_HOST_CHECK(N % 32 == 0, "N % 32");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+template <int MTMAX, int NT, int WAVES>
+static void launch_grouped(hipStream_t s, bf16* y, const bf16* x, const int* gather, const bf16* w, const int* counts,
+                           const int* offsets, int E, int N, int K, int mode) {
+  constexpr int BN = NT * 16;
   if (mode == 1) {
-    hipLaunchKernelGGL((moe_grouped_kernel<2, MOE_EPI_SWIGLU>), dim3(N / 2 / 16, E), dim3(512), 0, s, (bf16*)y,
-                       (const bf16*)x, (const int*)gather, (const bf16*)w, (const int*)counts,
-                       (const int*)offsets, N, K, N / 2);
+    DLLM_HOST_CHECK(N % BN == 0, "moe grouped: 2I must be a multiple of the column tile");
+    hipLaunchKernelGGL((moe_grouped_kernel<MTMAX, NT, WAVES, MOE_EPI_SWIGLU>), dim3(N / BN, E), dim3(WAVES * 64), 0,
+                       s, y, x, gather, w, counts, offsets, N, K, N / 2);
   } else {
-    hipLaunchKernelGGL((moe_grouped_kernel<2, MOE_EPI_STORE>), dim3(N / 32, E), dim3(512), 0, s, (bf16*)y,
-                       (const bf16*)x, (const int*)gather, (const bf16*)w, (const int*)counts,
-                       (const int*)offsets, N, K, N);
+    DLLM_HOST_CHECK(N % BN == 0, "moe grouped: N must be a multiple of the column tile");
+    hipLaunchKernelGGL((moe_grouped_kernel<MTMAX, NT, WAVES, MOE_EPI_STORE>), dim3(N / BN, E), dim3(WAVES * 64), 0, s,
+                       y, x, gather, w, counts, offsets, N, K, N);
+  }
+}
+
+// mode 1 (SwiGLU): w [E, 2I, K] -> y [T*k, I]; mode 0: w [E, N, K] -> y [T*k, N].
+// rows_hint = expected rows per expert (T*k/E) picks the kernel family; variant > 0 forces one
+// (benchmarking: 1 = <1,4,8>, 2 = <2,4,8>, 3 = <4,2,8>, 4 = <2,4,4>, 5 = <4,4,4>, 6 = <2,2,8>).
+void moe_grouped_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets,
+                      int E, int N, int K, int mode, int rows_hint, int variant, uintptr_t stream) {
+  DLLM_HOST_CHECK(K % 128 == 0, "K % 128");
+  DLLM_HOST_CHECK(N % 64 == 0, "N % 64");   // every column tile (32 or 64) divides N
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  auto args = [&](auto f) {
+    f(s, (bf16*)y, (const bf16*)x, (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, E, N,
+      K, mode);
+  };
+  // measured (bench/moe_bench.py, Mixtral shapes): 4-wave <4,4,4> is best or tied at every
+  // decode token count -- 4.4 TB/s at T=16, 3.8 at T=64, 3.0 at T=128 -- the 8-wave forms
+  // spill and split K too finely (profiles/moe_grouped_variants.txt)
+  (void)rows_hint;
+  if (variant <= 0) variant = 5;
+  switch (variant) {
+    case 1: args(launch_grouped<1, 4, 8>); break;
+    case 2: args(launch_grouped<2, 4, 8>); break;
+    case 3: args(launch_grouped<4, 2, 8>); break;
+    case 4: args(launch_grouped<2, 4, 4>); break;
+    case 5: args(launch_grouped<4, 4, 4>); break;
+    case 6: args(launch_grouped<2, 2, 8>); break;
+    default: DLLM_HOST_CHECK(false, "moe grouped: unknown variant");
   }
   DLLM_HIP_CHECK(hipGetLastError());
 }

@@ -2,7 +2,10 @@
 // (gemm_skinny.hip) and the Mixtral grouped expert GEMM (moe.hip).
 //
 // v_mfma_f32_16x16x32_bf16 fragments, k permuted inside each 128-wide k-group identically
-// for X and W so each lane loads 64 contiguous bytes per operand row (4 x dwordx4).
+// for X and W (a dot product is order-invariant): load i of lane (r, g) reads elements
+// 32*i + 8*g .. +7 of row r, so ONE wave-instruction reads 64 contiguous bytes of each of
+// 16 rows (16 half-lines) rather than 16 B from each of 32 lines (the first layout, 8*i + 32*g),
+// halving the lines the texture path touches per instruction.  Row pointers carry the +8*g.
 #pragma once
 #include "common.h"
 
@@ -17,13 +20,13 @@ __device__ __forceinline__ void sk_load(bf16x8 (&xa)[MT][4], bf16x8 (&wb)[NT][4]
   for (int nt = 0; nt < NT; ++nt) {
     const bf16x8* p = reinterpret_cast<const bf16x8*>(wrow[nt] + k);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) wb[nt][i] = __builtin_nontemporal_load(p + i);
+    for (int i = 0; i < 4; ++i) wb[nt][i] = __builtin_nontemporal_load(p + 4 * i);
   }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const bf16x8* p = reinterpret_cast<const bf16x8*>(xrow[mt] + k);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xa[mt][i] = p[i];
+    for (int i = 0; i < 4; ++i) xa[mt][i] = p[4 * i];
   }
 }
 

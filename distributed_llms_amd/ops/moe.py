@@ -11,6 +11,8 @@ CPU path: the PyTorch reference (ops/reference.py).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -18,6 +20,8 @@ from .. import _ext
 from . import reference as ref
 
 GROUPED_MAX_TOKENS = 256      # beyond this the per-expert row count makes library GEMMs cheaper
+# 0 = pick by expected rows per expert; 1..6 force a kernel variant (bench/moe_bench.py sweeps them)
+GROUPED_VARIANT = int(os.environ.get("DLLM_MOE_VARIANT", "0"))
 
 
 def route(router_logits: torch.Tensor, top_k: int):
@@ -54,10 +58,11 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     ys = torch.empty(t * top_k, h, dtype=x.dtype, device=dev)
     if t <= GROUPED_MAX_TOKENS:
         act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
+        rows = -(-t * top_k // e)        # expected rows per expert picks the kernel's row tile
         k.moe_grouped_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
-                           counts.data_ptr(), offsets.data_ptr(), e, two_i, h, 1, st)
+                           counts.data_ptr(), offsets.data_ptr(), e, two_i, h, 1, rows, GROUPED_VARIANT, st)
         k.moe_grouped_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), counts.data_ptr(),
-                           offsets.data_ptr(), e, h, inter, 0, st)
+                           offsets.data_ptr(), e, h, inter, 0, rows, GROUPED_VARIANT, st)
     else:
         xs = x.index_select(0, sorted_tok.long())
         off = offsets.cpu().tolist()          # prefill only: eager, host sync is fine here

@@ -28,9 +28,11 @@ def test_moe_forward(cuda, t, e, k, h, i):
     torch.testing.assert_close(out.float(), expect, atol=3e-2, rtol=3e-2)
 
 
-def test_moe_skewed_routing_multi_chunk(cuda):
-    """All tokens routed to the same experts: > 64 rows per expert exercises the row-chunk loop."""
-    t, e, k, h, i = 150, 8, 2, 256, 256
+@pytest.mark.parametrize("t", [40, 100, 150])
+def test_moe_skewed_routing_multi_chunk(cuda, t):
+    """All tokens routed to the same two experts: far more rows per expert than the row tile the
+    expected count selected (t*k/e -> 16/32/64-row tiles) exercises the row-chunk loop."""
+    e, k, h, i = 8, 2, 256, 256
     x = _bf(t, h)
     wr = torch.zeros(e, h, device="cuda", dtype=torch.bfloat16)
     wr[3] = 0.05
