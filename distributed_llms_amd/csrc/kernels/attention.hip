@@ -26,33 +26,42 @@ struct WaveState {
   float lsum;   // lane-partial softmax denominator
 };
 
-// Process one 32-key chunk (one KV block) for the wave's 16 columns.
-//   kmax_col : last admissible key index for this lane's column (causal / range), inclusive
+// One 32-key chunk's operands, loaded into registers: K rows as two 16-key A tiles, V^T as
+// the A fragments of the P.V MFMA (two 8-byte halves per lane, k-order permuted to match P).
 template <int D>
-__device__ __forceinline__ void attend_chunk(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
-                                             const bf16* __restrict__ kblk, const bf16* __restrict__ vblk,
-                                             int t0, int kmax_col, float scale_log2, int lane) {
-  const int r = lane & 15, g = lane >> 4;
-  // Issue every K and V load of the chunk before any math: V does not depend on the scores,
-  // so its HBM latency overlaps K's instead of following the softmax.
+struct KVChunk {
   bf16x8 ka[D / 32], kb[D / 32];
   bf16x4 vlo[D / 16], vhi[D / 16];
+};
+
+template <int D>
+__device__ __forceinline__ void load_chunk(KVChunk<D>& c, const bf16* __restrict__ kblk,
+                                           const bf16* __restrict__ vblk, int lane) {
+  const int r = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
-    ka[ks] = *reinterpret_cast<const bf16x8*>(kblk + r * D + ks * 32 + 8 * g);
-    kb[ks] = *reinterpret_cast<const bf16x8*>(kblk + (16 + r) * D + ks * 32 + 8 * g);
+    c.ka[ks] = *reinterpret_cast<const bf16x8*>(kblk + r * D + ks * 32 + 8 * g);
+    c.kb[ks] = *reinterpret_cast<const bf16x8*>(kblk + (16 + r) * D + ks * 32 + 8 * g);
   }
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt) {
     const bf16* vr = vblk + (dt * 16 + r) * kBS;
-    vlo[dt] = *reinterpret_cast<const bf16x4*>(vr + 4 * g);
-    vhi[dt] = *reinterpret_cast<const bf16x4*>(vr + 16 + 4 * g);
+    c.vlo[dt] = *reinterpret_cast<const bf16x4*>(vr + 4 * g);
+    c.vhi[dt] = *reinterpret_cast<const bf16x4*>(vr + 16 + 4 * g);
   }
+}
+
+// Online-softmax update of the wave's 16 columns with one loaded chunk.
+//   kmax_col : last admissible key index for this lane's column (causal / range), inclusive
+template <int D>
+__device__ __forceinline__ void compute_chunk(WaveState<D>& st, const bf16x8 (&qf)[D / 32], const KVChunk<D>& c,
+                                              int t0, int kmax_col, float scale_log2, int lane) {
+  const int g = lane >> 4;
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
-    s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[ks], qf[ks], s0, 0, 0, 0);
-    s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[ks], qf[ks], s1, 0, 0, 0);
+    s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.ka[ks], qf[ks], s0, 0, 0, 0);
+    s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.kb[ks], qf[ks], s1, 0, 0, 0);
   }
   float p[8];
   float cm = -INFINITY;
@@ -84,12 +93,22 @@ __device__ __forceinline__ void attend_chunk(WaveState<D>& st, const bf16x8 (&qf
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt) {
     st.acc[dt] *= alpha;
-    const bf16x4 lo = vlo[dt], hi = vhi[dt];
+    const bf16x4 lo = c.vlo[dt], hi = c.vhi[dt];
     bf16x8 va;
     va[0] = lo[0]; va[1] = lo[1]; va[2] = lo[2]; va[3] = lo[3];
     va[4] = hi[0]; va[5] = hi[1]; va[6] = hi[2]; va[7] = hi[3];
     st.acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, st.acc[dt], 0, 0, 0);
   }
+}
+
+// Load + compute one chunk (prefill: its chunks are issued by 4 waves in turn).
+template <int D>
+__device__ __forceinline__ void attend_chunk(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
+                                             const bf16* __restrict__ kblk, const bf16* __restrict__ vblk,
+                                             int t0, int kmax_col, float scale_log2, int lane) {
+  KVChunk<D> c;
+  load_chunk<D>(c, kblk, vblk, lane);
+  compute_chunk<D>(st, qf, c, t0, kmax_col, scale_log2, lane);
 }
 
 template <int D>
@@ -101,27 +120,32 @@ __device__ __forceinline__ void init_state(WaveState<D>& st) {
 }
 
 // ---------------------------------------------------------------------------
-// Decode: grid (num_splits, Hkv, B); 4 waves split the WG's key range by chunk,
-// then combine through LDS. num_splits > 1 writes (o, m, l) partials for the
-// split-reduce kernel below.
+// Decode: grid (num_splits, Hkv / WPB, B), WPB waves per workgroup, ONE wave per
+// (split, kv-head, sequence).  The wave walks its split's chunks with a depth-2 software
+// pipeline -- chunk c+1's K/V loads are in flight while chunk c's MFMAs and softmax run --
+// and the chunk -> block ids come from one lane-parallel load of the block-table row
+// (read back with readlane), so the only dependent HBM latency per chunk is the KV
+// stream itself.  No LDS, no barrier.  num_splits > 1 writes (o, m, l) partials for the
+// split-reduce kernel below.  (The first version used 4 waves per (split, head, seq) with
+// chunks round-robin, no cross-chunk prefetch and an LDS combine: 47 us per layer at
+// B=256 / ctx 128-256 on Llama-3-8B, profiles/llama3_8b_b256_kernels_auto.md.)
 // ---------------------------------------------------------------------------
-template <int D>
-__global__ void __launch_bounds__(256) attn_decode_kernel(
+template <int D, int WPB>
+__global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg: min waves per SIMD
     bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
     const int32_t* __restrict__ seq_lens, float* __restrict__ part_o, float* __restrict__ part_ml,
     int hq, int hkv, int max_blocks, int split_len, float scale_log2) {
-  __shared__ float sm_o[kWaves][D][16];
-  __shared__ float sm_m[kWaves][16];
-  __shared__ float sm_l[kWaves][16];
-  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int split = blockIdx.x, b = blockIdx.z;
+  const int lane = threadIdx.x & 63;
+  const int kvh = blockIdx.y * WPB + (threadIdx.x >> 6);
   const int nsplit = gridDim.x;
   const int G = hq / hkv;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int ctx = seq_lens[b];
   const int kbeg = split * split_len;
   const int kend = min(kbeg + split_len, ctx);  // exclusive
+  const int c0 = kbeg / kBS, c1 = (kend + kBS - 1) / kBS;
 
   // Q^T fragments: column r = head kvh*G + r (zero beyond G)
   bf16x8 qf[D / 32];
@@ -138,43 +162,53 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   const int kmax = kend - 1;
   const size_t kv_head_stride = (size_t)kBS * D;
   const int32_t* bt = block_tables + (size_t)b * max_blocks;
-  for (int c = kbeg / kBS + w; c * kBS < kend; c += kWaves) {
-    const int blk = bt[c];
-    const size_t base = ((size_t)blk * hkv + kvh) * kv_head_stride;
-    attend_chunk<D>(st, qf, k_cache + base, v_cache + base, c * kBS, kmax, scale_log2, lane);
+  const size_t head_off = (size_t)kvh * kv_head_stride;
+  const size_t blk_stride = (size_t)hkv * kv_head_stride;
+  for (int cb = c0; cb < c1; cb += 64) {            // 64 chunks (2048 keys) of block ids per pass
+    const int n = min(64, c1 - cb);
+    const int my_blk = lane < n ? bt[cb + lane] : 0;
+    KVChunk<D> cur, nxt;
+    {
+      const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, 0) * blk_stride + head_off;
+      load_chunk<D>(cur, k_cache + base, v_cache + base, lane);
+    }
+    int j = 0;
+    for (; j + 2 <= n; j += 2) {                    // ping-pong: cur <-> nxt
+      {
+        const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, j + 1) * blk_stride + head_off;
+        load_chunk<D>(nxt, k_cache + base, v_cache + base, lane);
+      }
+      compute_chunk<D>(st, qf, cur, (cb + j) * kBS, kmax, scale_log2, lane);
+      if (j + 2 < n) {
+        const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, j + 2) * blk_stride + head_off;
+        load_chunk<D>(cur, k_cache + base, v_cache + base, lane);
+      }
+      compute_chunk<D>(st, qf, nxt, (cb + j + 1) * kBS, kmax, scale_log2, lane);
+    }
+    if (j < n) compute_chunk<D>(st, qf, cur, (cb + j) * kBS, kmax, scale_log2, lane);
   }
   float lt = st.lsum;
   lt += __shfl_xor(lt, 16, 64);
   lt += __shfl_xor(lt, 32, 64);
-  // stage this wave's (m, l, O^T) into LDS
-  if (g == 0) { sm_m[w][r] = st.m; sm_l[w][r] = lt; }
+  if (!col_ok) return;                              // after the last MFMA: divergence is safe
+  const int h = kvh * G + r;
+  if (nsplit == 1) {
+    // a true division, exactly as the split-reduce computes num / den (bit-identical results
+    // whether a sequence's keys land in one split or in one non-empty split of several)
+    bf16* orow = out + ((size_t)b * hq + h) * D;
 #pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt)
+    for (int dt = 0; dt < D / 16; ++dt) {
+      bf16x4 o;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sm_o[w][dt * 16 + 4 * g + i][r] = st.acc[dt][i];
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < D * G; idx += blockDim.x) {
-    const int c = idx % G, d = idx / G;
-    float M = -INFINITY;
-#pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) M = fmaxf(M, sm_m[ww][c]);
-    float num = 0.f, den = 0.f;
-    if (M != -INFINITY) {
-#pragma unroll
-      for (int ww = 0; ww < kWaves; ++ww) {
-        const float f = exp2f(sm_m[ww][c] - M);
-        num += sm_o[ww][d][c] * f;
-        den += sm_l[ww][c] * f;
-      }
+      for (int i = 0; i < 4; ++i) o[i] = f2bf(lt > 0.f ? st.acc[dt][i] / lt : 0.f);
+      *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = o;
     }
-    const int h = kvh * G + c;
-    if (nsplit == 1) {
-      out[((size_t)b * hq + h) * D + d] = f2bf(den > 0.f ? num / den : 0.f);
-    } else {
-      const size_t pi = ((size_t)b * hq + h) * nsplit + split;
-      part_o[pi * D + d] = num;
-      if (d == 0) { part_ml[pi * 2] = M; part_ml[pi * 2 + 1] = den; }
-    }
+  } else {
+    const size_t pi = ((size_t)b * hq + h) * nsplit + split;
+    float* po = part_o + pi * D;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) *reinterpret_cast<f32x4*>(po + dt * 16 + 4 * g) = st.acc[dt];
+    if (g == 0) { part_ml[pi * 2] = st.m; part_ml[pi * 2 + 1] = lt; }
   }
 }
 
@@ -268,17 +302,23 @@ void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintp
   if (batch == 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float sl2 = scale * 1.4426950408889634f;
-  dim3 grid(num_splits, hkv, batch);
-  if (d == 128)
-    hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,
-                       (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)block_tables,
-                       (const int32_t*)seq_lens, (float*)part_o, (float*)part_ml, hq, hkv, max_blocks,
-                       split_len, sl2);
-  else
-    hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,
-                       (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)block_tables,
-                       (const int32_t*)seq_lens, (float*)part_o, (float*)part_ml, hq, hkv, max_blocks,
-                       split_len, sl2);
+  // one wave per kv head; pack up to 4 heads (independent waves) per workgroup
+  const int wpb = hkv % 4 == 0 ? 4 : hkv % 2 == 0 ? 2 : 1;
+  dim3 grid(num_splits, hkv / wpb, batch);
+  auto go = [&](auto kern, int threads) {
+    hipLaunchKernelGGL(kern, grid, dim3(threads), 0, s, (bf16*)out, (const bf16*)q, (const bf16*)k_cache,
+                       (const bf16*)v_cache, (const int32_t*)block_tables, (const int32_t*)seq_lens, (float*)part_o,
+                       (float*)part_ml, hq, hkv, max_blocks, split_len, sl2);
+  };
+  if (d == 128) {
+    if (wpb == 4) go(attn_decode_kernel<128, 4>, 256);
+    else if (wpb == 2) go(attn_decode_kernel<128, 2>, 128);
+    else go(attn_decode_kernel<128, 1>, 64);
+  } else {
+    if (wpb == 4) go(attn_decode_kernel<64, 4>, 256);
+    else if (wpb == 2) go(attn_decode_kernel<64, 2>, 128);
+    else go(attn_decode_kernel<64, 1>, 64);
+  }
   DLLM_HIP_CHECK(hipGetLastError());
   if (num_splits > 1) {
     if (d == 128)

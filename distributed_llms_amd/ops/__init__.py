@@ -161,19 +161,21 @@ def rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, n
 
 # ---------------------------------------------------------- K6 / K7
 def decode_split_plan(batch: int, num_kv_heads: int, max_ctx: int, block_size: int = 32,
-                      target_wgs: int = 512) -> Tuple[int, int]:
-    """(num_splits, split_len) for the decode kernel.
+                      max_blocks: Optional[int] = None, target_waves: int = 2048) -> Tuple[int, int]:
+    """(num_splits, split_len) for the decode kernel (one wave per split x kv-head x sequence).
 
-    Enough workgroups to fill 256 CUs several times over, each split a multiple of
-    4 waves x 32 keys; fixed for a given (batch, max_ctx) bucket so graphs can replay.
+    Aim for ~8 waves per CU (256 CUs) with >= 2 KV blocks per split so each wave's load
+    pipeline has something to overlap.  The split BOUNDARIES depend only on the pow2-bucketed
+    batch x kv-heads and on the block-table width -- not on ``max_ctx`` -- so a graph replayed
+    at a padded (batch, context) bucket and the eager path partition every sequence's keys
+    identically: the extra splits of the bucket are empty and add exact zeros, and the two
+    paths produce bit-identical attention.
     """
-    chunk = 4 * block_size
-    max_splits = max(1, -(-max_ctx // chunk))
-    want = max(1, -(-target_wgs // max(1, batch * num_kv_heads)))
-    splits = min(want, max_splits, 64)
-    split_len = -(-max_ctx // splits)
-    split_len = -(-split_len // block_size) * block_size
-    splits = -(-max_ctx // split_len)
+    max_blocks = max_blocks or -(-max_ctx // block_size)
+    pairs = 1 << max(0, (max(1, batch * num_kv_heads) - 1).bit_length())
+    target = max(1, min(64, target_waves // pairs))
+    split_len = block_size * max(2, -(-max_blocks // target))
+    splits = max(1, -(-max_ctx // split_len))
     return splits, split_len
 
 
@@ -193,7 +195,7 @@ def paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale: f
         max_ctx = max_blocks * bs
     if max_ctx > max_blocks * bs:
         raise ValueError("max_ctx exceeds block table capacity")
-    splits, split_len = decode_split_plan(b, hkv, max_ctx, bs)
+    splits, split_len = decode_split_plan(b, hkv, max_ctx, bs, max_blocks)
     out = torch.empty_like(q)
     po = pml = 0
     if splits > 1:

@@ -42,6 +42,8 @@ class DistTransport(Transport):
     """One pipeline = ranks ``ranks[0..pp-1]`` (global ranks), stage = index in that list."""
 
     def __init__(self, ranks, stage: int, ctrl_group=None, data_group=None):
+        """``data_group`` None = the default group (RCCL on GPU).  A gloo ``data_group`` with GPU
+        stages means host-staged activations (D2H -> gloo -> H2D): the TCP fallback."""
         self.ranks = list(ranks)
         self.stage = stage
         self.num_stages = len(self.ranks)
@@ -99,15 +101,20 @@ class DistTransport(Transport):
     def send_hidden(self, t: torch.Tensor):
         # copy: `t` may be a graph's static output that the next replay overwrites while the
         # send (on the comm stream) is still reading it
-        t = t.clone(memory_format=torch.contiguous_format)
+        if t.is_cuda and self.data is not None and dist.get_backend(self.data) == "gloo":
+            t = t.to("cpu")                      # host-staged fallback (synchronous D2H)
+        else:
+            t = t.clone(memory_format=torch.contiguous_format)
         w = dist.isend(t, self.next, group=self.data)
         self._pending.append((w, t))
         self._reap()
 
     def recv_hidden(self, rows, hidden, dtype, device):
-        buf = torch.empty(rows, hidden, dtype=dtype, device=device)
+        staged = torch.device(device).type == "cuda" and self.data is not None \
+            and dist.get_backend(self.data) == "gloo"
+        buf = torch.empty(rows, hidden, dtype=dtype, device="cpu" if staged else device)
         dist.recv(buf, self.prev, group=self.data)
-        return buf
+        return buf.to(device) if staged else buf
 
     def drain(self):
         for w, _ in self._pending:

@@ -34,6 +34,11 @@ class DistContext:
     pp: int
     ctrl_group: object
     device: str
+    data_group: object = None      # None = the default (RCCL) group
+
+    @property
+    def host_staged(self) -> bool:
+        return self.data_group is not None
 
     @property
     def pipeline_id(self) -> int:
@@ -51,25 +56,35 @@ class DistContext:
 
 def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
                      timeout_s: float = 1800) -> DistContext:
+    """Environment knobs (tests / rehearsal only):
+      DLLM_SHARE_GPU=1       ranks share the visible GPUs round-robin (local_rank % device_count)
+      DLLM_DATA_BACKEND=gloo activations go host-staged over a gloo group instead of RCCL -- the
+                             cross-host TCP fallback, and the only way to run several GPU ranks on
+                             one device (RCCL refuses: "Duplicate GPU detected")."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = torch.cuda.is_available() and backend != "gloo"
+    dev_idx = local_rank
+    if use_gpu and os.environ.get("DLLM_SHARE_GPU", "0") == "1":
+        dev_idx = local_rank % max(1, torch.cuda.device_count())
+    host_staged = use_gpu and os.environ.get("DLLM_DATA_BACKEND", "") == "gloo"
     if use_gpu:
-        torch.cuda.set_device(local_rank)
-    backend = backend or ("nccl" if use_gpu else "gloo")
+        torch.cuda.set_device(dev_idx)
+    backend = backend or ("gloo" if host_staged else "nccl" if use_gpu else "gloo")
+    tmo = datetime.timedelta(seconds=timeout_s)
     if not dist.is_initialized():
-        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=tmo)
         if backend == "nccl":
-            kw["device_id"] = torch.device("cuda", local_rank)
+            kw["device_id"] = torch.device("cuda", dev_idx)
         dist.init_process_group(**kw)
-    ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s)) if backend != "gloo" \
-        else dist.group.WORLD
+    ctrl = dist.new_group(backend="gloo", timeout=tmo) if backend != "gloo" else dist.group.WORLD
+    data = dist.new_group(backend="gloo", timeout=tmo) if host_staged else None
     pp = pp or world
     if world % pp:
         raise ValueError(f"world {world} not divisible by pp {pp}")
     return DistContext(rank, world, local_rank, world // pp, pp, ctrl,
-                       f"cuda:{local_rank}" if use_gpu else "cpu")
+                       f"cuda:{dev_idx}" if use_gpu else "cpu", data)
 
 
 def agree_min(ctx: DistContext, value: int) -> int:
@@ -105,7 +120,8 @@ class RankRole:
             self.engine = LLMEngine(ecfg1, stage)
         else:
             self.runner = StageRunner(stage, ecfg, num_blocks=nb)
-            self.transport = DistTransport(ctx.pipeline_ranks, ctx.stage, ctrl_group=ctx.ctrl_group)
+            self.transport = DistTransport(ctx.pipeline_ranks, ctx.stage, ctrl_group=ctx.ctrl_group,
+                                           data_group=ctx.data_group)
             if ctx.stage == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.runner, self.transport, ecfg, bm)
