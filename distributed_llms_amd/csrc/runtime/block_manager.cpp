@@ -58,6 +58,19 @@ class BlockManager {
     return true;
   }
 
+  // Grow every sequence i to lens[i] tokens, in order; returns the index of the first one that
+  // does not fit (nothing allocated for it or after it), or -1 when all fit.  One call per
+  // decode step instead of one per sequence.
+  int64_t ensure_capacity_batch(py::array_t<int64_t, py::array::c_style> seqs,
+                                py::array_t<int64_t, py::array::c_style> lens) {
+    auto s = seqs.unchecked<1>();
+    auto l = lens.unchecked<1>();
+    if (s.shape(0) != l.shape(0)) throw std::invalid_argument("seqs/lens length mismatch");
+    for (py::ssize_t i = 0; i < s.shape(0); ++i)
+      if (!ensure_capacity(s(i), l(i))) return i;
+    return -1;
+  }
+
   void free_sequence(int64_t seq) {
     auto it = tables_.find(seq);
     if (it == tables_.end()) return;
@@ -130,6 +143,7 @@ void register_block_manager(py::module_& m) {
       .def("extra_blocks_needed", &BlockManager::extra_blocks_needed)
       .def("can_fit", &BlockManager::can_fit)
       .def("ensure_capacity", &BlockManager::ensure_capacity)
+      .def("ensure_capacity_batch", &BlockManager::ensure_capacity_batch)
       .def("free_sequence", &BlockManager::free_sequence)
       .def("block_table", &BlockManager::block_table)
       .def("fill_block_tables", &BlockManager::fill_block_tables, py::arg("seqs"), py::arg("out"),

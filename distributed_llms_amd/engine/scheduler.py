@@ -12,8 +12,11 @@ running sequence of that slot is preempted (blocks freed, recomputed later).
 from __future__ import annotations
 
 import collections
+import time
 from dataclasses import dataclass
 from typing import Deque, Dict, List, Optional
+
+import numpy as np
 
 from .sequence import Sequence, SeqStatus
 
@@ -104,17 +107,19 @@ class Scheduler:
                 return Step(True, admitted, slot)
         if not running:
             return None
-        # decode: every running sequence of the slot needs room for one more token
+        # decode: every running sequence of the slot needs room for one more token (one native
+        # call for the whole slot; on failure preempt the youngest and retry from there)
         i = 0
         while i < len(running):
-            seq = running[i]
-            if self.bm.ensure_capacity(seq.seq_id, seq.total_len):
-                i += 1
-                continue
+            rest = running[i:]
+            ids = np.fromiter((s.seq_id for s in rest), dtype=np.int64, count=len(rest))
+            lens = np.fromiter((len(s.prompt) + len(s.output) for s in rest), dtype=np.int64, count=len(rest))
+            bad = self.bm.ensure_capacity_batch(ids, lens)
+            if bad < 0:
+                break
+            i += bad
             victim = running.pop()  # youngest
             self._preempt(victim)
-            if victim is seq:
-                continue
         if not running:
             return None
         return Step(False, list(running), slot)
@@ -131,13 +136,18 @@ class Scheduler:
         """Apply sampled tokens of an executed step; returns sequences that finished."""
         done = []
         running = self.running[step.slot]
+        if hasattr(tokens, "tolist"):
+            tokens = tokens.tolist()      # python ints once, not a numpy scalar per sequence
+        now = time.perf_counter() if now is None else now
+        prefill = step.is_prefill
         for seq, tok in zip(step.seqs, tokens):
-            if seq.finished:      # aborted while in flight
+            st = seq.status
+            if st is SeqStatus.FINISHED or st is SeqStatus.ABORTED:   # aborted while in flight
                 continue
-            seq.num_cached = seq.total_len
-            if step.is_prefill:
+            seq.num_cached = len(seq.prompt) + len(seq.output)
+            if prefill:
                 running.append(seq)
-            if seq.append(int(tok), now) or seq.total_len >= self.max_seq_len:
+            if seq.append(tok, now) or seq.num_cached + 1 >= self.max_seq_len:
                 if not seq.finished:
                     seq.finish("max_seq_len", now)
                 if seq in running:

@@ -80,7 +80,7 @@ class Sequence:
     def append(self, tok: int, now: Optional[float] = None) -> bool:
         """Append a generated token; returns True if the sequence just finished."""
         now = time.perf_counter() if now is None else now
-        self.output.append(int(tok))
+        self.output.append(tok if type(tok) is int else int(tok))
         self.token_times.append(now)
         if self.first_token_time is None:
             self.first_token_time = now
