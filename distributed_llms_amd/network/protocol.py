@@ -114,6 +114,33 @@ class MessageProtocol:
         # the reference took a pyzmq context; the transport here is plain TCP
         self.zmq_context = zmq_context
 
+    # socket "types" of the reference's setup_zmq_socket (src/network/protocol.py:27-36), mapped
+    # to TCP roles.  The reference bound only PUB/PUSH/REP, so its ROUTER master connected to
+    # nobody; here every server-side type binds and every client-side type connects.
+    SERVER_TYPES = ("ROUTER", "REP", "PUB", "PUSH", "SERVER")
+    CLIENT_TYPES = ("REQ", "DEALER", "SUB", "PULL", "CLIENT")
+
+    def setup_zmq_socket(self, socket_type: str, address: str, timeout: Optional[float] = 10.0,
+                         backlog: int = 64) -> socket.socket:
+        """``address`` like ``tcp://host:port``.  Server types return a listening socket (accept
+        connections yourself); client types return a connected stream socket."""
+        kind = str(socket_type).upper()
+        hostport = address.split("://", 1)[-1]
+        host, _, port = hostport.rpartition(":")
+        host = host.strip("[]") or "0.0.0.0"
+        if kind in self.SERVER_TYPES:
+            s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            s.bind(("0.0.0.0" if host == "*" else host, int(port)))
+            s.listen(backlog)
+            return s
+        if kind in self.CLIENT_TYPES:
+            s = socket.create_connection((host, int(port)), timeout=timeout)
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            s.settimeout(None)
+            return s
+        raise ValueError(f"unknown socket type {socket_type!r}")
+
     @staticmethod
     def _lock_for(sock) -> threading.Lock:
         key = id(sock)

@@ -132,3 +132,31 @@ def test_python_codec_matches_native():
     assert nat.encode_frame_head(7, 0, h, 123) == py.encode_frame_head(7, 0, h, 123)
     assert tuple(nat.decode_frame_prefix(py.encode_frame_head(7, 0, h, 123)[:24])) == \
         py.decode_frame_prefix(py.encode_frame_head(7, 0, h, 123)[:24])
+
+
+def test_setup_zmq_socket_binds_servers_and_connects_clients():
+    """Reference API (src/network/protocol.py:27-36) with D1 fixed: ROUTER binds, REQ connects."""
+    import threading
+    mp = MessageProtocol()
+    srv = mp.setup_zmq_socket("ROUTER", "tcp://127.0.0.1:0")
+    port = srv.getsockname()[1]
+    got = {}
+
+    def serve():
+        conn, _ = srv.accept()
+        got["msg"] = MessageProtocol.receive_message(conn, timeout=10)
+        MessageProtocol.send_message(conn, "REGISTER_ACK", metadata={"worker_id": 7})
+        conn.close()
+
+    t = threading.Thread(target=serve)
+    t.start()
+    cli = mp.setup_zmq_socket("REQ", f"tcp://127.0.0.1:{port}")
+    assert MessageProtocol.send_message(cli, "REGISTER", metadata={"capabilities": {"device": "cpu"}})
+    hdr, _ = MessageProtocol.receive_message(cli, timeout=10)
+    t.join(10)
+    cli.close()
+    srv.close()
+    assert got["msg"][0]["command"] == "REGISTER" and hdr["worker_id"] == 7
+    import pytest
+    with pytest.raises(ValueError):
+        mp.setup_zmq_socket("BOGUS", "tcp://127.0.0.1:1")
