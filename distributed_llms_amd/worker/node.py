@@ -532,10 +532,20 @@ class WorkerNode:
         self._serve_thread = None
         self.stage_runner = None
         if self._dist_ctx is not None:
+            # membership changed (a peer died or the master re-planned): ABORT the communicators
+            # first (ncclCommAbort under RCCL) so collectives/p2p still pending against a dead
+            # peer return instead of hanging, then destroy; the next LOAD_SHARD re-initialises
             try:
                 import torch.distributed as dist
+                from torch.distributed import distributed_c10d as c10d
                 if dist.is_initialized():
-                    dist.destroy_process_group()
+                    if send_stop is False and hasattr(c10d, "_abort_process_group"):
+                        try:
+                            c10d._abort_process_group()
+                        except Exception:
+                            pass
+                    if dist.is_initialized():
+                        dist.destroy_process_group()
             except Exception:
                 pass
             self._dist_ctx = None
