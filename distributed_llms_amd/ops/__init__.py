@@ -160,8 +160,11 @@ def rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, n
 
 
 # ---------------------------------------------------------- K6 / K7
+DECODE_TARGET_WAVES = 1024     # waves the decode split plan aims for (sweep: profiles/attn_decode_sweep.txt)
+
+
 def decode_split_plan(batch: int, num_kv_heads: int, max_ctx: int, block_size: int = 32,
-                      max_blocks: Optional[int] = None, target_waves: int = 2048) -> Tuple[int, int]:
+                      max_blocks: Optional[int] = None, target_waves: Optional[int] = None) -> Tuple[int, int]:
     """(num_splits, split_len) for the decode kernel (one wave per split x kv-head x sequence).
 
     Aim for ~8 waves per CU (256 CUs) with >= 2 KV blocks per split so each wave's load
@@ -171,6 +174,7 @@ def decode_split_plan(batch: int, num_kv_heads: int, max_ctx: int, block_size: i
     identically: the extra splits of the bucket are empty and add exact zeros, and the two
     paths produce bit-identical attention.
     """
+    target_waves = target_waves or DECODE_TARGET_WAVES
     max_blocks = max_blocks or -(-max_ctx // block_size)
     pairs = 1 << max(0, (max(1, batch * num_kv_heads) - 1).bit_length())
     target = max(1, min(64, target_waves // pairs))
