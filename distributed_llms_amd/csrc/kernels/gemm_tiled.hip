@@ -155,6 +155,92 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16* __restrict__ o
   }
 }
 
+// Split-K reduce fused into the NEXT op of a Llama block: residual add + RMSNorm.
+//   h = bf16(sum_s P[s, row, :]);  r = bf16(h + residual);  residual <- r;  y = rmsnorm(r) * w
+// Bit-identical to splitk_reduce_kernel followed by rms_norm_kernel with a residual (same
+// per-element summation order, same thread -> vector mapping for the sum of squares), minus one
+// launch and the bf16 h round trip through HBM.  One 256-thread workgroup per row.
+template <int MAXV>
+__global__ void __launch_bounds__(256) splitk_add_rms_norm_kernel(bf16* __restrict__ y, bf16* __restrict__ residual,
+                                                                  const float* __restrict__ P, int S, int M, int N,
+                                                                  const bf16* __restrict__ w, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const int nvec = N >> 3;
+  const size_t slab = (size_t)M * N;
+  bf16x8* rr = reinterpret_cast<bf16x8*>(residual + (size_t)row * N);
+  float v[MAXV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int idx = threadIdx.x + i * 256;
+    if (idx < nvec) {
+      const float* p = P + (size_t)row * N + idx * 8;
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < S; ++s) {
+        a0 += *reinterpret_cast<const f32x4*>(p + s * slab);
+        a1 += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
+      }
+      const bf16x8 b = rr[idx];
+      bf16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float h = bf2f(f2bf(j < 4 ? a0[j] : a1[j - 4]));
+        r[j] = f2bf(h + bf2f(b[j]));
+      }
+      rr[idx] = r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = bf2f(r[j]);
+        ss += v[i][j] * v[i][j];
+      }
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)N + eps);
+  const bf16x8* wv = reinterpret_cast<const bf16x8*>(w);
+  bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)row * N);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int idx = threadIdx.x + i * 256;
+    if (idx < nvec) {
+      const bf16x8 g = wv[idx];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(g[j]));
+      yr[idx] = o;
+    }
+  }
+}
+
+void splitk_add_rms_norm(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, int M, int N, uintptr_t w, float eps,
+                         uintptr_t stream) {
+  DLLM_HOST_CHECK(N % 8 == 0 && N <= 8 * 256 * 8, "hidden must be a multiple of 8 and <= 16384");
+  DLLM_HOST_CHECK(S >= 1 && M >= 0, "S >= 1");
+  if (M == 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(M), dim3(256), 0, s, (bf16*)y, (bf16*)residual, (const float*)ws, S, M, N,
+                       (const bf16*)w, eps);
+  };
+  const int nvec = N / 8;
+  if (nvec <= 256) go(splitk_add_rms_norm_kernel<1>);
+  else if (nvec <= 512) go(splitk_add_rms_norm_kernel<2>);
+  else if (nvec <= 1024) go(splitk_add_rms_norm_kernel<4>);
+  else go(splitk_add_rms_norm_kernel<8>);
+  DLLM_HIP_CHECK(hipGetLastError());
+}
+
+// plain split-K reduce of partials left by gemm_tiled(mode 2): out = bf16(sum_s P[s]) (+bias)
+void splitk_reduce(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M, int N, uintptr_t stream) {
+  long blocks = ((long)M * N / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) return;
+  hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3((unsigned)blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (bf16*)out, (const float*)ws, (const bf16*)bias, S, M, N);
+  DLLM_HIP_CHECK(hipGetLastError());
+}
+
 // mode 0: C[M,N] = A B^T (+bias);  mode 1 (SwiGLU): C[M, N/2] = silu(A Bg^T) * (A Bu^T), B = [Bg; Bu]
 void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t ws, long ws_floats, int M, int N,
                 int K, int splits, int mode, uintptr_t stream) {
@@ -162,11 +248,12 @@ void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t
   DLLM_HOST_CHECK(N % TBN == 0, "N must be a multiple of 128");
   DLLM_HOST_CHECK(K % TBK == 0, "K must be a multiple of 64");
   DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
-  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");   // 2: leave f32 partials in ws, no reduce
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int kps = (K / TBK + splits - 1) / splits * TBK;
   const int S = (K + kps - 1) / kps;
   dim3 grid((N / TBN) * ((M + TBM - 1) / TBM) * S);
+  DLLM_HOST_CHECK(mode != 2 || S > 1, "mode 2 needs a K split");
   if (S == 1 && mode == 0 && bias == 0) {
     hipLaunchKernelGGL(gemm_tiled_kernel<false>, grid, dim3(256), 0, s, (const bf16*)a, (const bf16*)b, (bf16*)c,
                        (float*)nullptr, M, N, K, kps);
@@ -177,6 +264,7 @@ void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t
   hipLaunchKernelGGL(gemm_tiled_kernel<true>, grid, dim3(256), 0, s, (const bf16*)a, (const bf16*)b, (bf16*)nullptr,
                      (float*)ws, M, N, K, kps);
   DLLM_HIP_CHECK(hipGetLastError());
+  if (mode == 2) return;
   const int ncols = mode == 1 ? N / 2 : N;
   long blocks = ((long)M * ncols / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;

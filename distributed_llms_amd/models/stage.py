@@ -184,7 +184,8 @@ class ModelStage:
         if self.cfg.is_moe:
             return ops.moe_forward(h, lw["router"], lw["experts_gate_up"], lw["experts_down"],
                                    self.cfg.experts_per_token)
-        return ops.linear(ops.linear_swiglu(h, lw["w_gate_up"]), lw["w_down"])
+        # defer: the down projection's split-K reduce is fused into the next residual-add + RMSNorm
+        return ops.linear(ops.linear_swiglu(h, lw["w_gate_up"]), lw["w_down"], defer=True)
 
     def _units(self):
         for u in range(self.unit_start, self.unit_end):
@@ -207,6 +208,8 @@ class ModelStage:
                 h = ops.linear(a, lw["wo"])
             else:
                 h = self._mlp(x, lw)
+        if isinstance(h, ops.gemm.SplitKPartial):
+            h = h.materialize()
         if not self.is_last:
             return ops.add_(residual, h)
         return self._logits(h, residual, meta)

@@ -16,6 +16,7 @@ from typing import Optional, Tuple
 import torch
 
 from .. import _ext
+from . import gemm
 from . import reference as ref
 
 __all__ = [
@@ -66,7 +67,19 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
 
 def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
                        eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
-    """residual <- x + residual (in place); returns (rms_norm(residual) * w, residual)."""
+    """residual <- x + residual (in place); returns (rms_norm(residual) * w, residual).
+
+    ``x`` may be a :class:`gemm.SplitKPartial` (split-K GEMM output not yet reduced): the
+    reduction then happens inside the same kernel (splitk_add_rms_norm)."""
+    if isinstance(x, gemm.SplitKPartial):
+        _ck(residual, "fused_add_rms_norm.residual")
+        _ck(w, "fused_add_rms_norm.w")
+        if tuple(x.shape) != tuple(residual.shape):
+            raise ValueError("x/residual shape mismatch")
+        y = torch.empty_like(residual)
+        _ext.kernels().splitk_add_rms_norm(y.data_ptr(), residual.data_ptr(), x.ws.data_ptr(), x.splits, x.m, x.n,
+                                           w.data_ptr(), float(eps), _stream())
+        return y, residual
     if not _gpu(x):
         return ref.fused_add_rms_norm(x, residual, w, eps)
     _ck(x, "fused_add_rms_norm.x")
@@ -91,12 +104,12 @@ def gelu_tanh(x):
 
 
 # --------------------------------------------------------------- GEMM
-def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = x @ w^T (+bias). w is [N, K]."""
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, defer: bool = False):
+    """y = x @ w^T (+bias). w is [N, K].  ``defer`` (GPU): the result may come back as a
+    :class:`gemm.SplitKPartial` for ``fused_add_rms_norm`` to reduce (or ``materialize()``)."""
     if not _gpu(x):
         return ref.linear(x, w, bias)
-    from . import gemm
-    return gemm.linear(x, w, bias)
+    return gemm.linear(x, w, bias, defer=defer)
 
 
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:

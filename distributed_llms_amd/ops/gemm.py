@@ -50,8 +50,35 @@ def _use_tiled(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool
     return GEMM_MODE == "tiled" or k >= 8192
 
 
+class SplitKPartial:
+    """f32 split-K partial sums of ``x @ w.T`` still in the per-stream workspace (not reduced).
+
+    Returned by ``linear(..., defer=True)`` when the split-K tiled kernel ran, so the NEXT op can
+    fuse the reduction (``ops.fused_add_rms_norm`` -> splitk_add_rms_norm); anything else calls
+    :meth:`materialize`.  Valid only until the next tiled GEMM on the same stream reuses the
+    workspace -- consume it immediately."""
+
+    __slots__ = ("ws", "splits", "m", "n", "shape", "dtype", "device")
+
+    def __init__(self, ws, splits, m, n, shape, dtype, device):
+        self.ws, self.splits, self.m, self.n = ws, splits, m, n
+        self.shape, self.dtype, self.device = shape, dtype, device
+
+    def materialize(self) -> torch.Tensor:
+        y = torch.empty(self.shape, dtype=self.dtype, device=self.device)
+        _ext.kernels().splitk_reduce(y.data_ptr(), self.ws.data_ptr(), 0, self.splits, self.m, self.n,
+                                     torch.cuda.current_stream().cuda_stream)
+        return y
+
+
+def _effective_splits(k: int, splits: int) -> int:
+    kps = -(-(k // 64) // splits) * 64            # same rounding as csrc/kernels/gemm_tiled.hip
+    return -(-k // kps)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
-           force_skinny: bool = False) -> torch.Tensor:
+           force_skinny: bool = False, defer: bool = False):
+    """y = x w^T (+bias).  ``defer``: may return a :class:`SplitKPartial` (see there)."""
     k = x.shape[-1]
     n = w.shape[0]
     m = x.numel() // k
@@ -62,6 +89,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         _launch(x, w, bias, y, m, n, k, 0)
         return y
     if _use_tiled(m, n, k, x, w) and (bias is None or bias.dtype == torch.bfloat16):
+        if defer and bias is None:
+            return linear_tiled(x, w, None, defer=True)
         return linear_tiled(x, w, bias)
     return F.linear(x, w, bias)
 
@@ -85,7 +114,7 @@ def tiled_splits(m: int, n: int, k: int, target_wgs: int = 512) -> int:
 
 
 def linear_tiled(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, splits: int = 0,
-                 swiglu: bool = False) -> torch.Tensor:
+                 swiglu: bool = False, defer: bool = False):
     """Split-K LDS-tiled MFMA GEMM (csrc/kernels/gemm_tiled.hip) for decode-sized M."""
     k = x.shape[-1]
     n = w.shape[0]
@@ -100,6 +129,11 @@ def linear_tiled(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     ws = _workspace(x.device)
     if s * m * n > ws.numel():
         s = max(1, ws.numel() // (m * n))
+    if defer and not swiglu and bias is None and _effective_splits(k, s) > 1:
+        se = _effective_splits(k, s)
+        _ext.kernels().gemm_tiled(0, x.data_ptr(), w.data_ptr(), 0, ws.data_ptr(), ws.numel(), m, n, k, s, 2,
+                                  torch.cuda.current_stream().cuda_stream)
+        return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
     _ext.kernels().gemm_tiled(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0 if bias is None else bias.data_ptr(),
                               ws.data_ptr(), ws.numel(), m, n, k, s, 1 if swiglu else 0,
                               torch.cuda.current_stream().cuda_stream)

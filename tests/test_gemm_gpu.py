@@ -78,3 +78,29 @@ def test_tiled_swiglu_and_bias(cuda, m):
     b = _bf(1024)
     y2 = gemm.linear_tiled(x, w, bias=b, splits=2)
     torch.testing.assert_close(y2.float(), gu + b.float(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 4096, 14336), (96, 1024, 8192)])
+def test_deferred_splitk_fused_add_rms_norm_bit_exact(cuda, m, n, k):
+    """linear(defer=True) -> fused_add_rms_norm reduces the split-K partials inside the norm
+    kernel; it must equal reduce-then-norm bit for bit, and match the fp32 reference."""
+    from distributed_llms_amd import ops
+    from distributed_llms_amd.ops import gemm
+    from distributed_llms_amd.ops import reference as ref
+    torch.manual_seed(0)
+    x = (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16)
+    w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(n, device="cuda")).to(torch.bfloat16)
+    res0 = torch.randn(m, n, device="cuda").to(torch.bfloat16)
+    p = ops.linear(x, w, defer=True)
+    assert isinstance(p, gemm.SplitKPartial) and p.splits > 1
+    r1 = res0.clone()
+    y1, _ = ops.fused_add_rms_norm(p, r1, g, 1e-5)
+    p2 = ops.linear(x, w, defer=True)
+    h = p2.materialize()
+    r2 = res0.clone()
+    y2, _ = ops.fused_add_rms_norm(h, r2, g, 1e-5)
+    assert torch.equal(y1, y2) and torch.equal(r1, r2)
+    torch.testing.assert_close(h.float(), ref.linear(x.float(), w.float()), atol=2e-2, rtol=2e-2)
+    yr, rr = ref.fused_add_rms_norm(h.float(), res0.float(), g.float(), 1e-5)
+    torch.testing.assert_close(y1.float(), yr, atol=3e-2, rtol=3e-2)
