@@ -11,6 +11,7 @@ import torch
 
 from ..config import EngineConfig, ModelConfig
 from ..models.stage import KVCache, ModelStage
+from ..ops.tuning import enable_tuned_gemms
 from ..utils.tracing import get_tracer
 from .batch import HostBatch, to_device_meta
 from .graphs import DecodeGraphRunner
@@ -48,6 +49,8 @@ class StageRunner:
         self.stage = stage
         self.ecfg = ecfg
         self.tracer = get_tracer()
+        if stage.device.type == "cuda":
+            enable_tuned_gemms()          # before any graph capture fixes the GEMM solutions
         self.block_size = ecfg.kv_block_size
         nb = num_blocks or plan_kv_blocks(stage.cfg, stage.num_layers, ecfg, stage.device)
         stage.allocate_kv(nb, self.block_size)
