@@ -2,6 +2,7 @@
 
 ``_C_kernels``  HIP/CDNA4 kernels for gfx950 (csrc/kernels/*.hip), pybind11 module.
 ``_C_runtime``  host C++ runtime: paged-KV block manager, wire-frame codec (csrc/runtime).
+``_C_rccl``     native RCCL p2p transport (csrc/comm).
 
 Both are built in-tree by ``python -m distributed_llms_amd.csrc.build`` (also run by
 ``__graft_entry__.build()``).  GPU ops never fall back silently: if the kernel module is
@@ -50,6 +51,22 @@ def runtime():
                 "distributed_llms_amd._C_runtime is not built: "
                 f"{e}. Run `python -m distributed_llms_amd.csrc.build`.") from e
     return _runtime
+
+
+_rccl = None
+
+
+def rccl():
+    """The native RCCL p2p module; raises if it is not built."""
+    global _rccl
+    if _rccl is None:
+        try:
+            _rccl = _import("_C_rccl")
+        except ImportError as e:
+            raise RuntimeError(
+                "distributed_llms_amd._C_rccl is not built (or failed to load): "
+                f"{e}. Run `python -m distributed_llms_amd.csrc.build`.") from e
+    return _rccl
 
 
 def has_kernels() -> bool:

@@ -6,6 +6,8 @@
   plus the pybind11 binding TU, linked into ``distributed_llms_amd/_C_kernels<EXT_SUFFIX>``.
 * ``_C_runtime``: host-only C++17 (``csrc/runtime/*.cpp``), paged-KV block manager and
   wire-frame codec, linked into ``distributed_llms_amd/_C_runtime<EXT_SUFFIX>``.
+* ``_C_rccl``: native RCCL p2p transport (``csrc/comm/rccl_p2p.cpp``), linked against
+  ``librccl.so.1`` -- at run time the copy PyTorch already loaded (one RCCL per process).
 
 Objects go to ``build/`` (git-ignored); the ``.so`` files land in the package
 directory so they travel to the GPU box with the repo snapshot.
@@ -106,8 +108,23 @@ def build_runtime(force=False, jobs=8, verbose=False) -> str:
     return target
 
 
+def build_comm(force=False, jobs=8, verbose=False) -> str:
+    src = os.path.join(HERE, "comm", "rccl_p2p.cpp")
+    out_dir = os.path.join(BUILD, "comm")
+    os.makedirs(out_dir, exist_ok=True)
+    obj = os.path.join(out_dir, "rccl_p2p.o")
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    if force or _stale(obj, [src]):
+        _run([CXX, "-c", src, "-o", obj, "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
+              "-D__HIP_PLATFORM_AMD__", f"-I{rocm}/include"] + [f"-I{p}" for p in _py_includes()])
+    target = _ext_path("_C_rccl")
+    if force or _stale(target, [obj]):
+        _run([CXX, "-shared", "-fPIC", "-o", target, obj, f"-L{rocm}/lib", "-lrccl", "-lamdhip64"])
+    return target
+
+
 def build_all(force=False, jobs=8, verbose=False):
-    return build_runtime(force, jobs, verbose), build_kernels(force, jobs, verbose)
+    return build_runtime(force, jobs, verbose), build_kernels(force, jobs, verbose), build_comm(force, jobs, verbose)
 
 
 def main(argv=None):
@@ -115,12 +132,14 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("-v", "--verbose", action="store_true")
-    ap.add_argument("--only", choices=["kernels", "runtime"], default=None)
+    ap.add_argument("--only", choices=["kernels", "runtime", "comm"], default=None)
     a = ap.parse_args(argv)
     if a.only in (None, "runtime"):
         print("built", build_runtime(a.force, a.jobs, a.verbose))
     if a.only in (None, "kernels"):
         print("built", build_kernels(a.force, a.jobs, a.verbose))
+    if a.only in (None, "comm"):
+        print("built", build_comm(a.force, a.jobs, a.verbose))
 
 
 if __name__ == "__main__":

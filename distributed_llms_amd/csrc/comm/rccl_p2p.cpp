@@ -1,0 +1,119 @@
+// N3: native RCCL point-to-point transport for pipeline activations.
+//
+// One communicator per pipeline (rank = stage index), created from a unique id that stage 0
+// generates and the control plane distributes.  send/recv are ncclSend/ncclRecv of raw bytes
+// on a caller-chosen HIP stream -- the pipeline runs them on a dedicated comm stream ordered
+// against the compute stream with HIP events, so a stage's next microbatch never waits behind
+// a transfer, and (because RCCL p2p is graph-capturable) a stage step can later be captured
+// together with its hops.  abort() is ncclCommAbort: pending transfers against a dead peer
+// return instead of hanging (membership change).
+//
+// Links against the librccl.so that PyTorch already loaded (same SONAME), so the process keeps
+// ONE RCCL instance; the header comes from /opt/rocm/include/rccl.
+#include <hip/hip_runtime_api.h>
+#include <pybind11/pybind11.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+
+namespace {
+
+void check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess && r != ncclInProgress)
+    throw std::runtime_error(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(r));
+}
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+py::bytes unique_id() {
+  ncclUniqueId id;
+  check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  return py::bytes(id.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+class RcclComm {
+ public:
+  RcclComm(int nranks, int rank, const std::string& uid, int device) : nranks_(nranks), rank_(rank) {
+    if (uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("unique id must be 128 bytes");
+    if (rank < 0 || rank >= nranks) throw std::invalid_argument("rank out of range");
+    ncclUniqueId id;
+    std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    py::gil_scoped_release nogil;   // init rendezvous blocks until every rank joins
+    check(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+  }
+  ~RcclComm() {
+    if (comm_) ncclCommDestroy(comm_);
+  }
+
+  void send(uintptr_t ptr, long nbytes, int peer, uintptr_t stream) {
+    live();
+    check(ncclSend(reinterpret_cast<const void*>(ptr), (size_t)nbytes, ncclUint8, peer, comm_,
+                   reinterpret_cast<hipStream_t>(stream)), "ncclSend");
+  }
+  void recv(uintptr_t ptr, long nbytes, int peer, uintptr_t stream) {
+    live();
+    check(ncclRecv(reinterpret_cast<void*>(ptr), (size_t)nbytes, ncclUint8, peer, comm_,
+                   reinterpret_cast<hipStream_t>(stream)), "ncclRecv");
+  }
+  // fused exchange (both directions in one group: no ordering deadlock between the two)
+  void sendrecv(uintptr_t sptr, long sbytes, int speer, uintptr_t rptr, long rbytes, int rpeer, uintptr_t stream) {
+    live();
+    check(ncclGroupStart(), "ncclGroupStart");
+    send(sptr, sbytes, speer, stream);
+    recv(rptr, rbytes, rpeer, stream);
+    check(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  void abort() {
+    if (comm_) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+  }
+  void destroy() {
+    if (comm_) {
+      check(ncclCommDestroy(comm_), "ncclCommDestroy");
+      comm_ = nullptr;
+    }
+  }
+  int rank() const { return rank_; }
+  int nranks() const { return nranks_; }
+  bool alive() const { return comm_ != nullptr; }
+
+ private:
+  void live() const {
+    if (!comm_) throw std::runtime_error("RCCL communicator was aborted/destroyed");
+  }
+  ncclComm_t comm_ = nullptr;
+  int nranks_, rank_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_C_rccl, m) {
+  m.doc() = "Native RCCL p2p transport (pipeline activations over xGMI)";
+  m.def("unique_id", &unique_id);
+  m.def("version", []() {
+    int v = 0;
+    ncclGetVersion(&v);
+    return v;
+  });
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init<int, int, const std::string&, int>(), py::arg("nranks"), py::arg("rank"), py::arg("uid"),
+           py::arg("device"))
+      .def("send", &RcclComm::send, py::arg("ptr"), py::arg("nbytes"), py::arg("peer"), py::arg("stream"))
+      .def("recv", &RcclComm::recv, py::arg("ptr"), py::arg("nbytes"), py::arg("peer"), py::arg("stream"))
+      .def("sendrecv", &RcclComm::sendrecv)
+      .def("abort", &RcclComm::abort)
+      .def("destroy", &RcclComm::destroy)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def_property_readonly("alive", &RcclComm::alive);
+}

@@ -87,6 +87,15 @@ def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
                        f"cuda:{dev_idx}" if use_gpu else "cpu", data)
 
 
+def make_transport(ranks, stage: int, ctrl_group, data_group, device: str):
+    """Activation transport for one pipeline stage: torch.distributed's RCCL process group by
+    default; ``DLLM_TRANSPORT=rccl`` selects the native RCCL p2p module (own comm stream)."""
+    if os.environ.get("DLLM_TRANSPORT", "") == "rccl" and data_group is None and str(device).startswith("cuda"):
+        from .rccl_transport import RcclTransport
+        return RcclTransport(ranks, stage, ctrl_group, device)
+    return DistTransport(ranks, stage, ctrl_group=ctrl_group, data_group=data_group)
+
+
 def agree_min(ctx: DistContext, value: int) -> int:
     t = torch.tensor([value], dtype=torch.int64)
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctx.ctrl_group)
@@ -120,8 +129,8 @@ class RankRole:
             self.engine = LLMEngine(ecfg1, stage)
         else:
             self.runner = StageRunner(stage, ecfg, num_blocks=nb)
-            self.transport = DistTransport(ctx.pipeline_ranks, ctx.stage, ctrl_group=ctx.ctrl_group,
-                                           data_group=ctx.data_group)
+            self.transport = make_transport(ctx.pipeline_ranks, ctx.stage, ctx.ctrl_group, ctx.data_group,
+                                            ctx.device)
             if ctx.stage == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.runner, self.transport, ecfg, bm)

@@ -424,8 +424,8 @@ class WorkerNode:
             self._serve_thread = self._spawn(self._serve_loop)
         else:
             self.stage_runner = StageRunner(stage, ecfg, num_blocks=nb)
-            transport = DistTransport(list(range(world)), stage_idx, ctrl_group=ctx.ctrl_group,
-                                      data_group=ctx.data_group)
+            from ..parallel.dist_engine import make_transport
+            transport = make_transport(list(range(world)), stage_idx, ctx.ctrl_group, ctx.data_group, self.device)
             if stage_idx == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.stage_runner, transport, ecfg, bm)
