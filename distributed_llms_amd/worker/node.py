@@ -435,7 +435,11 @@ class WorkerNode:
                 self.role = "follower"
                 self._follower_transport = transport
                 self._serve_thread = self._spawn(self._follower_loop, stage_worker_loop, transport)
-        self._instrument(self.engine.runner if self.engine is not None else self.stage_runner)
+        runner = self.engine.runner if self.engine is not None else self.stage_runner
+        if stage.device.type == "cuda" and ecfg.use_graphs:
+            # capture the decode graphs of the first context bucket now: load time, not first-request time
+            runner.warmup_graphs(ctx_buckets=(min(256, ecfg.max_seq_len),))
+        self._instrument(runner)
         return {"shard_id": int(plan.get("shard_id", stage_idx)), "stage": stage_idx, "layer_range": [a, b],
                 "weight_bytes": stage.weight_bytes(), "kv_blocks": nb, "load_s": round(time.time() - t0, 3),
                 "role": self.role}

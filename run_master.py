@@ -39,6 +39,7 @@ def parse(argv=None):
     ap.add_argument("--auto", action="store_true", help="wait for workers, assign + distribute, no REPL prompt")
     ap.add_argument("--auto-recover", action="store_true", help="re-distribute after a worker failure")
     ap.add_argument("--bench", type=int, default=0, help="with --auto: submit N synthetic requests, print metrics")
+    ap.add_argument("--bench-warmup", type=int, default=1, help="untimed warmup rounds before --bench")
     ap.add_argument("--prompt-len", type=int, default=32)
     ap.add_argument("--gen-len", type=int, default=16)
     ap.add_argument("--wait-timeout", type=float, default=300.0)
@@ -70,6 +71,8 @@ def main(argv=None):
                 rng = np.random.default_rng(0)
                 vocab = master.model_config.vocab_size
                 prompts = rng.integers(3, min(vocab, 30000), size=(a.bench, a.prompt_len)).tolist()
+                for _ in range(a.bench_warmup):     # untimed: first-use costs (graph replays, allocator)
+                    master.generate(prompts, max_new_tokens=a.gen_len, ignore_eos=True)
                 t0 = time.perf_counter()
                 res = master.generate(prompts, max_new_tokens=a.gen_len, ignore_eos=True)
                 el = time.perf_counter() - t0
