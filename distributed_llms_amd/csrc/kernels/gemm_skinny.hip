@@ -11,9 +11,11 @@
 //    profiles/gemm_skinny_v1.txt; guide price list rows splitk-seam / publish-large);
 //  * W and X fragments go straight to VGPRs (operand streamed once, guide "GEMV/M<=16" row);
 //    W with non-temporal loads (read once per step, never re-read from L2/MALL);
-//  * k is permuted inside each 128-wide k-group identically for X and W so that every lane
-//    loads 64 contiguous bytes per operand (4 x dwordx4) and a row's 256 B are covered by
-//    the 4 lane groups -- full 128-B lines per request;
+//  * k is permuted inside each 128-wide k-group identically for X and W (skinny_common.h):
+//    load i of lane (r, g) reads elements 32i + 8g..+7 of row r, so one wave-instruction
+//    covers 64 contiguous bytes of each of 16 rows.  The first layout (8i + 32g) touched 32
+//    lines per instruction and only tied hipBLASLt; this one streams 4-5 TB/s at M <= 4
+//    (profiles/gemm_skinny_v3_vs_hipblaslt.txt);
 //  * waves combine their partial tiles with LDS float atomics (ds_add_f32) into one
 //    [M_pad x BN] f32 tile; the epilogue writes bf16 (+bias), or SwiGLU: the workgroup's two
 //    column tiles are the gate rows n and the up rows I+n of the fused [2I, K] weight.

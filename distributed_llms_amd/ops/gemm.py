@@ -1,7 +1,9 @@
 """Dense GEMM dispatch for y = x @ w^T (w is [N, K], nn.Linear layout).
 
-* M <= 64 (decode): hand-written weight-streaming MFMA kernel (csrc/kernels/gemm_skinny.hip),
-  8 waves per workgroup split K and reduce in LDS; optional fused SwiGLU epilogue.
+* small M (decode, M <= 2..16 by weight size): hand-written weight-streaming MFMA kernel
+  (csrc/kernels/gemm_skinny.hip), 8 waves per workgroup split K and reduce in LDS; optional
+  fused SwiGLU epilogue;
+* 64 <= M <= 512 with K >= 8192: split-K LDS-tiled MFMA kernel (gemm_tiled.hip);
 * larger M (prefill) or shapes the kernel does not tile: plain library GEMM (hipBLASLt via
   torch).  That is the only non-HIP GPU path and it is purely shape-based.
 """
@@ -16,15 +18,29 @@ import torch.nn.functional as F
 from .. import _ext
 
 SKINNY_MAX_M = 64
-# Engine dispatch threshold: the skinny kernel is used for M <= ENGINE_SKINNY_M.  Set from
-# measurements (bench/gemm_bench.py, profiles/gemm_skinny_v2.txt): v2 ties hipBLASLt only at
-# M = 1, so the engine keeps the library GEMM until the kernel wins.
-ENGINE_SKINNY_M = 0
+# Engine dispatch: the weight-streaming kernel serves M <= engine_skinny_max_m(N, K).  Measured
+# against hipBLASLt with cold caches (bench/gemm_bench.py, profiles/gemm_skinny_v3_vs_hipblaslt.txt):
+# with the coalesced k-permutation it streams 4-5 TB/s at M <= 4 and wins 1.4-1.8x on the MLP and
+# big projections, less as M grows; the LM head (N > 64K) stays on hipBLASLt (4.6 TB/s there).
+SKINNY_ENABLED = os.environ.get("DLLM_SKINNY", "1") != "0"
+
+
+def engine_skinny_max_m(n: int, k: int) -> int:
+    if not SKINNY_ENABLED or n > 65536:
+        return 0
+    # in-engine A/B (warm, TunableOp-tuned hipBLASLt, HIP graphs; scripts/gpu_ab_skinny.sh):
+    # B=1 +6.6 %, B=8/16 -1..-4 % with the cold-cache thresholds (16/8/2) -> keep it to M <= 4
+    e = n * k
+    if e >= 50_000_000:       # 8B gate|up (117M) and down (59M), 70B qkv / down / gate|up
+        return 4
+    if e >= 16_000_000:       # 8B o (17M), 8B qkv (25M)
+        return 2
+    return 0
 
 
 def skinny_ok(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False,
               force: bool = False) -> bool:
-    lim = SKINNY_MAX_M if force else ENGINE_SKINNY_M
+    lim = SKINNY_MAX_M if force else engine_skinny_max_m(n, k)
     return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and 1 <= m <= lim
             and k % 128 == 0 and n % (32 if swiglu else 16) == 0 and x.is_contiguous() and w.is_contiguous())
 
@@ -40,6 +56,8 @@ def _launch(x, w, bias, y, m, n, k, mode):
 #                   hipBLASLt elsewhere (ties or wins there)
 #   DLLM_GEMM=tiled / blas  force one implementation (A/B experiments)
 GEMM_MODE = os.environ.get("DLLM_GEMM", "auto")
+#   DLLM_TILED_NMAX=<n>: (auto mode) also route shapes with N <= n to the tiled kernel (A/B knob)
+TILED_NMAX = int(os.environ.get("DLLM_TILED_NMAX", "0"))
 
 
 def _use_tiled(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -47,7 +65,7 @@ def _use_tiled(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool
         return False
     if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
         return False
-    return GEMM_MODE == "tiled" or k >= 8192
+    return GEMM_MODE == "tiled" or k >= 8192 or n <= TILED_NMAX
 
 
 class SplitKPartial:
