@@ -130,12 +130,43 @@ __device__ __forceinline__ void init_state(WaveState<D>& st) {
 // chunks round-robin, no cross-chunk prefetch and an LDS combine: 47 us per layer at
 // B=256 / ctx 128-256 on Llama-3-8B, profiles/llama3_8b_b256_kernels_auto.md.)
 // ---------------------------------------------------------------------------
-template <int D, int WPB>
+// Fused RoPE + KV append (decode only): the wave reads its q heads and the new token's k / v
+// straight from the qkv projection, rotates q and k in registers (pair (e, e + D/2) lives in
+// fragments ks and ks + D/64 of the same lane), writes k and v^T into the paged cache (the
+// split that owns key ctx-1 only), and folds the new key in as a one-key register chunk --
+// the separate rope_cache_kernel launch and the q round trip disappear.
+struct RopeArgs {
+  const bf16* qkv;          // [B, (hq + 2 hkv) * D]
+  const int32_t* positions; // [B]
+  const float* cos_sin;     // [max_pos, D] (first half cos, second half sin) or null (no RoPE)
+  const int32_t* slots;     // [B] cache slot of the new token
+};
+
+template <int D, bool FUSED>
+__device__ __forceinline__ void rope_rotate(bf16x8 (&f)[D / 32], const float* cs, int g) {
+  if (cs == nullptr) return;
+#pragma unroll
+  for (int ks = 0; ks < D / 64; ++ks) {
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + ks * 32 + 8 * g);
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + ks * 32 + 8 * g + 4);
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + D / 2 + ks * 32 + 8 * g);
+    const f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + D / 2 + ks * 32 + 8 * g + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c = j < 4 ? c0[j] : c1[j - 4], s = j < 4 ? s0[j] : s1[j - 4];
+      const float a = bf2f(f[ks][j]), b = bf2f(f[ks + D / 64][j]);
+      f[ks][j] = f2bf(a * c - b * s);
+      f[ks + D / 64][j] = f2bf(b * c + a * s);
+    }
+  }
+}
+
+template <int D, int WPB, bool FUSED>
 __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg: min waves per SIMD
-    bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
-    const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
+    bf16* __restrict__ out, const bf16* __restrict__ q, bf16* __restrict__ k_cache,
+    bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
     const int32_t* __restrict__ seq_lens, float* __restrict__ part_o, float* __restrict__ part_ml,
-    int hq, int hkv, int max_blocks, int split_len, float scale_log2) {
+    int hq, int hkv, int max_blocks, int split_len, float scale_log2, RopeArgs ra) {
   const int split = blockIdx.x, b = blockIdx.z;
   const int lane = threadIdx.x & 63;
   const int kvh = blockIdx.y * WPB + (threadIdx.x >> 6);
@@ -144,19 +175,65 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
   const int r = lane & 15, g = lane >> 4;
   const int ctx = seq_lens[b];
   const int kbeg = split * split_len;
-  const int kend = min(kbeg + split_len, ctx);  // exclusive
-  const int c0 = kbeg / kBS, c1 = (kend + kBS - 1) / kBS;
+  // FUSED: the new key (ctx - 1) is not read from the cache; the split that owns it adds it last
+  const bool owns_new = FUSED && ctx > 0 && (ctx - 1) / split_len == split;
+  const int kend = min(kbeg + split_len, FUSED ? ctx - 1 : ctx);  // exclusive (cache keys)
+  const int c0 = kbeg / kBS, c1 = kend > kbeg ? (kend + kBS - 1) / kBS : c0;
 
   // Q^T fragments: column r = head kvh*G + r (zero beyond G)
   bf16x8 qf[D / 32];
   const bool col_ok = r < G;
-  const bf16* qrow = q + ((size_t)b * hq + kvh * G + (col_ok ? r : 0)) * D;
+  bf16x8 kn[D / 32];
+  bf16 vn[D / 16];
+  if (FUSED) {
+    const bf16* row = ra.qkv + (size_t)b * (hq + 2 * hkv) * D;
+    const bf16* qrow = row + (size_t)(kvh * G + (col_ok ? r : 0)) * D;
+    const bf16* krow = row + (size_t)(hq + kvh) * D;
+    const bf16* vrow = row + (size_t)(hq + hkv + kvh) * D;
 #pragma unroll
-  for (int ks = 0; ks < D / 32; ++ks) {
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
-    if (!col_ok) v = bf16x8{};
-    qf[ks] = v;
+    for (int ks = 0; ks < D / 32; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
+      kn[ks] = *reinterpret_cast<const bf16x8*>(krow + ks * 32 + 8 * g);
+    }
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) vn[dt] = vrow[dt * 16 + r];
+  } else {
+    const bf16* qrow = q + ((size_t)b * hq + kvh * G + (col_ok ? r : 0)) * D;
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
+      if (!col_ok) v = bf16x8{};
+      qf[ks] = v;
+    }
   }
+  // FUSED: rotate q/k and append k/v AFTER the first KV chunk's loads are issued, so the
+  // positions -> cos/sin -> rotate dependency overlaps the KV stream instead of preceding it
+  bool rope_done = !FUSED;
+  auto finish_rope = [&]() {
+    if (!FUSED || rope_done) return;
+    rope_done = true;
+    const float* cs = ra.cos_sin ? ra.cos_sin + (size_t)ra.positions[b] * D : nullptr;
+    rope_rotate<D, FUSED>(qf, cs, g);
+    rope_rotate<D, FUSED>(kn, cs, g);
+    if (!col_ok) {
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) qf[ks] = bf16x8{};
+    }
+    if (owns_new) {   // append k (row layout) and v^T (column `off`) to the paged cache
+      const int slot = ra.slots[b];
+      const int blk = slot / kBS, off = slot % kBS;
+      const size_t base = ((size_t)blk * hkv + kvh) * kBS * D;
+      if (r == 0) {
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks)
+          *reinterpret_cast<bf16x8*>(k_cache + base + (size_t)off * D + ks * 32 + 8 * g) = kn[ks];
+      }
+      if (g == 0) {
+#pragma unroll
+        for (int dt = 0; dt < D / 16; ++dt) v_cache[base + (size_t)(dt * 16 + r) * kBS + off] = vn[dt];
+      }
+    }
+  };
   WaveState<D> st;
   init_state(st);
   const int kmax = kend - 1;
@@ -172,6 +249,7 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
       const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, 0) * blk_stride + head_off;
       load_chunk<D>(cur, k_cache + base, v_cache + base, lane);
     }
+    finish_rope();
     int j = 0;
     for (; j + 2 <= n; j += 2) {                    // ping-pong: cur <-> nxt
       {
@@ -186,6 +264,23 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
       compute_chunk<D>(st, qf, nxt, (cb + j + 1) * kBS, kmax, scale_log2, lane);
     }
     if (j < n) compute_chunk<D>(st, qf, cur, (cb + j) * kBS, kmax, scale_log2, lane);
+  }
+  finish_rope();   // no cache chunk in this split
+  if (owns_new) {   // the new key as a one-key chunk: K row 0 = k, V^T column 0 = v, rest masked
+    KVChunk<D> nc;
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) {
+      nc.ka[ks] = r == 0 ? kn[ks] : bf16x8{};
+      nc.kb[ks] = bf16x8{};
+    }
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      bf16x4 lo = {};
+      if (g == 0) lo[0] = vn[dt];
+      nc.vlo[dt] = lo;
+      nc.vhi[dt] = bf16x4{};
+    }
+    compute_chunk<D>(st, qf, nc, ctx - 1, ctx - 1, scale_log2, lane);
   }
   float lt = st.lsum;
   lt += __shfl_xor(lt, 16, 64);
@@ -289,16 +384,16 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(
 }
 
 // ------------------------------------------------------------------ launchers
-void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
-                            uintptr_t block_tables, uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml,
-                            int batch, int hq, int hkv, int d, int block_size, int max_blocks, int num_splits,
-                            int split_len, float scale, uintptr_t stream) {
+static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache, uintptr_t block_tables,
+                          uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml, int batch, int hq, int hkv, int d,
+                          int block_size, int max_blocks, int num_splits, int split_len, float scale, RopeArgs ra,
+                          bool fused, uintptr_t stream) {
   DLLM_HOST_CHECK(block_size == kBS, "paged attention requires block_size 32");
   DLLM_HOST_CHECK(hq % hkv == 0 && hq / hkv <= 16, "GQA group size must be <= 16");
   DLLM_HOST_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
   DLLM_HOST_CHECK(num_splits >= 1 && split_len % kBS == 0 && split_len > 0, "split_len multiple of 32");
   DLLM_HOST_CHECK(num_splits == 1 || (part_o && part_ml), "split workspace");
-  DLLM_HOST_CHECK((long)num_splits * split_len >= 1, "splits");
+  DLLM_HOST_CHECK(!fused || (ra.qkv && ra.positions && ra.slots), "fused decode needs qkv, positions, slots");
   if (batch == 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float sl2 = scale * 1.4426950408889634f;
@@ -306,19 +401,22 @@ void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintp
   const int wpb = hkv % 4 == 0 ? 4 : hkv % 2 == 0 ? 2 : 1;
   dim3 grid(num_splits, hkv / wpb, batch);
   auto go = [&](auto kern, int threads) {
-    hipLaunchKernelGGL(kern, grid, dim3(threads), 0, s, (bf16*)out, (const bf16*)q, (const bf16*)k_cache,
-                       (const bf16*)v_cache, (const int32_t*)block_tables, (const int32_t*)seq_lens, (float*)part_o,
-                       (float*)part_ml, hq, hkv, max_blocks, split_len, sl2);
+    hipLaunchKernelGGL(kern, grid, dim3(threads), 0, s, (bf16*)out, (const bf16*)q, (bf16*)k_cache, (bf16*)v_cache,
+                       (const int32_t*)block_tables, (const int32_t*)seq_lens, (float*)part_o, (float*)part_ml, hq,
+                       hkv, max_blocks, split_len, sl2, ra);
   };
+#define DLLM_DEC(DD, FF)                                              \
+  do {                                                                \
+    if (wpb == 4) go(attn_decode_kernel<DD, 4, FF>, 256);             \
+    else if (wpb == 2) go(attn_decode_kernel<DD, 2, FF>, 128);        \
+    else go(attn_decode_kernel<DD, 1, FF>, 64);                       \
+  } while (0)
   if (d == 128) {
-    if (wpb == 4) go(attn_decode_kernel<128, 4>, 256);
-    else if (wpb == 2) go(attn_decode_kernel<128, 2>, 128);
-    else go(attn_decode_kernel<128, 1>, 64);
+    if (fused) DLLM_DEC(128, true); else DLLM_DEC(128, false);
   } else {
-    if (wpb == 4) go(attn_decode_kernel<64, 4>, 256);
-    else if (wpb == 2) go(attn_decode_kernel<64, 2>, 128);
-    else go(attn_decode_kernel<64, 1>, 64);
+    if (fused) DLLM_DEC(64, true); else DLLM_DEC(64, false);
   }
+#undef DLLM_DEC
   DLLM_HIP_CHECK(hipGetLastError());
   if (num_splits > 1) {
     if (d == 128)
@@ -329,6 +427,25 @@ void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintp
                          (const float*)part_o, (const float*)part_ml, num_splits);
     DLLM_HIP_CHECK(hipGetLastError());
   }
+}
+
+void paged_attention_decode(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
+                            uintptr_t block_tables, uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml,
+                            int batch, int hq, int hkv, int d, int block_size, int max_blocks, int num_splits,
+                            int split_len, float scale, uintptr_t stream) {
+  decode_launch(out, q, k_cache, v_cache, block_tables, seq_lens, part_o, part_ml, batch, hq, hkv, d, block_size,
+                max_blocks, num_splits, split_len, scale, RopeArgs{nullptr, nullptr, nullptr, nullptr}, false, stream);
+}
+
+// decode with RoPE + KV append fused in: reads the raw qkv projection [B, (hq + 2 hkv) * d]
+void paged_attention_decode_rope(uintptr_t out, uintptr_t qkv, uintptr_t positions, uintptr_t cos_sin, uintptr_t slots,
+                                 uintptr_t k_cache, uintptr_t v_cache, uintptr_t block_tables, uintptr_t seq_lens,
+                                 uintptr_t part_o, uintptr_t part_ml, int batch, int hq, int hkv, int d,
+                                 int block_size, int max_blocks, int num_splits, int split_len, float scale,
+                                 uintptr_t stream) {
+  RopeArgs ra{(const bf16*)qkv, (const int32_t*)positions, (const float*)cos_sin, (const int32_t*)slots};
+  decode_launch(out, 0, k_cache, v_cache, block_tables, seq_lens, part_o, part_ml, batch, hq, hkv, d, block_size,
+                max_blocks, num_splits, split_len, scale, ra, true, stream);
 }
 
 template <int D>

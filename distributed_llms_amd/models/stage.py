@@ -14,6 +14,7 @@ Stage I/O:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -23,6 +24,9 @@ from .. import ops
 from ..config import ModelConfig
 from ..ops import reference as ref
 from . import weights as W
+
+# decode: RoPE + KV append fused into the attention kernel (one launch); DLLM_FUSED_ROPE=0 -> two launches
+FUSED_ROPE_DECODE = os.environ.get("DLLM_FUSED_ROPE", "1") != "0"
 
 
 @dataclass
@@ -170,6 +174,12 @@ class ModelStage:
     def _attention(self, qkv: torch.Tensor, li: int, meta: BatchMeta) -> torch.Tensor:
         cfg = self.cfg
         k_cache, v_cache = self.kv.layer(li)
+        if not meta.is_prefill and qkv.is_cuda and FUSED_ROPE_DECODE:
+            o = ops.paged_attention_decode_rope(qkv, meta.positions, self.cos_sin, k_cache, v_cache, meta.slot_mapping,
+                                                meta.block_tables, meta.seq_lens, cfg.num_heads, cfg.num_kv_heads,
+                                                cfg.head_dim, self.scale, max_ctx=meta.max_ctx or None,
+                                                workspace=meta.attn_workspace)
+            return o.view(o.shape[0], cfg.q_size)
         q = ops.rope_cache_append(qkv, meta.positions, self.cos_sin, k_cache, v_cache, meta.slot_mapping,
                                   cfg.num_heads, cfg.num_kv_heads, cfg.head_dim)
         if meta.is_prefill:

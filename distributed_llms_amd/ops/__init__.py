@@ -22,7 +22,7 @@ from . import reference as ref
 __all__ = [
     "embedding", "rms_norm", "fused_add_rms_norm", "layer_norm", "linear", "silu_mul",
     "gelu_tanh", "rope_cache_append", "paged_attention_decode", "paged_attention_prefill",
-    "argmax", "add_", "moe_route", "moe_mlp", "decode_split_plan",
+    "argmax", "add_", "moe_route", "moe_mlp", "decode_split_plan", "paged_attention_decode_rope",
 ]
 
 
@@ -227,6 +227,57 @@ def paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale: f
     _ext.kernels().paged_attention_decode(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                           block_tables.data_ptr(), seq_lens.data_ptr(), po, pml, b, hq, hkv, d,
                                           bs, max_blocks, splits, split_len, float(scale), _stream())
+    return out
+
+
+def paged_attention_decode_rope(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, block_tables, seq_lens,
+                                num_heads: int, num_kv_heads: int, head_dim: int, scale: float,
+                                max_ctx: Optional[int] = None, workspace: Optional[tuple] = None):
+    """Decode attention with RoPE + KV-cache append fused in (one launch instead of two): reads the raw
+    qkv projection [B, (Hq + 2 Hkv) * D], appends each sequence's new k / v at ``slot_mapping`` and
+    attends over the whole context including it.  Same result as ``rope_cache_append`` followed by
+    ``paged_attention_decode`` (the new key is folded in last instead of inside its block)."""
+    if not _gpu(qkv):
+        q = ref.rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, num_heads, num_kv_heads,
+                                  head_dim)
+        return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
+    _ck(qkv, "attn.qkv")
+    _ck(k_cache, "k_cache")
+    _ck(v_cache, "v_cache")
+    _ck(positions, "positions", torch.int32)
+    _ck(slot_mapping, "slot_mapping", torch.int32)
+    _ck(block_tables, "block_tables", torch.int32)
+    _ck(seq_lens, "seq_lens", torch.int32)
+    b = qkv.shape[0]
+    hq, hkv, d = num_heads, num_kv_heads, head_dim
+    if qkv.shape[1] != (hq + 2 * hkv) * d:
+        raise ValueError("qkv width mismatch")
+    if cos_sin is not None:
+        _ck(cos_sin, "cos_sin", torch.float32)
+        if cos_sin.shape[1] != d:
+            raise ValueError("cos_sin width must equal head_dim")
+    bs = k_cache.shape[2]
+    max_blocks = block_tables.shape[1]
+    if max_ctx is None:
+        max_ctx = max_blocks * bs
+    if max_ctx > max_blocks * bs:
+        raise ValueError("max_ctx exceeds block table capacity")
+    splits, split_len = decode_split_plan(b, hkv, max_ctx, bs, max_blocks)
+    out = torch.empty(b, hq, d, dtype=qkv.dtype, device=qkv.device)
+    po = pml = 0
+    if splits > 1:
+        if workspace is None:
+            po_t = torch.empty(b * hq * splits * d, dtype=torch.float32, device=qkv.device)
+            pml_t = torch.empty(b * hq * splits * 2, dtype=torch.float32, device=qkv.device)
+        else:
+            po_t, pml_t = workspace
+            if po_t.numel() < b * hq * splits * d or pml_t.numel() < b * hq * splits * 2:
+                raise ValueError("attention workspace too small")
+        po, pml = po_t.data_ptr(), pml_t.data_ptr()
+    _ext.kernels().paged_attention_decode_rope(
+        out.data_ptr(), qkv.data_ptr(), positions.data_ptr(), 0 if cos_sin is None else cos_sin.data_ptr(),
+        slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), seq_lens.data_ptr(),
+        po, pml, b, hq, hkv, d, bs, max_blocks, splits, split_len, float(scale), _stream())
     return out
 
 

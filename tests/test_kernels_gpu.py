@@ -107,6 +107,31 @@ def test_paged_attention_decode(cuda, hq, hkv, d, lens):
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (12, 12, 64), (4, 1, 128)])
+@pytest.mark.parametrize("lens", [[1], [7, 33, 100], [640, 5, 2049, 32]])
+@pytest.mark.parametrize("rope", [True, False])
+def test_paged_attention_decode_fused_rope(cuda, hq, hkv, d, lens, rope):
+    """RoPE + KV append fused into decode attention == rope_cache_append + paged_attention_decode
+    (fp32 reference), including what lands in the cache; also with split-KV (long contexts)."""
+    k, v, bt = _fill_paged(lens, hkv, d)
+    b = len(lens)
+    sl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    pos = sl - 1
+    # slot of the new token: position len-1 inside its sequence's block table
+    slots = torch.stack([bt[i, (n - 1) // 32] * 32 + (n - 1) % 32 for i, n in enumerate(lens)]).to(torch.int32)
+    qkv = _bf(b, (hq + 2 * hkv) * d)
+    cs = ref.rope_cos_sin(d, 4096, 500000.0, device="cuda") if rope else None
+    scale = 1 / math.sqrt(d)
+    k1, v1 = k.clone(), v.clone()
+    out = ops.paged_attention_decode_rope(qkv, pos, cs, k1, v1, slots, bt, sl, hq, hkv, d, scale)
+    k2, v2 = k.float(), v.float()
+    q2 = ref.rope_cache_append(qkv.float(), pos, cs, k2, v2, slots, hq, hkv, d)
+    expect = ref.paged_attention_decode(q2, k2, v2, bt, sl, scale)
+    torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(k1.float(), k2, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(v1.float(), v2, atol=0, rtol=0)
+
+
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 64)])
 def test_paged_attention_prefill(cuda, hq, hkv, d):
     ctx = [37, 128, 300, 5]
