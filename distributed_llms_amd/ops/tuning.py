@@ -19,8 +19,8 @@ import torch
 
 log = logging.getLogger("dllm.tuning")
 
-TUNED_CSV = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
-                         "tunableop_gfx950.csv")
+TUNED_CSV = os.environ.get("DLLM_TUNABLEOP_FILE") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "tunableop_gfx950.csv")
 _state = {"done": False, "ok": False}
 
 
