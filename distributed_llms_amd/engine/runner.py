@@ -25,7 +25,8 @@ def plan_kv_blocks(mcfg: ModelConfig, num_layers: int, ecfg: EngineConfig, devic
     if ecfg.num_kv_blocks > 0:
         return ecfg.num_kv_blocks
     per_seq = -(-ecfg.max_seq_len // bs)
-    slots = max(1, ecfg.microbatches or ecfg.num_workers)
+    # microbatch slots in flight: the pipeline driver runs pp + 1 (parallel/pipeline.py)
+    slots = ecfg.microbatches or (ecfg.num_workers + 1 if ecfg.num_workers > 1 else 1)
     want = ecfg.max_batch * slots * per_seq + 2
     per_block = max(1, KVCache.bytes_per_block(num_layers, mcfg.num_kv_heads, mcfg.head_dim, bs))
     dev = torch.device(device)

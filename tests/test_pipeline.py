@@ -140,3 +140,15 @@ def test_unit_planner_balances_better_than_layers():
         assert u.imbalance() < l.imbalance()
         assert u.units[0][0] == 0 and u.units[-1][1] == 64
         assert all(a[1] == b[0] for a, b in zip(u.units, u.units[1:]))
+
+
+def test_kv_plan_covers_all_pipeline_slots():
+    """A pp-stage pipeline keeps pp + 1 microbatch slots in flight; the KV pool must hold all of them."""
+    from distributed_llms_amd.engine.runner import plan_kv_blocks
+    cfg = get_model_config("tiny-llama")
+    per_seq = -(-288 // 32)
+    for pp, slots in ((1, 1), (2, 3), (8, 9)):
+        e = EngineConfig(model="tiny-llama", device="cpu", max_batch=16, max_seq_len=288, num_workers=pp)
+        assert plan_kv_blocks(cfg, 1, e, "cpu") == 16 * slots * per_seq + 2
+    e = EngineConfig(model="tiny-llama", device="cpu", max_batch=16, max_seq_len=288, num_workers=8, microbatches=4)
+    assert plan_kv_blocks(cfg, 1, e, "cpu") == 16 * 4 * per_seq + 2
