@@ -42,10 +42,15 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--tiled", action="store_true", help="compare the split-K tiled kernel instead")
+    ap.add_argument("--wide", action="store_true", help="three-way: wide-M kernel vs tiled kernel vs hipBLASLt")
+    ap.add_argument("--warm", action="store_true", help="no cache flush between calls (in-engine-like)")
+    ap.add_argument("--splits", type=int, default=0)
     a = ap.parse_args()
     # a scratch buffer larger than the 256 MiB Infinity Cache to flush it between calls
     flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
     print(f"{'shape':12s} {'M':>4s} {'ours_us':>9s} {'ours_TB/s':>10s} {'blas_us':>9s} {'blas_TB/s':>10s} {'speedup':>8s}")
+    if a.wide:
+        return wide(a, flush)
     for name in a.shapes:
         n, k, sw = SHAPES[name]
         w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
@@ -70,6 +75,55 @@ def main():
             to, tb = min(to), min(tb)
             byt = n * k * 2
             print(f"{name:12s} {m:4d} {to*1e6:9.1f} {byt/to/1e12:10.2f} {tb*1e6:9.1f} {byt/tb/1e12:10.2f} {tb/to:8.2f}",
+                  flush=True)
+
+
+def wide(a, flush):
+    """Three-way comparison.  Cold = rotate through enough weight copies (> 768 MB) that every call
+    streams its weight from HBM, with no dirty flush buffer competing for write-back (in-engine-like:
+    each layer's weights are read once per step).  --warm = one copy (MALL-resident)."""
+    print(f"{'shape':12s} {'M':>4s} {'wide_us':>8s} {'TB/s':>6s} {'TF':>6s} {'tiled_us':>8s} {'blas_us':>8s} "
+          f"{'vs_tiled':>8s} {'vs_blas':>8s}  ({'warm' if a.warm else 'cold, rotating weights'})")
+    for name in a.shapes:
+        n, k, sw = SHAPES[name]
+        copies = 1 if a.warm else max(2, -(-(768 << 20) // (n * k * 2)))
+        ws = [(torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(copies)]
+        for m in a.m:
+            x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
+            # one HIP graph per implementation: `copies` back-to-back calls, each on its own weight
+            # copy (launch overhead out of the measurement, like the engine's captured decode step)
+            impls = {
+                "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=0),
+                "wide1": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=1),
+                "wide2": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=3),
+                "tiled": lambda w: gemm.linear_tiled(x, w, swiglu=sw),
+                "blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w)),
+            }
+            reps = max(copies, 8)
+            graphs = {}
+            for key, f in impls.items():
+                st = torch.cuda.Stream()
+                st.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(st):
+                    for i in range(reps):
+                        f(ws[i % copies])
+                torch.cuda.current_stream().wait_stream(st)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=st):
+                    for i in range(reps):
+                        f(ws[i % copies])
+                graphs[key] = g
+            for g in graphs.values():
+                g.replay()
+            res = {key: [] for key in graphs}
+            for _ in range(3):
+                for key, g in graphs.items():
+                    res[key].append(timeit(g.replay, max(3, a.iters // 5)) / reps)
+            t = {key: min(v) for key, v in res.items()}
+            byt, fl_ = n * k * 2, 2.0 * m * n * k
+            print(f"{name:12s} {m:4d} {t['wide']*1e6:8.1f} {byt/t['wide']/1e12:6.2f} {fl_/t['wide']/1e12:6.0f} "
+                  f"{t['tiled']*1e6:8.1f} {t['blas']*1e6:8.1f} {t['tiled']/t['wide']:8.2f} {t['blas']/t['wide']:8.2f} "
+                  f"v1 {t['wide1']*1e6:6.1f} v2 {t['wide2']*1e6:6.1f}",
                   flush=True)
 
 

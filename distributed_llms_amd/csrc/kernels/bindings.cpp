@@ -24,6 +24,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("moe_grouped_gemm", &dllm::moe_grouped_gemm);
   m.def("splitk_add_rms_norm", &dllm::splitk_add_rms_norm);
   m.def("splitk_reduce", &dllm::splitk_reduce);
+  m.def("gemm_wide", &dllm::gemm_wide);
   m.def("moe_combine", &dllm::moe_combine);
   m.def("paged_attention_decode", &dllm::paged_attention_decode);
   m.def("paged_attention_decode_rope", &dllm::paged_attention_decode_rope);

@@ -232,13 +232,25 @@ void splitk_add_rms_norm(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, i
 }
 
 // plain split-K reduce of partials left by gemm_tiled(mode 2): out = bf16(sum_s P[s]) (+bias)
-void splitk_reduce(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M, int N, uintptr_t stream) {
-  long blocks = ((long)M * N / 4 + 255) / 256;
+void splitk_reduce_ex(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M, int N, int swiglu,
+                      uintptr_t stream) {
+  DLLM_HOST_CHECK(N % (swiglu ? 8 : 4) == 0, "N alignment");
+  const int ncols = swiglu ? N / 2 : N;
+  long blocks = ((long)M * ncols / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks == 0) return;
-  hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3((unsigned)blocks), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), (bf16*)out, (const float*)ws, (const bf16*)bias, S, M, N);
+  if (swiglu)
+    hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3((unsigned)blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), (bf16*)out, (const float*)ws, (const bf16*)nullptr, S, M,
+                       N);
+  else
+    hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3((unsigned)blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), (bf16*)out, (const float*)ws, (const bf16*)bias, S, M, N);
   DLLM_HIP_CHECK(hipGetLastError());
+}
+
+void splitk_reduce(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M, int N, uintptr_t stream) {
+  splitk_reduce_ex(out, ws, bias, S, M, N, 0, stream);
 }
 
 // mode 0: C[M,N] = A B^T (+bias);  mode 1 (SwiGLU): C[M, N/2] = silu(A Bg^T) * (A Bu^T), B = [Bg; Bu]

@@ -1,0 +1,465 @@
+// Decode GEMM for batch-sized M (128..512): C[M,N] = A[M,K] . B[N,K]^T, bf16 in, f32 accumulate.
+//
+// Why a second tiled kernel: at M = 256 the decode projections sit on the ridge between weight
+// streaming and MFMA (256 FLOP per weight byte).  The 128x128 two-phase kernel (gemm_tiled.hip)
+// re-reads every weight tile once per 128-row M tile and drains its single prefetch at every
+// barrier; hipBLASLt's 256x128 tile runs the MLP gate|up at ~3.2 TB/s / 0.8 PF in the engine
+// (profiles/llama3_8b_b256_kernels_current.md) -- latency-bound at one workgroup per CU.
+//
+// Structure (gfx950, wave64):
+//  * tile BM x 128 x 64 with BM = 256 (or 128 for M <= 128): ALL decode rows in one tile, so
+//    each weight byte leaves HBM once per step; 512 threads = 8 waves in 4 (M) x 2 (N), wave
+//    tile (BM/4) x 64 = (BM/64) x 4 v_mfma_f32_16x16x32_bf16 accumulators;
+//  * global -> LDS with global_load_lds_dwordx4 (lane-linear 1 KiB per wave-instruction =
+//    8 rows x 128 B), bank-conflict swizzle chunk ^ ((row >> 1) & 7) applied on the per-lane
+//    SOURCE address and on the ds_read address (guide rule 21);
+//  * THREE LDS buffers (3 x 48 KiB at BM = 256): tiles t+1 and t+2 stay in flight while tile t
+//    is multiplied.  One raw s_barrier per K-tile preceded by a COUNTED vmcnt (never 0 in the
+//    loop) -- __syncthreads() would drain the LDS-DMA queue (guide "Pipelining across barriers");
+//    all LDS lives in one __shared__ array (guide trap 4a);
+//  * SwiGLU layout without a weight permutation: the 128 B-tile rows are 16-row groups taken
+//    alternately from the gate half and the up half of the fused [2I, K] weight, so the same lane
+//    holds gate column j and up column j in neighbouring accumulators and the epilogue writes
+//    silu(g) * u directly (no [M, 2I] intermediate, no separate silu_mul launch);
+//  * optional split-K: f32 partial slabs in natural column order, reduced by the next op
+//    (splitk_add_rms_norm) or by splitk_reduce(_swiglu);
+//  * XCD-aware block order (bijective remap): the M tiles and K slices of one N tile run
+//    back-to-back on one XCD.
+#include "common.h"
+#include "launchers.h"
+
+#include <type_traits>
+
+namespace dllm {
+
+typedef __attribute__((address_space(3))) void* lds_vptr_w;
+typedef __attribute__((address_space(1))) void* glb_vptr_w;
+
+namespace {
+constexpr int WBN = 128, WBK = 64;
+
+__device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+#define DLLM_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+// wait until at most `younger` tiles of G LDS-DMA instructions each are still in flight
+template <int G>
+__device__ __forceinline__ void wait_tiles(int younger) {
+  static_assert(G == 4 || G == 6, "G");
+  if (younger <= 0) { DLLM_VM(0); return; }
+  if constexpr (G == 4) {
+    if (younger == 1) DLLM_VM(4); else if (younger == 2) DLLM_VM(8); else DLLM_VM(12);
+  } else {
+    if (younger == 1) DLLM_VM(6); else if (younger == 2) DLLM_VM(12); else DLLM_VM(18);
+  }
+}
+#undef DLLM_VM
+}  // namespace
+
+// B-tile row r (0..127) -> row of the weight matrix.
+//   plain:  n0 + r
+//   SwiGLU: 16-row group g = r / 16 alternates gate (even g) / up (odd g); output column
+//           c = (g / 2) * 16 + r % 16 of this tile's 64 outputs
+template <bool SWIGLU>
+__device__ __forceinline__ int wide_b_row(int r, int n_t, int half) {
+  if (!SWIGLU) return n_t * WBN + r;
+  const int g = r >> 4;
+  return ((g & 1) ? half : 0) + n_t * 64 + (g >> 1) * 16 + (r & 15);
+}
+
+// epilogue shared by both wide kernels: acc[rt][ct] lane holds tile column (lane & 15), rows
+// 4 * (lane >> 4) + i of each 16 x 16 fragment
+template <int BM, bool SPLIT, bool SWIGLU>
+__device__ __forceinline__ void wide_epilogue(const f32x4 (&acc)[BM / 64][4], bf16* __restrict__ C,
+                                              float* __restrict__ P, int M, int N, int m0, int n_t, int split, int wm,
+                                              int wn, int lane) {
+  constexpr int RT = BM / 64;
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * (BM / 4) + rt * 16 + 4 * fq + i;
+      if (m >= M) continue;
+      if (SWIGLU && !SPLIT) {
+        const int half = N / 2;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int c = n_t * 64 + (wn * 2 + p) * 16 + fr;
+          const float g = acc[rt][2 * p][i], u = acc[rt][2 * p + 1][i];
+          C[(size_t)m * half + c] = f2bf(silu_f(g) * u);
+        }
+      } else {
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const int n = wide_b_row<SWIGLU>(wn * 64 + ct * 16 + fr, n_t, N / 2);
+          if (SPLIT) P[((size_t)split * M + m) * N + n] = acc[rt][ct][i];
+          else C[(size_t)m * N + n] = f2bf(acc[rt][ct][i]);
+        }
+      }
+    }
+  }
+}
+
+template <int BM, bool SPLIT, bool SWIGLU, int NBUF, int VAR>
+__global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                           bf16* __restrict__ C, float* __restrict__ P, int M, int N,
+                                                           int K, int kt_per_split, int nsplit) {
+  constexpr int AEL = BM * WBK, BEL = WBN * WBK, BUF = AEL + BEL;   // bf16 elements
+  constexpr int AI = BM / 64;                 // A glds instructions per thread per tile
+  constexpr int BI = 2;                       // B glds instructions per thread per tile
+  constexpr int G = AI + BI;                  // glds per thread per tile (vmcnt unit)
+  constexpr int RT = BM / 64;                 // 16-row fragments per wave in M
+  static_assert(NBUF >= 3 && NBUF * BUF * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int mtiles = (M + BM - 1) / BM;
+  const int ntiles = SWIGLU ? (N / 2) / 64 : N / WBN;
+  const int total = gridDim.x;
+  // bijective XCD remap: blocks b with b % 8 == x run on XCD x; give XCD x a contiguous run
+  int b = blockIdx.x;
+  {
+    const int q = total >> 3, r = total & 7, x = b & 7;
+    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  }
+  const int m_t = b % mtiles, rest = b / mtiles;
+  const int split = rest % nsplit, n_t = rest / nsplit;
+  (void)ntiles;
+  const int m0 = m_t * BM;
+  const int kt0 = split * kt_per_split;
+  const int nt = max(0, min(K / WBK, kt0 + kt_per_split) - kt0);
+
+  // per-lane staging sources: instruction i covers tile rows 8i .. 8i+7, lane -> (row, chunk)
+  const bf16* srcA[AI];
+  const bf16* srcB[BI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int i = wv * AI + j;
+    const int r = 8 * i + (lane >> 3);
+    srcA[j] = A + (size_t)min(m0 + r, M - 1) * K + (size_t)kt0 * WBK + wswz(r, lane & 7) * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int i = wv * BI + j;
+    const int r = 8 * i + (lane >> 3);
+    srcB[j] = B + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + (size_t)kt0 * WBK + wswz(r, lane & 7) * 8;
+  }
+  auto stage = [&](int buf, int t) {
+    bf16* base = smem + buf * BUF;
+    const int ko = t * WBK;
+#pragma unroll
+    for (int j = 0; j < AI; ++j)
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcA[j] + ko), (lds_vptr_w)(base + (wv * AI + j) * 512), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < BI; ++j)
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcB[j] + ko), (lds_vptr_w)(base + AEL + (wv * BI + j) * 512), 16,
+                                       0, 0);
+  };
+
+  f32x4 acc[RT][4];
+#pragma unroll
+  for (int a = 0; a < RT; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // one glds piece: p < AI -> A rows, else B rows
+  auto piece = [&](bf16* base, int ko, int p) {
+    if (p < AI)
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcA[p] + ko), (lds_vptr_w)(base + (wv * AI + p) * 512), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcB[p - AI] + ko),
+                                       (lds_vptr_w)(base + AEL + (wv * BI + p - AI) * 512), 16, 0, 0);
+  };
+  // one K-tile of MFMAs from buffer `cur`; with STG the next tile's G LDS-DMA pieces are issued
+  // in between the MFMAs (each glds costs ~60-185 issue cycles: issued back to back after the
+  // barrier they idle the MFMA pipe -- spread out, they hide under MFMA execution)
+  auto ktile = [&](int cur, bf16* dst, int ko, auto stg) {
+    constexpr bool STG = decltype(stg)::value;
+    const bf16* sa = smem + cur * BUF;
+    const bf16* sb = sa + AEL;
+    bf16x8 fa[2][RT], fb[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int row = wm * (BM / 4) + rt * 16 + fr;
+        fa[s][rt] = *reinterpret_cast<const bf16x8*>(sa + row * WBK + wswz(row, 4 * s + fq) * 8);
+      }
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int row = wn * 64 + ct * 16 + fr;
+        fb[s][ct] = *reinterpret_cast<const bf16x8*>(sb + row * WBK + wswz(row, 4 * s + fq) * 8);
+      }
+    }
+    constexpr int NMF = 2 * RT * 4;
+    constexpr int EVERY = NMF / (G + 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][rt], fb[s][ct], acc[rt][ct], 0, 0, 0);
+          if constexpr (STG) {
+            const int i = (s * RT + rt) * 4 + ct + 1;
+            if (i % EVERY == 0 && i / EVERY <= G) piece(dst, ko, i / EVERY - 1);
+          }
+        }
+    if constexpr (STG && VAR == 1) {
+      // pin the interleave: 8 LDS reads of substep 0, then (EVERY MFMAs, 1 VMEM) x G, rest
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (RT + 4), 0);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, EVERY, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF - G * EVERY, 0);
+    }
+  };
+
+  if (nt > 0) {
+#pragma unroll
+    for (int p = 0; p < NBUF - 1; ++p)
+      if (p < nt) stage(p, p);
+    int cur = 0;
+    int t = 0;
+    // steady state: tile t + NBUF - 1 exists, NBUF - 2 younger tiles stay in flight
+    for (; t + NBUF - 1 < nt; ++t) {
+      wait_tiles<G>(NBUF - 2);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // buffer (t-1) % NBUF was last read in iteration t-1, which every wave finished before
+      // this barrier: refill it with tile t + NBUF - 1
+      const int nb = cur == 0 ? NBUF - 1 : cur - 1;
+      if constexpr (VAR == 0) {
+        stage(nb, t + NBUF - 1);
+        ktile(cur, smem, 0, std::false_type{});
+      } else {
+        ktile(cur, smem + nb * BUF, (t + NBUF - 1) * WBK, std::true_type{});
+      }
+      cur = cur == NBUF - 1 ? 0 : cur + 1;
+    }
+    // drain: no more tiles to stage
+    for (; t < nt; ++t) {
+      wait_tiles<G>(nt - 1 - t);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      ktile(cur, smem, 0, std::false_type{});
+      cur = cur == NBUF - 1 ? 0 : cur + 1;
+    }
+  }
+
+  wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
+}
+
+// ---------------------------------------------------------------------------------------------
+// gemm_wide2: the same tile (BM x 128, 8 waves 4 x 2) with BK = 32 and a software pipeline on
+// the MFMA fragments.  In gemm_wide every wave reads its K-tile's fragments right after the
+// barrier, so all 8 waves wait on the LDS (512 array cycles per 64-deep K-tile) with the MFMA
+// pipe idle.  Here the fragments of tile t+1 are read from LDS while the MFMAs of tile t (held in
+// registers since the previous step) execute, and the LDS-DMA pieces of tile t+NBUF-1 are issued
+// in between those MFMAs.  32-deep tiles halve the LDS footprint per stage, so NBUF = 6 stages
+// (144 KiB at BM = 256) keep NBUF-3 tiles in flight while one is landing and one is being read.
+//
+// LDS image per stage: A [BM][32] then B [128][32] bf16, 64-B rows, lane-linear glds (one
+// wave-instruction = 16 rows x 64 B).  16-B chunk c of row r is stored at c ^ f(r) with
+// f(r) = (0x78 >> 2 * ((r >> 2) & 3)) & 3: the four 16-lane groups of a ds_read_b128
+// ({0-3,12-15,20-27}, ...) then hit 16 distinct 16-B bank slots (conflict-free).
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr int W2BK = 32;
+__device__ __forceinline__ int w2swz(int row, int chunk) { return chunk ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3); }
+
+template <int G>
+__device__ __forceinline__ void wait2(int younger) {
+  static_assert(G == 2 || G == 3, "G");
+#define DLLM_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+  if (younger <= 0) { DLLM_VM(0); return; }
+  if constexpr (G == 2) {
+    if (younger == 1) DLLM_VM(2); else if (younger == 2) DLLM_VM(4); else if (younger == 3) DLLM_VM(6);
+    else DLLM_VM(8);
+  } else {
+    if (younger == 1) DLLM_VM(3); else if (younger == 2) DLLM_VM(6); else if (younger == 3) DLLM_VM(9);
+    else DLLM_VM(12);
+  }
+#undef DLLM_VM
+}
+}  // namespace
+
+template <int BM, bool SPLIT, bool SWIGLU, int NBUF>
+__global__ void __launch_bounds__(512, 1) gemm_wide2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                            bf16* __restrict__ C, float* __restrict__ P, int M, int N,
+                                                            int K, int kt64_per_split, int nsplit) {
+  constexpr int AEL = BM * W2BK, BEL = WBN * W2BK, BUF = AEL + BEL;   // bf16 elements per stage
+  constexpr int AI = BM / 128;                // A glds per thread per tile (16 rows x 64 B each)
+  constexpr int BI = 1;                       // B: 128 rows = 8 instructions = 1 per wave
+  constexpr int G = AI + BI;
+  constexpr int RT = BM / 64;
+  static_assert(NBUF >= 4 && NBUF * BUF * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int mtiles = (M + BM - 1) / BM;
+  const int total = gridDim.x;
+  int b = blockIdx.x;
+  {
+    const int q = total >> 3, r = total & 7, x = b & 7;
+    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  }
+  const int m_t = b % mtiles, rest = b / mtiles;
+  const int split = rest % nsplit, n_t = rest / nsplit;
+  const int m0 = m_t * BM;
+  const int kt0 = split * kt64_per_split * 2;                         // in 32-deep tiles
+  const int nt = max(0, min(K / W2BK, kt0 + kt64_per_split * 2) - kt0);
+
+  const bf16* srcA[AI];
+  const bf16* srcB[BI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int r = 16 * (wv * AI + j) + (lane >> 2);
+    srcA[j] = A + (size_t)min(m0 + r, M - 1) * K + (size_t)kt0 * W2BK + w2swz(r, lane & 3) * 8;
+  }
+  {
+    const int r = 16 * wv + (lane >> 2);
+    srcB[0] = B + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + (size_t)kt0 * W2BK + w2swz(r, lane & 3) * 8;
+  }
+  auto piece = [&](int buf, int t, int p) {
+    bf16* base = smem + buf * BUF;
+    const int ko = t * W2BK;
+    if (p < AI)
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcA[p] + ko), (lds_vptr_w)(base + (wv * AI + p) * 512), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcB[0] + ko), (lds_vptr_w)(base + AEL + wv * 512), 16, 0, 0);
+  };
+
+  f32x4 acc[RT][4];
+#pragma unroll
+  for (int a = 0; a < RT; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  int aoff[RT], boff[4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int row = wm * (BM / 4) + rt * 16 + fr;
+    aoff[rt] = row * W2BK + w2swz(row, fq) * 8;
+  }
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const int row = wn * 64 + ct * 16 + fr;
+    boff[ct] = AEL + row * W2BK + w2swz(row, fq) * 8;
+  }
+  auto read = [&](int buf, bf16x8 (&fa)[RT], bf16x8 (&fb)[4]) {
+    const bf16* base = smem + buf * BUF;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) fb[ct] = *reinterpret_cast<const bf16x8*>(base + boff[ct]);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) fa[rt] = *reinterpret_cast<const bf16x8*>(base + aoff[rt]);
+  };
+  // MFMAs of one tile with the G LDS-DMA pieces of tile `st` (into buffer `sbuf`) spread between them
+  auto mfmas = [&](const bf16x8 (&fa)[RT], const bf16x8 (&fb)[4], int sbuf, int st) {
+    constexpr int NMF = RT * 4;
+    constexpr int EVERY = NMF / (G + 1);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt], fb[ct], acc[rt][ct], 0, 0, 0);
+        const int i = rt * 4 + ct + 1;
+        if (i % EVERY == 0 && i / EVERY <= G) piece(sbuf, st, i / EVERY - 1);
+      }
+  };
+
+  // The loop is branch-free (a branch around the reads makes hipcc wait lgkmcnt(0) before the
+  // MFMAs, serialising exactly what the pipeline overlaps): every step stages a tile, past the
+  // end a re-load of the last tile (an L2 hit) into a buffer that is never read again.  nt is
+  // even (K % 64 == 0), so the two-step unroll needs no tail.
+  bf16x8 fa0[RT], fb0[4], fa1[RT], fb1[4];
+  if (nt > 0) {
+#pragma unroll
+    for (int p = 0; p < NBUF - 1; ++p)
+#pragma unroll
+      for (int q = 0; q < G; ++q) piece(p, min(p, nt - 1), q);
+    wait2<G>(NBUF - 2);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read(0, fa0, fb0);
+    // step t: tile t+1 lands (vmcnt + barrier) -> its fragments are read while tile t's MFMAs
+    // (fragments in registers since step t-1) run, and tile t+NBUF-1 is staged into the buffer
+    // of tile t-1 (every wave passed this barrier after consuming tile t-1's fragments)
+    int rb = 1, sb = NBUF - 1;
+    auto step = [&](int t, bf16x8 (&fac)[RT], bf16x8 (&fbc)[4], bf16x8 (&fan)[RT], bf16x8 (&fbn)[4]) {
+      wait2<G>(NBUF - 3);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      read(rb, fan, fbn);
+      mfmas(fac, fbc, sb, min(t + NBUF - 1, nt - 1));
+      rb = rb == NBUF - 1 ? 0 : rb + 1;
+      sb = sb == NBUF - 1 ? 0 : sb + 1;
+    };
+    for (int t = 0; t < nt; t += 2) {
+      step(t, fa0, fb0, fa1, fb1);
+      step(t + 1, fa1, fb1, fa0, fb0);
+    }
+    // no LDS-DMA may still be writing when the workgroup's LDS is handed to the next one
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
+}
+
+// mode 0: C = A B^T;  mode 1: SwiGLU, C[M, N/2] = silu(A Bg^T) * (A Bu^T) with B = [Bg; Bu];
+// mode 2: leave f32 split-K partials in ws (no reduce; S > 1 required).
+// Returns the effective number of K slices S (the partial slabs a deferred reduce must sum).
+int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
+              int mode, int variant, uintptr_t stream) {
+  DLLM_HOST_CHECK(M >= 1, "M >= 1");
+  DLLM_HOST_CHECK(K % WBK == 0, "K must be a multiple of 64");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");
+  const bool swiglu = mode == 1;
+  DLLM_HOST_CHECK(swiglu ? (N % 128 == 0) : (N % WBN == 0), "N must be a multiple of 128");
+  DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int ktiles = K / WBK;
+  const int kts = (ktiles + splits - 1) / splits;
+  const int S = (ktiles + kts - 1) / kts;
+  DLLM_HOST_CHECK(mode != 2 || S > 1, "mode 2 needs a K split");
+  const int BM = M <= 128 ? 128 : 256;
+  const int mtiles = (M + BM - 1) / BM;
+  const int ntiles = swiglu ? (N / 2) / 64 : N / WBN;
+  const long grid = (long)ntiles * mtiles * S;
+  DLLM_HOST_CHECK(grid >= 1 && grid < (1L << 31), "grid");
+  if (S > 1) DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
+
+#define DLLM_WIDE_GO3(BM_, SPLIT_, SW_, V_)                                                                      \
+  hipLaunchKernelGGL((gemm_wide_kernel<BM_, SPLIT_, SW_, 3, V_>), dim3((unsigned)grid), dim3(512), 0, s,          \
+                     (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S)
+#define DLLM_WIDE_GO(BM_, SPLIT_, SW_)                                                                          \
+  do {                                                                                                         \
+    if (variant == 3)                                                                                          \
+      hipLaunchKernelGGL((gemm_wide2_kernel<BM_, SPLIT_, SW_, 6>), dim3((unsigned)grid), dim3(512), 0, s,      \
+                         (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S);               \
+    else if (variant == 1) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 1);                                                      \
+    else if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 2);                                                 \
+    else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 0);                                                                   \
+  } while (0)
+  if (S == 1) {
+    if (BM == 128) { if (swiglu) DLLM_WIDE_GO(128, false, true); else DLLM_WIDE_GO(128, false, false); }
+    else { if (swiglu) DLLM_WIDE_GO(256, false, true); else DLLM_WIDE_GO(256, false, false); }
+    DLLM_HIP_CHECK(hipGetLastError());
+    return 1;
+  }
+  if (BM == 128) { if (swiglu) DLLM_WIDE_GO(128, true, true); else DLLM_WIDE_GO(128, true, false); }
+  else { if (swiglu) DLLM_WIDE_GO(256, true, true); else DLLM_WIDE_GO(256, true, false); }
+#undef DLLM_WIDE_GO
+#undef DLLM_WIDE_GO3
+  DLLM_HIP_CHECK(hipGetLastError());
+  if (mode == 2) return S;
+  splitk_reduce_ex(c, ws, 0, S, M, N, swiglu ? 1 : 0, stream);
+  return S;
+}
+
+}  // namespace dllm

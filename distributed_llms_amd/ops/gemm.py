@@ -3,7 +3,10 @@
 * small M (decode, M <= 2..16 by weight size): hand-written weight-streaming MFMA kernel
   (csrc/kernels/gemm_skinny.hip), 8 waves per workgroup split K and reduce in LDS; optional
   fused SwiGLU epilogue;
-* 64 <= M <= 512 with K >= 8192: split-K LDS-tiled MFMA kernel (gemm_tiled.hip);
+* 64 < M <= 512: wide-M kernel (gemm_wide.hip: 256 x 128 tiles with all decode rows, 3-stage
+  LDS-DMA pipeline, fused SwiGLU for the MLP up projection, deferred split-K for the down
+  projection), selected by DLLM_WIDE;
+* otherwise 64 <= M <= 512 with K >= 8192: split-K LDS-tiled MFMA kernel (gemm_tiled.hip);
 * larger M (prefill) or shapes the kernel does not tile: plain library GEMM (hipBLASLt via
   torch).  That is the only non-HIP GPU path and it is purely shape-based.
 """
@@ -68,6 +71,29 @@ def _use_tiled(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool
     return GEMM_MODE == "tiled" or k >= 8192 or n <= TILED_NMAX
 
 
+# DLLM_WIDE: which decode-sized (64 < M <= 512) GEMMs the wide-M kernel (gemm_wide.hip) serves:
+#   comma list of gate_up (SwiGLU-fused MLP up projection), down (K >= 8192, deferred split-K),
+#   proj (the other projections: qkv, o), all, or none.  Default "auto", from the in-engine A/B
+#   (scripts/gpu_ab_wide.sh, profiles/wide_gemm.md): gate_up + down for M <= 512 (+4.3 % at
+#   B=256, +5.8 % at B=128, +1.2 % at B=512), proj only up to M = 256 (it loses at 512).
+WIDE = {t for t in os.environ.get("DLLM_WIDE", "auto").split(",") if t and t != "none"}
+WIDE_VARIANT = int(os.environ.get("DLLM_WIDE_VARIANT", "1"))
+
+
+def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
+    if not WIDE or GEMM_MODE == "blas" or not (64 < m <= 512) or n % 128 or k % 64:
+        return False
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        return False
+    if "all" in WIDE:
+        return True
+    if "auto" in WIDE:
+        return swiglu or k >= 8192 or m <= 256
+    if swiglu:
+        return "gate_up" in WIDE
+    return ("down" in WIDE) if k >= 8192 else ("proj" in WIDE)
+
+
 class SplitKPartial:
     """f32 split-K partial sums of ``x @ w.T`` still in the per-stream workspace (not reduced).
 
@@ -106,6 +132,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         y = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
         _launch(x, w, bias, y, m, n, k, 0)
         return y
+    if bias is None and _use_wide(m, n, k, x, w):
+        return linear_wide(x, w, defer=defer)
     if _use_tiled(m, n, k, x, w) and (bias is None or bias.dtype == torch.bfloat16):
         if defer and bias is None:
             return linear_tiled(x, w, None, defer=True)
@@ -158,12 +186,48 @@ def linear_tiled(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     return y
 
 
+def wide_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 256) -> int:
+    """K slices for gemm_wide: about one workgroup per CU, >= 8 K-tiles (512) per slice."""
+    tiles = (n // 128) * (-(-m // (128 if m <= 128 else 256)))
+    s = max(1, round(target_wgs / tiles))
+    return max(1, min(s, (k // 64) // 8, 16))
+
+
+def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = False, defer: bool = False,
+                variant: int = -1):
+    """Wide-M decode GEMM (csrc/kernels/gemm_wide.hip): 256 x 128 x 64 tiles, 3-deep LDS-DMA pipeline,
+    optional split-K and fused SwiGLU epilogue (``w`` = [Wg; Wu]).  ``defer``: may return a
+    :class:`SplitKPartial` (no SwiGLU)."""
+    k = x.shape[-1]
+    n = w.shape[0]
+    m = x.numel() // k
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        raise ValueError("linear_wide: bf16 contiguous operands")
+    if n % 128 or k % 64:
+        raise ValueError("linear_wide: N % 128 and K % 64")
+    s = splits or wide_splits(m, n, k, swiglu)
+    ws = _workspace(x.device)
+    if s > 1 and s * m * n > ws.numel():
+        s = max(1, ws.numel() // (m * n))
+    stream = torch.cuda.current_stream().cuda_stream
+    v = WIDE_VARIANT if variant < 0 else variant
+    if defer and not swiglu and s > 1:
+        se = _ext.kernels().gemm_wide(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, v, stream)
+        return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
+    y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
+    _ext.kernels().gemm_wide(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s,
+                             1 if swiglu else 0, v, stream)
+    return y
+
+
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor, force_skinny: bool = False) -> Optional[torch.Tensor]:
     """silu(x Wg^T) * (x Wu^T) with W = [Wg; Wu] in one launch; None if the shape is not eligible."""
     k = x.shape[-1]
     n = w_gate_up.shape[0]
     m = x.numel() // k
     if not skinny_ok(m, n, k, x, w_gate_up, swiglu=True, force=force_skinny):
+        if not force_skinny and _use_wide(m, n, k, x, w_gate_up, swiglu=True):
+            return linear_wide(x, w_gate_up, swiglu=True)
         return None
     y = torch.empty(*x.shape[:-1], n // 2, dtype=x.dtype, device=x.device)
     _launch(x, w_gate_up, None, y, m, n, k, 1)

@@ -118,3 +118,32 @@ def test_tuned_gemm_table_loads_and_matches(cuda):
     x = (torch.randn(256, 4096, device="cuda") * 0.5).to(torch.bfloat16)
     w = (torch.randn(28672, 4096, device="cuda") * 0.02).to(torch.bfloat16)
     torch.testing.assert_close(F.linear(x, w).float(), x.float() @ w.float().T, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [1, 100, 128, 129, 256, 384, 512])
+@pytest.mark.parametrize("n,k,splits", [(6144, 4096, 1), (6144, 4096, 5), (4096, 14336, 8), (4096, 4096, 3),
+                                        (1024, 512, 1)])
+@pytest.mark.parametrize("variant", [0, 3])
+def test_wide_linear(cuda, m, n, k, splits, variant):
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear_wide(x, w, splits=splits, variant=variant)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [7, 128, 256, 300])
+@pytest.mark.parametrize("inter,k,splits", [(14336, 4096, 1), (1024, 512, 1), (1024, 1024, 2)])
+@pytest.mark.parametrize("variant", [0, 1, 3])
+def test_wide_swiglu(cuda, m, inter, k, splits, variant):
+    x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
+    y = gemm.linear_wide(x, w, splits=splits, swiglu=True, variant=variant)
+    gu = x.float() @ w.float().t()
+    ref = F.silu(gu[:, :inter]) * gu[:, inter:]
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+def test_wide_deferred_splitk_matches_materialized(cuda):
+    x, w = _bf(256, 14336), _bf(4096, 14336, scale=0.02)
+    p = gemm.linear_wide(x, w, splits=8, defer=True)
+    assert isinstance(p, gemm.SplitKPartial) and p.splits == 8
+    y = p.materialize()
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
