@@ -140,7 +140,38 @@ struct RopeArgs {
   const int32_t* positions; // [B]
   const float* cos_sin;     // [max_pos, D] (first half cos, second half sin) or null (no RoPE)
   const int32_t* slots;     // [B] cache slot of the new token
+  // optional: the qkv projection as S f32 split-K partial slabs [S][B][(hq + 2 hkv) * D] (qkv
+  // unused); summed in slab order and rounded to bf16 -- bit-identical to splitk_reduce + bf16
+  const float* part = nullptr;
+  int nparts = 0;
+  long slab = 0;
 };
+
+// 8 consecutive qkv elements starting at row offset `off` of sequence b (bf16 or summed partials)
+__device__ __forceinline__ bf16x8 qkv_load8(const RopeArgs& ra, int b, int width, int off) {
+  if (ra.part == nullptr) return *reinterpret_cast<const bf16x8*>(ra.qkv + (size_t)b * width + off);
+  const float* p = ra.part + (size_t)b * width + off;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < ra.nparts; ++s) {
+    a0 += *reinterpret_cast<const f32x4*>(p + s * ra.slab);
+    a1 += *reinterpret_cast<const f32x4*>(p + s * ra.slab + 4);
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = f2bf(a0[j]);
+    o[j + 4] = f2bf(a1[j]);
+  }
+  return o;
+}
+
+__device__ __forceinline__ bf16 qkv_load1(const RopeArgs& ra, int b, int width, int off) {
+  if (ra.part == nullptr) return ra.qkv[(size_t)b * width + off];
+  const float* p = ra.part + (size_t)b * width + off;
+  float a = 0.f;
+  for (int s = 0; s < ra.nparts; ++s) a += p[s * ra.slab];
+  return f2bf(a);
+}
 
 template <int D, bool FUSED>
 __device__ __forceinline__ void rope_rotate(bf16x8 (&f)[D / 32], const float* cs, int g) {
@@ -186,17 +217,15 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
   bf16x8 kn[D / 32];
   bf16 vn[D / 16];
   if (FUSED) {
-    const bf16* row = ra.qkv + (size_t)b * (hq + 2 * hkv) * D;
-    const bf16* qrow = row + (size_t)(kvh * G + (col_ok ? r : 0)) * D;
-    const bf16* krow = row + (size_t)(hq + kvh) * D;
-    const bf16* vrow = row + (size_t)(hq + hkv + kvh) * D;
+    const int width = (hq + 2 * hkv) * D;
+    const int qo = (kvh * G + (col_ok ? r : 0)) * D, ko = (hq + kvh) * D, vo = (hq + hkv + kvh) * D;
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
-      qf[ks] = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
-      kn[ks] = *reinterpret_cast<const bf16x8*>(krow + ks * 32 + 8 * g);
+      qf[ks] = qkv_load8(ra, b, width, qo + ks * 32 + 8 * g);
+      kn[ks] = qkv_load8(ra, b, width, ko + ks * 32 + 8 * g);
     }
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) vn[dt] = vrow[dt * 16 + r];
+    for (int dt = 0; dt < D / 16; ++dt) vn[dt] = qkv_load1(ra, b, width, vo + dt * 16 + r);
   } else {
     const bf16* qrow = q + ((size_t)b * hq + kvh * G + (col_ok ? r : 0)) * D;
 #pragma unroll
@@ -393,7 +422,10 @@ static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr
   DLLM_HOST_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
   DLLM_HOST_CHECK(num_splits >= 1 && split_len % kBS == 0 && split_len > 0, "split_len multiple of 32");
   DLLM_HOST_CHECK(num_splits == 1 || (part_o && part_ml), "split workspace");
-  DLLM_HOST_CHECK(!fused || (ra.qkv && ra.positions && ra.slots), "fused decode needs qkv, positions, slots");
+  DLLM_HOST_CHECK(!fused || ((ra.qkv || ra.part) && ra.positions && ra.slots),
+                  "fused decode needs qkv, positions, slots");
+  DLLM_HOST_CHECK(ra.part == nullptr || (ra.nparts >= 1 && ra.slab >= (long)batch * (hq + 2 * hkv) * d),
+                  "qkv partial slabs");
   if (batch == 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float sl2 = scale * 1.4426950408889634f;
@@ -442,8 +474,9 @@ void paged_attention_decode_rope(uintptr_t out, uintptr_t qkv, uintptr_t positio
                                  uintptr_t k_cache, uintptr_t v_cache, uintptr_t block_tables, uintptr_t seq_lens,
                                  uintptr_t part_o, uintptr_t part_ml, int batch, int hq, int hkv, int d,
                                  int block_size, int max_blocks, int num_splits, int split_len, float scale,
-                                 uintptr_t stream) {
-  RopeArgs ra{(const bf16*)qkv, (const int32_t*)positions, (const float*)cos_sin, (const int32_t*)slots};
+                                 uintptr_t qkv_part, int qkv_nparts, long qkv_slab, uintptr_t stream) {
+  RopeArgs ra{(const bf16*)qkv, (const int32_t*)positions, (const float*)cos_sin, (const int32_t*)slots,
+              (const float*)qkv_part, qkv_nparts, qkv_slab};
   decode_launch(out, 0, k_cache, v_cache, block_tables, seq_lens, part_o, part_ml, batch, hq, hkv, d, block_size,
                 max_blocks, num_splits, split_len, scale, ra, true, stream);
 }

@@ -27,6 +27,11 @@ from . import weights as W
 
 # decode: RoPE + KV append fused into the attention kernel (one launch); DLLM_FUSED_ROPE=0 -> two launches
 FUSED_ROPE_DECODE = os.environ.get("DLLM_FUSED_ROPE", "1") != "0"
+# split-K partials handed to the consumer instead of reduced by a separate launch (A/B knobs):
+#   qkv -> the fused decode attention kernel sums them (every wave re-reads S f32 slabs on its
+#   critical path: -3 % at B=256, off by default); o -> the MLP half's add + RMSNorm (+1 %)
+DEFER_QKV = os.environ.get("DLLM_DEFER_QKV", "0") == "1"   # measured -3 %: off
+DEFER_O = os.environ.get("DLLM_DEFER_O", "1") != "0"
 
 
 @dataclass
@@ -171,10 +176,16 @@ class ModelStage:
             return self._forward_gpt2(inp, meta)
         return self._forward_llama(inp, meta)
 
-    def _attention(self, qkv: torch.Tensor, li: int, meta: BatchMeta) -> torch.Tensor:
+    def _attention(self, qkv, li: int, meta: BatchMeta) -> torch.Tensor:
+        """``qkv``: [T, (Hq + 2 Hkv) D] or, from a split-K projection, a SplitKPartial that the fused
+        decode kernel reduces itself (any other path materialises it)."""
         cfg = self.cfg
         k_cache, v_cache = self.kv.layer(li)
-        if not meta.is_prefill and qkv.is_cuda and FUSED_ROPE_DECODE:
+        fused = not meta.is_prefill and FUSED_ROPE_DECODE and \
+            (isinstance(qkv, ops.gemm.SplitKPartial) or qkv.is_cuda)
+        if not fused and isinstance(qkv, ops.gemm.SplitKPartial):
+            qkv = qkv.materialize()
+        if fused:
             o = ops.paged_attention_decode_rope(qkv, meta.positions, self.cos_sin, k_cache, v_cache, meta.slot_mapping,
                                                 meta.block_tables, meta.seq_lens, cfg.num_heads, cfg.num_kv_heads,
                                                 cfg.head_dim, self.scale, max_ctx=meta.max_ctx or None,
@@ -214,8 +225,9 @@ class ModelStage:
             else:
                 x, residual = ops.fused_add_rms_norm(h, residual, norm_w, eps)
             if is_attn:
-                a = self._attention(ops.linear(x, lw["wqkv"]), self.kv_index[l], meta)
-                h = ops.linear(a, lw["wo"])
+                a = self._attention(ops.linear(x, lw["wqkv"], defer=DEFER_QKV), self.kv_index[l], meta)
+                # defer: a split-K o-projection's reduce is fused into the MLP half's add + RMSNorm
+                h = ops.linear(a, lw["wo"], defer=DEFER_O)
             else:
                 h = self._mlp(x, lw)
         if isinstance(h, ops.gemm.SplitKPartial):

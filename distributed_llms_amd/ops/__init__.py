@@ -236,21 +236,32 @@ def paged_attention_decode_rope(qkv, positions, cos_sin, k_cache, v_cache, slot_
     """Decode attention with RoPE + KV-cache append fused in (one launch instead of two): reads the raw
     qkv projection [B, (Hq + 2 Hkv) * D], appends each sequence's new k / v at ``slot_mapping`` and
     attends over the whole context including it.  Same result as ``rope_cache_append`` followed by
-    ``paged_attention_decode`` (the new key is folded in last instead of inside its block)."""
-    if not _gpu(qkv):
+    ``paged_attention_decode`` (the new key is folded in last instead of inside its block).
+
+    ``qkv`` may be a :class:`gemm.SplitKPartial`: the kernel then sums the f32 split-K slabs itself
+    (bit-identical to reducing first), which removes the reduce launch and the bf16 round trip."""
+    part = None
+    if isinstance(qkv, gemm.SplitKPartial):
+        part = qkv
+        if len(part.shape) != 2:
+            raise ValueError("qkv partial must be [B, (Hq + 2 Hkv) * D]")
+        b, width, qdtype, qdev = part.m, part.n, part.dtype, part.device
+    else:
+        b, width, qdtype, qdev = qkv.shape[0], qkv.shape[-1], qkv.dtype, qkv.device
+    if part is None and not _gpu(qkv):
         q = ref.rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, num_heads, num_kv_heads,
                                   head_dim)
         return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
-    _ck(qkv, "attn.qkv")
+    if part is None:
+        _ck(qkv, "attn.qkv")
     _ck(k_cache, "k_cache")
     _ck(v_cache, "v_cache")
     _ck(positions, "positions", torch.int32)
     _ck(slot_mapping, "slot_mapping", torch.int32)
     _ck(block_tables, "block_tables", torch.int32)
     _ck(seq_lens, "seq_lens", torch.int32)
-    b = qkv.shape[0]
     hq, hkv, d = num_heads, num_kv_heads, head_dim
-    if qkv.shape[1] != (hq + 2 * hkv) * d:
+    if width != (hq + 2 * hkv) * d:
         raise ValueError("qkv width mismatch")
     if cos_sin is not None:
         _ck(cos_sin, "cos_sin", torch.float32)
@@ -263,21 +274,24 @@ def paged_attention_decode_rope(qkv, positions, cos_sin, k_cache, v_cache, slot_
     if max_ctx > max_blocks * bs:
         raise ValueError("max_ctx exceeds block table capacity")
     splits, split_len = decode_split_plan(b, hkv, max_ctx, bs, max_blocks)
-    out = torch.empty(b, hq, d, dtype=qkv.dtype, device=qkv.device)
+    out = torch.empty(b, hq, d, dtype=qdtype, device=qdev)
     po = pml = 0
     if splits > 1:
         if workspace is None:
-            po_t = torch.empty(b * hq * splits * d, dtype=torch.float32, device=qkv.device)
-            pml_t = torch.empty(b * hq * splits * 2, dtype=torch.float32, device=qkv.device)
+            po_t = torch.empty(b * hq * splits * d, dtype=torch.float32, device=qdev)
+            pml_t = torch.empty(b * hq * splits * 2, dtype=torch.float32, device=qdev)
         else:
             po_t, pml_t = workspace
             if po_t.numel() < b * hq * splits * d or pml_t.numel() < b * hq * splits * 2:
                 raise ValueError("attention workspace too small")
         po, pml = po_t.data_ptr(), pml_t.data_ptr()
     _ext.kernels().paged_attention_decode_rope(
-        out.data_ptr(), qkv.data_ptr(), positions.data_ptr(), 0 if cos_sin is None else cos_sin.data_ptr(),
+        out.data_ptr(), 0 if part is not None else qkv.data_ptr(), positions.data_ptr(),
+        0 if cos_sin is None else cos_sin.data_ptr(),
         slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), seq_lens.data_ptr(),
-        po, pml, b, hq, hkv, d, bs, max_blocks, splits, split_len, float(scale), _stream())
+        po, pml, b, hq, hkv, d, bs, max_blocks, splits, split_len, float(scale),
+        0 if part is None else part.ws.data_ptr(), 0 if part is None else part.splits,
+        0 if part is None else part.m * part.n, _stream())
     return out
 
 

@@ -158,3 +158,28 @@ def test_attention_masked_spike(cuda):
     out = ops.paged_attention_decode(q, k, v, bt, sl, 1 / math.sqrt(d))
     expect = ref.paged_attention_decode(q.float(), k.float(), v.float(), bt, sl, 1 / math.sqrt(d))
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("b", [100, 256])
+def test_decode_rope_consumes_splitk_qkv_bit_exact(cuda, b):
+    """The fused decode kernel summing the qkv projection's f32 split-K slabs itself gives exactly
+    the result of reducing first (same slab order, same bf16 rounding)."""
+    from distributed_llms_amd.ops import gemm
+    hq, hkv, d, hidden = 32, 8, 128, 4096
+    lens = [int(x) for x in torch.randint(40, 300, (b,))]
+    k, v, bt = _fill_paged(lens, hkv, d)
+    x = _bf(b, hidden)
+    w = _bf((hq + 2 * hkv) * d, hidden, scale=0.02)
+    sl = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    pos = sl - 1
+    slots = torch.stack([bt[i, (lens[i] - 1) // 32] * 32 + (lens[i] - 1) % 32 for i in range(b)]).to(torch.int32)
+    cs = ref.rope_cos_sin(d, 4096, 500000.0, device="cuda")
+    part = gemm.linear_wide(x, w, splits=5, defer=True)
+    assert isinstance(part, gemm.SplitKPartial)
+    k1, v1, k2, v2 = k.clone(), v.clone(), k.clone(), v.clone()
+    o1 = ops.paged_attention_decode_rope(part, pos, cs, k1, v1, slots, bt, sl, hq, hkv, d, 1 / math.sqrt(d))
+    qkv = part.materialize()
+    o2 = ops.paged_attention_decode_rope(qkv, pos, cs, k2, v2, slots, bt, sl, hq, hkv, d, 1 / math.sqrt(d))
+    torch.testing.assert_close(o1, o2, atol=0, rtol=0)
+    torch.testing.assert_close(k1, k2, atol=0, rtol=0)
+    torch.testing.assert_close(v1, v2, atol=0, rtol=0)
