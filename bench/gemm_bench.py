@@ -93,9 +93,8 @@ def wide(a, flush):
             # one HIP graph per implementation: `copies` back-to-back calls, each on its own weight
             # copy (launch overhead out of the measurement, like the engine's captured decode step)
             impls = {
-                "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=0),
-                "wide1": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=1),
-                "wide2": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=3),
+                "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=1),
+                "wide0": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=0),
                 "tiled": lambda w: gemm.linear_tiled(x, w, swiglu=sw),
                 "blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w)),
             }
@@ -123,7 +122,7 @@ def wide(a, flush):
             byt, fl_ = n * k * 2, 2.0 * m * n * k
             print(f"{name:12s} {m:4d} {t['wide']*1e6:8.1f} {byt/t['wide']/1e12:6.2f} {fl_/t['wide']/1e12:6.0f} "
                   f"{t['tiled']*1e6:8.1f} {t['blas']*1e6:8.1f} {t['tiled']/t['wide']:8.2f} {t['blas']/t['wide']:8.2f} "
-                  f"v1 {t['wide1']*1e6:6.1f} v2 {t['wide2']*1e6:6.1f}",
+                  f"variant0 {t['wide0']*1e6:6.1f}",
                   flush=True)
 
 

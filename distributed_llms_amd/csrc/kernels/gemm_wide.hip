@@ -24,7 +24,14 @@
 //  * optional split-K: f32 partial slabs in natural column order, reduced by the next op
 //    (splitk_add_rms_norm) or by splitk_reduce(_swiglu);
 //  * XCD-aware block order (bijective remap): the M tiles and K slices of one N tile run
-//    back-to-back on one XCD.
+//    back-to-back on one XCD;
+//  * the next tile's LDS-DMA pieces are issued between the MFMAs (pinned with
+//    sched_group_barrier): +9 % on the MLP up projection over issuing them after the barrier.
+// Measured and dropped (profiles/wide_gemm.md): BK = 32 with 6 stages and a fragment software
+// pipeline (slower: twice the barriers), 4/5 stages at BM = 128, weights pre-tiled into
+// contiguous 16 KiB tiles (+0-3 %), setprio, other read/MFMA/VMEM orders.  Ablations at M = 256:
+// no LDS reads = same time, no barrier = same time, no staging loads = -21 % -- the loop is bound
+// by the load pipeline with a ~50 %-busy MFMA phase behind it.
 #include "common.h"
 #include "launchers.h"
 
@@ -207,7 +214,7 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
             if (i % EVERY == 0 && i / EVERY <= G) piece(dst, ko, i / EVERY - 1);
           }
         }
-    if constexpr (STG && VAR == 1) {
+    if constexpr (STG) {
       // pin the interleave: 8 LDS reads of substep 0, then (EVERY MFMAs, 1 VMEM) x G, rest
       __builtin_amdgcn_sched_group_barrier(0x100, 2 * (RT + 4), 0);
 #pragma unroll
@@ -254,163 +261,6 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
   wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
 }
 
-// ---------------------------------------------------------------------------------------------
-// gemm_wide2: the same tile (BM x 128, 8 waves 4 x 2) with BK = 32 and a software pipeline on
-// the MFMA fragments.  In gemm_wide every wave reads its K-tile's fragments right after the
-// barrier, so all 8 waves wait on the LDS (512 array cycles per 64-deep K-tile) with the MFMA
-// pipe idle.  Here the fragments of tile t+1 are read from LDS while the MFMAs of tile t (held in
-// registers since the previous step) execute, and the LDS-DMA pieces of tile t+NBUF-1 are issued
-// in between those MFMAs.  32-deep tiles halve the LDS footprint per stage, so NBUF = 6 stages
-// (144 KiB at BM = 256) keep NBUF-3 tiles in flight while one is landing and one is being read.
-//
-// LDS image per stage: A [BM][32] then B [128][32] bf16, 64-B rows, lane-linear glds (one
-// wave-instruction = 16 rows x 64 B).  16-B chunk c of row r is stored at c ^ f(r) with
-// f(r) = (0x78 >> 2 * ((r >> 2) & 3)) & 3: the four 16-lane groups of a ds_read_b128
-// ({0-3,12-15,20-27}, ...) then hit 16 distinct 16-B bank slots (conflict-free).
-// ---------------------------------------------------------------------------------------------
-namespace {
-constexpr int W2BK = 32;
-__device__ __forceinline__ int w2swz(int row, int chunk) { return chunk ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3); }
-
-template <int G>
-__device__ __forceinline__ void wait2(int younger) {
-  static_assert(G == 2 || G == 3, "G");
-#define DLLM_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
-  if (younger <= 0) { DLLM_VM(0); return; }
-  if constexpr (G == 2) {
-    if (younger == 1) DLLM_VM(2); else if (younger == 2) DLLM_VM(4); else if (younger == 3) DLLM_VM(6);
-    else DLLM_VM(8);
-  } else {
-    if (younger == 1) DLLM_VM(3); else if (younger == 2) DLLM_VM(6); else if (younger == 3) DLLM_VM(9);
-    else DLLM_VM(12);
-  }
-#undef DLLM_VM
-}
-}  // namespace
-
-template <int BM, bool SPLIT, bool SWIGLU, int NBUF>
-__global__ void __launch_bounds__(512, 1) gemm_wide2_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                            bf16* __restrict__ C, float* __restrict__ P, int M, int N,
-                                                            int K, int kt64_per_split, int nsplit) {
-  constexpr int AEL = BM * W2BK, BEL = WBN * W2BK, BUF = AEL + BEL;   // bf16 elements per stage
-  constexpr int AI = BM / 128;                // A glds per thread per tile (16 rows x 64 B each)
-  constexpr int BI = 1;                       // B: 128 rows = 8 instructions = 1 per wave
-  constexpr int G = AI + BI;
-  constexpr int RT = BM / 64;
-  static_assert(NBUF >= 4 && NBUF * BUF * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BUF];
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
-  const int mtiles = (M + BM - 1) / BM;
-  const int total = gridDim.x;
-  int b = blockIdx.x;
-  {
-    const int q = total >> 3, r = total & 7, x = b & 7;
-    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-  }
-  const int m_t = b % mtiles, rest = b / mtiles;
-  const int split = rest % nsplit, n_t = rest / nsplit;
-  const int m0 = m_t * BM;
-  const int kt0 = split * kt64_per_split * 2;                         // in 32-deep tiles
-  const int nt = max(0, min(K / W2BK, kt0 + kt64_per_split * 2) - kt0);
-
-  const bf16* srcA[AI];
-  const bf16* srcB[BI];
-#pragma unroll
-  for (int j = 0; j < AI; ++j) {
-    const int r = 16 * (wv * AI + j) + (lane >> 2);
-    srcA[j] = A + (size_t)min(m0 + r, M - 1) * K + (size_t)kt0 * W2BK + w2swz(r, lane & 3) * 8;
-  }
-  {
-    const int r = 16 * wv + (lane >> 2);
-    srcB[0] = B + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + (size_t)kt0 * W2BK + w2swz(r, lane & 3) * 8;
-  }
-  auto piece = [&](int buf, int t, int p) {
-    bf16* base = smem + buf * BUF;
-    const int ko = t * W2BK;
-    if (p < AI)
-      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcA[p] + ko), (lds_vptr_w)(base + (wv * AI + p) * 512), 16, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcB[0] + ko), (lds_vptr_w)(base + AEL + wv * 512), 16, 0, 0);
-  };
-
-  f32x4 acc[RT][4];
-#pragma unroll
-  for (int a = 0; a < RT; ++a)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  int aoff[RT], boff[4];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-    const int row = wm * (BM / 4) + rt * 16 + fr;
-    aoff[rt] = row * W2BK + w2swz(row, fq) * 8;
-  }
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const int row = wn * 64 + ct * 16 + fr;
-    boff[ct] = AEL + row * W2BK + w2swz(row, fq) * 8;
-  }
-  auto read = [&](int buf, bf16x8 (&fa)[RT], bf16x8 (&fb)[4]) {
-    const bf16* base = smem + buf * BUF;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) fb[ct] = *reinterpret_cast<const bf16x8*>(base + boff[ct]);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) fa[rt] = *reinterpret_cast<const bf16x8*>(base + aoff[rt]);
-  };
-  // MFMAs of one tile with the G LDS-DMA pieces of tile `st` (into buffer `sbuf`) spread between them
-  auto mfmas = [&](const bf16x8 (&fa)[RT], const bf16x8 (&fb)[4], int sbuf, int st) {
-    constexpr int NMF = RT * 4;
-    constexpr int EVERY = NMF / (G + 1);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt], fb[ct], acc[rt][ct], 0, 0, 0);
-        const int i = rt * 4 + ct + 1;
-        if (i % EVERY == 0 && i / EVERY <= G) piece(sbuf, st, i / EVERY - 1);
-      }
-  };
-
-  // The loop is branch-free (a branch around the reads makes hipcc wait lgkmcnt(0) before the
-  // MFMAs, serialising exactly what the pipeline overlaps): every step stages a tile, past the
-  // end a re-load of the last tile (an L2 hit) into a buffer that is never read again.  nt is
-  // even (K % 64 == 0), so the two-step unroll needs no tail.
-  bf16x8 fa0[RT], fb0[4], fa1[RT], fb1[4];
-  if (nt > 0) {
-#pragma unroll
-    for (int p = 0; p < NBUF - 1; ++p)
-#pragma unroll
-      for (int q = 0; q < G; ++q) piece(p, min(p, nt - 1), q);
-    wait2<G>(NBUF - 2);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    read(0, fa0, fb0);
-    // step t: tile t+1 lands (vmcnt + barrier) -> its fragments are read while tile t's MFMAs
-    // (fragments in registers since step t-1) run, and tile t+NBUF-1 is staged into the buffer
-    // of tile t-1 (every wave passed this barrier after consuming tile t-1's fragments)
-    int rb = 1, sb = NBUF - 1;
-    auto step = [&](int t, bf16x8 (&fac)[RT], bf16x8 (&fbc)[4], bf16x8 (&fan)[RT], bf16x8 (&fbn)[4]) {
-      wait2<G>(NBUF - 3);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      read(rb, fan, fbn);
-      mfmas(fac, fbc, sb, min(t + NBUF - 1, nt - 1));
-      rb = rb == NBUF - 1 ? 0 : rb + 1;
-      sb = sb == NBUF - 1 ? 0 : sb + 1;
-    };
-    for (int t = 0; t < nt; t += 2) {
-      step(t, fa0, fb0, fa1, fb1);
-      step(t + 1, fa1, fb1, fa0, fb0);
-    }
-    // no LDS-DMA may still be writing when the workgroup's LDS is handed to the next one
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
-}
-
 // mode 0: C = A B^T;  mode 1: SwiGLU, C[M, N/2] = silu(A Bg^T) * (A Bu^T) with B = [Bg; Bu];
 // mode 2: leave f32 split-K partials in ws (no reduce; S > 1 required).
 // Returns the effective number of K slices S (the partial slabs a deferred reduce must sum).
@@ -439,12 +289,8 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
                      (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S)
 #define DLLM_WIDE_GO(BM_, SPLIT_, SW_)                                                                          \
   do {                                                                                                         \
-    if (variant == 3)                                                                                          \
-      hipLaunchKernelGGL((gemm_wide2_kernel<BM_, SPLIT_, SW_, 6>), dim3((unsigned)grid), dim3(512), 0, s,      \
-                         (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S);               \
-    else if (variant == 1) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 1);                                                      \
-    else if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 2);                                                 \
-    else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 0);                                                                   \
+    if (variant == 0) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 0);                                                      \
+    else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 1);                                                                   \
   } while (0)
   if (S == 1) {
     if (BM == 128) { if (swiglu) DLLM_WIDE_GO(128, false, true); else DLLM_WIDE_GO(128, false, false); }

@@ -123,7 +123,7 @@ def test_tuned_gemm_table_loads_and_matches(cuda):
 @pytest.mark.parametrize("m", [1, 100, 128, 129, 256, 384, 512])
 @pytest.mark.parametrize("n,k,splits", [(6144, 4096, 1), (6144, 4096, 5), (4096, 14336, 8), (4096, 4096, 3),
                                         (1024, 512, 1)])
-@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("variant", [0, 1])
 def test_wide_linear(cuda, m, n, k, splits, variant):
     x, w = _bf(m, k), _bf(n, k, scale=0.05)
     y = gemm.linear_wide(x, w, splits=splits, variant=variant)
@@ -132,7 +132,7 @@ def test_wide_linear(cuda, m, n, k, splits, variant):
 
 @pytest.mark.parametrize("m", [7, 128, 256, 300])
 @pytest.mark.parametrize("inter,k,splits", [(14336, 4096, 1), (1024, 512, 1), (1024, 1024, 2)])
-@pytest.mark.parametrize("variant", [0, 1, 3])
+@pytest.mark.parametrize("variant", [0, 1])
 def test_wide_swiglu(cuda, m, inter, k, splits, variant):
     x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
     y = gemm.linear_wide(x, w, splits=splits, swiglu=True, variant=variant)
