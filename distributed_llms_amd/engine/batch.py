@@ -135,6 +135,25 @@ def build_host_batch(step: Step, bm, block_size: int, max_blocks: Optional[int] 
                      max_ctx, step.slot, step_id, sampling)
 
 
+def build_decode_batch(seq_ids: np.ndarray, seq_lens: np.ndarray, bm, block_size: int, max_blocks: int,
+                       step_id: int = 0, slot: int = 0) -> HostBatch:
+    """Decode HostBatch straight from arrays (lookahead path: the input ids are not known on the
+    host yet -- they are gathered on the device -- so ``ids`` is a zero placeholder)."""
+    b = seq_ids.shape[0]
+    positions = (seq_lens - 1).astype(np.int32)
+    slots = np.empty(b, dtype=np.int32)
+    n = bm.fill_slots(seq_ids, positions, np.ones(b, dtype=np.int32), slots)
+    assert n == b
+    need_blocks = int(-(-int(seq_lens.max()) // block_size)) if b else 1
+    if max_blocks < need_blocks:
+        raise ValueError("max_blocks too small for batch")
+    bt = np.zeros((b, max_blocks), dtype=np.int32)
+    bm.fill_block_tables(seq_ids, bt, 0)
+    return HostBatch(False, np.zeros(b, dtype=np.int32), positions, slots, seq_lens.astype(np.int32),
+                     np.arange(b + 1, dtype=np.int32), bt, np.arange(b, dtype=np.int32), 1,
+                     int(seq_lens.max()) if b else 0, slot, step_id, None)
+
+
 def to_device_meta(hb: HostBatch, device, pad_ctx_to: Optional[int] = None) -> (torch.Tensor, BatchMeta):
     """Upload a HostBatch; returns (ids tensor, BatchMeta)."""
     dev = torch.device(device)

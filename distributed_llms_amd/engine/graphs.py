@@ -122,11 +122,15 @@ class DecodeGraphRunner:
             if bb > b:
                 self.hidden[b:bb].zero_()
 
-    def run(self, hb: HostBatch, hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Replay the bucket's graph; returns the (static) output truncated to the real batch."""
+    def run(self, hb: HostBatch, hidden: Optional[torch.Tensor] = None,
+            ids_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Replay the bucket's graph; returns the (static) output truncated to the real batch.
+        ``ids_dev``: device-resident input ids overriding ``hb.ids`` (lookahead decode)."""
         b = hb.num_seqs
         bb, cb = self.bucket(b, hb.max_ctx)
         self.load_inputs(hb, bb, hidden)
+        if ids_dev is not None:
+            self.ids[:b].copy_(ids_dev, non_blocking=True)
         entry = self.graphs.get((bb, cb))
         if entry is None:
             entry = self.capture(bb, cb)

@@ -9,15 +9,17 @@ from __future__ import annotations
 
 import collections
 import logging
+import os
 import time
 from typing import Iterable, List, Optional
 
+import numpy as np
 import torch
 
 from .. import _ext
 from ..config import EngineConfig, resolve_device, torch_dtype
 from ..models.stage import ModelStage
-from .batch import build_host_batch
+from .batch import build_decode_batch, build_host_batch
 from .graphs import SCRATCH_SEQ_ID
 from .runner import StageRunner
 from .sampler import sample, step_sampling_args
@@ -70,12 +72,19 @@ class LLMEngine:
         # async slots: each has its own stream, pinned token buffer and completion event
         self.inflight = collections.deque()
         self.busy = [False] * self.num_slots
+        # lookahead: issue a slot's next decode step before completing the one in flight (input
+        # ids gathered on device from the in-flight step's samples), so the host's complete /
+        # schedule / build work overlaps the GPU instead of idling it (DLLM_LOOKAHEAD=0: off)
+        self.lookahead = gpu and os.environ.get("DLLM_LOOKAHEAD", "1") != "0"
+        self.num_lookahead = 0
         if gpu:
             dev = self.stage.device
             self.streams = [torch.cuda.Stream(dev) for _ in range(self.num_slots)]
-            self.tok_host = [torch.empty(max(ecfg.max_batch, 1), dtype=torch.int32).pin_memory()
+            # two pinned token buffers + events per slot: with lookahead two steps of a slot are in flight
+            self.tok_host = [[torch.empty(max(ecfg.max_batch, 1), dtype=torch.int32).pin_memory() for _ in range(2)]
                              for _ in range(self.num_slots)]
-            self.events = [torch.cuda.Event() for _ in range(self.num_slots)]
+            self.events = [[torch.cuda.Event() for _ in range(2)] for _ in range(self.num_slots)]
+            self.tok_i = [0] * self.num_slots
 
     # ------------------------------------------------------------ requests
     def add_request(self, prompt: List[int], params: Optional[SamplingParams] = None,
@@ -106,28 +115,77 @@ class LLMEngine:
         ids = sample(logits, **step_sampling_args(step.seqs))
         return ids.cpu().tolist()
 
+    def _launch(self, step: Step, hb, slot: int, ids_src: Optional[torch.Tensor] = None, keep=None):
+        """``ids_src`` (lookahead): the in-flight step's sampled ids on the device, rows ``keep``
+        (None = all) become this step's input ids.  The gather runs on the slot's stream, behind
+        the sampling that produces ``ids_src``."""
+        s = self.streams[slot]
+        s.wait_stream(torch.cuda.current_stream())
+        i = self.tok_i[slot]
+        self.tok_i[slot] ^= 1
+        with torch.cuda.stream(s):
+            ids_dev = None
+            if ids_src is not None:
+                ids_dev = ids_src if keep is None else ids_src.index_select(
+                    0, torch.tensor(keep, dtype=torch.int64).pin_memory().to(ids_src.device, non_blocking=True))
+            logits = self.runner.execute(hb, slot=slot, ids_dev=ids_dev)
+            ids = sample(logits, **step_sampling_args(step.seqs))
+            n = ids.shape[0]
+            self.tok_host[slot][i][:n].copy_(ids, non_blocking=True)
+            self.events[slot][i].record(s)
+        self.inflight.append((step, slot, n, i, ids))
+        self.busy[slot] = True
+
     def _issue(self, slot: int) -> bool:
         step = self.scheduler.schedule(slot)
         if step is None:
             return False
-        hb = self._host_batch(step)
-        s = self.streams[slot]
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            logits = self.runner.execute(hb, slot=slot)
-            ids = sample(logits, **step_sampling_args(step.seqs))
-            n = ids.shape[0]
-            self.tok_host[slot][:n].copy_(ids, non_blocking=True)
-            self.events[slot].record(s)
-        self.inflight.append((step, slot, n))
-        self.busy[slot] = True
+        self._launch(step, self._host_batch(step), slot)
+        return True
+
+    def _issue_lookahead(self, slot: int) -> bool:
+        """Issue the decode step that follows the slot's newest in-flight decode step, before that
+        step's tokens reach the host.  Sequences that step will finish by length are left out;
+        one finishing by EOS (unknowable here) computes one throw-away row, skipped by complete().
+        Safe for the KV pool: blocks freed on completion are only reused by later steps on the
+        same stream.  Returns False (caller falls back to the synchronous path) when anything
+        needs the host first: waiting requests, non-decode steps, KV growth failures."""
+        if not self.lookahead or self.scheduler.waiting or not self.inflight:
+            return False
+        prev, pslot, pn, _, pids = self.inflight[-1]
+        if pslot != slot or prev.is_prefill or len(self.inflight) > 1:
+            return False
+        sch = self.scheduler
+        keep, lens = [], []
+        for j, seq in enumerate(prev.seqs):
+            if seq.finished:
+                continue
+            total = len(seq.prompt) + len(seq.output) + 1        # after the in-flight step
+            if len(seq.output) + 1 >= seq.params.max_new_tokens or total >= sch.max_seq_len:
+                continue                                        # finishes by length there
+            keep.append(j)
+            lens.append(total)
+        if not keep:
+            return False
+        seqs = [prev.seqs[j] for j in keep]
+        seq_ids = np.fromiter((q.seq_id for q in seqs), dtype=np.int64, count=len(seqs))
+        lens_a = np.asarray(lens, dtype=np.int64)
+        if self.bm.ensure_capacity_batch(seq_ids, lens_a) >= 0:
+            return False
+        step = Step(False, seqs, slot)
+        hb = build_decode_batch(seq_ids, lens_a.astype(np.int32), self.bm, self.ecfg.kv_block_size,
+                                self.runner.max_blocks, self.step_id, slot)
+        self.step_id += 1
+        self.num_decode_tokens += len(seqs)
+        self._launch(step, hb, slot, ids_src=pids[:pn], keep=None if len(keep) == pn else keep)
+        self.num_lookahead += 1
         return True
 
     def _complete_oldest(self):
-        step, slot, n = self.inflight.popleft()
-        self.events[slot].synchronize()
-        self.scheduler.complete(step, self.tok_host[slot][:n].tolist(), time.perf_counter())
-        self.busy[slot] = False
+        step, slot, n, i, _ = self.inflight.popleft()
+        self.events[slot][i].synchronize()
+        self.scheduler.complete(step, self.tok_host[slot][i][:n].tolist(), time.perf_counter())
+        self.busy[slot] = any(e[1] == slot for e in self.inflight)
 
     def step(self) -> List[Sequence]:
         """One pass over the microbatch slots; returns sequences that finished."""
@@ -139,6 +197,11 @@ class LLMEngine:
             return self.scheduler.pop_finished()
         issued = False
         for slot in range(self.num_slots):
+            if self.busy[slot] and self._issue_lookahead(slot):
+                # the step after the in-flight one is queued behind it: now absorb the older one
+                self._complete_oldest()
+                issued = True
+                continue
             while self.busy[slot]:
                 self._complete_oldest()
             if self._issue(slot):

@@ -72,21 +72,27 @@ class StageRunner:
         return self.graph_sets[0] if self.graph_sets else None
 
     @torch.inference_mode()
-    def execute(self, hb: HostBatch, hidden: Optional[torch.Tensor] = None, slot: int = 0) -> torch.Tensor:
+    def execute(self, hb: HostBatch, hidden: Optional[torch.Tensor] = None, slot: int = 0,
+                ids_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``ids_dev`` (first stage, decode): input token ids already on the device (they replace
+        ``hb.ids``, a placeholder then)."""
         tr = self.tracer
         if not tr.enabled:
-            return self._execute(hb, hidden, slot)
+            return self._execute(hb, hidden, slot, ids_dev)
         kind = "prefill" if hb.is_prefill else "decode"
         gspan = tr.gpu_span(kind, cat="stage") if self.stage.device.type == "cuda" else tr.span(kind, cat="stage")
         with tr.span(f"stage.{kind}", cat="host", rows=hb.num_tokens, seqs=hb.num_seqs, slot=slot), gspan:
-            return self._execute(hb, hidden, slot)
+            return self._execute(hb, hidden, slot, ids_dev)
 
-    def _execute(self, hb: HostBatch, hidden: Optional[torch.Tensor], slot: int) -> torch.Tensor:
+    def _execute(self, hb: HostBatch, hidden: Optional[torch.Tensor], slot: int,
+                 ids_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
         st = self.stage
         gr = self.graph_sets[slot % len(self.graph_sets)] if self.graph_sets else None
         if (not hb.is_prefill) and gr is not None and gr.can_run(hb.num_seqs, hb.max_ctx):
-            return gr.run(hb, hidden)
+            return gr.run(hb, hidden, ids_dev=ids_dev)
         ids, meta = to_device_meta(hb, st.device)
+        if ids_dev is not None:
+            ids = ids_dev.to(torch.int32)
         return st.forward(ids if st.is_first else hidden, meta)
 
     def warmup_graphs(self, batch_sizes=None, ctx_buckets=(256,)):

@@ -186,10 +186,13 @@ def linear_tiled(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     return y
 
 
-def wide_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 256) -> int:
+WIDE_TARGET_WGS = int(os.environ.get("DLLM_WIDE_TARGET", "256"))
+
+
+def wide_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 0) -> int:
     """K slices for gemm_wide: about one workgroup per CU, >= 8 K-tiles (512) per slice."""
     tiles = (n // 128) * (-(-m // (128 if m <= 128 else 256)))
-    s = max(1, round(target_wgs / tiles))
+    s = max(1, round((target_wgs or WIDE_TARGET_WGS) / tiles))
     return max(1, min(s, (k // 64) // 8, 16))
 
 

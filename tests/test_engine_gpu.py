@@ -54,3 +54,33 @@ def test_graph_decode_matches_eager(cuda, name):
 
 def test_native_kernels_used(cuda):
     assert _ext.kernels().arch == "gfx950"
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_lookahead_decode_matches_synchronous(cuda, graphs):
+    """Lookahead (next decode issued before the in-flight step's tokens reach the host, input ids
+    gathered on device) generates exactly what the synchronous loop does: sequences finishing by
+    length at different steps (device gather path) and by EOS (a throw-away row in flight)."""
+    prompts = [[1, 5, 9, 200], [3, 4, 7], list(range(10, 70)), [8] * 33, [9, 9, 9], [2, 3]]
+    lens = [5, 17, 24, 9, 24, 2]
+
+    def run(lookahead, eos=None):
+        _, eng = _engines("tiny-llama", graphs=graphs)
+        eng.lookahead = lookahead
+        if eos is not None:
+            eng.mcfg.eos_token_id = eos
+        seqs = [eng.add_request(p, SamplingParams(max_new_tokens=n, ignore_eos=eos is None))
+                for p, n in zip(prompts, lens)]
+        eng.run_until_done()
+        return [s.output for s in seqs], eng.num_lookahead
+
+    sync, n0 = run(False)
+    la, n1 = run(True)
+    assert n0 == 0 and n1 > 0, "lookahead path never taken"
+    assert la == sync
+    # an EOS id that one sequence produces mid-way (and stops at) in the synchronous run
+    eos = sync[2][7]
+    sync_e, _ = run(False, eos)
+    la_e, _ = run(True, eos)
+    assert la_e == sync_e
+    assert any(len(o) < n for o, n in zip(sync_e, lens)), "EOS never fired"
