@@ -26,6 +26,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("splitk_reduce", &dllm::splitk_reduce);
   m.def("gemm_wide", &dllm::gemm_wide);
   m.def("moe_combine", &dllm::moe_combine);
+  m.def("moe_wide_gemm", &dllm::moe_wide_gemm);
   m.def("paged_attention_decode", &dllm::paged_attention_decode);
   m.def("paged_attention_decode_rope", &dllm::paged_attention_decode_rope);
   m.def("paged_attention_prefill", &dllm::paged_attention_prefill);

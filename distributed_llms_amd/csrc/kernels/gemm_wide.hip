@@ -51,9 +51,11 @@ __device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ ((row >
 // wait until at most `younger` tiles of G LDS-DMA instructions each are still in flight
 template <int G>
 __device__ __forceinline__ void wait_tiles(int younger) {
-  static_assert(G == 4 || G == 6, "G");
+  static_assert(G == 3 || G == 4 || G == 6, "G");
   if (younger <= 0) { DLLM_VM(0); return; }
-  if constexpr (G == 4) {
+  if constexpr (G == 3) {
+    if (younger == 1) DLLM_VM(3); else if (younger == 2) DLLM_VM(6); else DLLM_VM(9);
+  } else if constexpr (G == 4) {
     if (younger == 1) DLLM_VM(4); else if (younger == 2) DLLM_VM(8); else DLLM_VM(12);
   } else {
     if (younger == 1) DLLM_VM(6); else if (younger == 2) DLLM_VM(12); else DLLM_VM(18);
@@ -107,51 +109,16 @@ __device__ __forceinline__ void wide_epilogue(const f32x4 (&acc)[BM / 64][4], bf
   }
 }
 
-template <int BM, bool SPLIT, bool SWIGLU, int NBUF, int VAR>
-__global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                           bf16* __restrict__ C, float* __restrict__ P, int M, int N,
-                                                           int K, int kt_per_split, int nsplit) {
-  constexpr int AEL = BM * WBK, BEL = WBN * WBK, BUF = AEL + BEL;   // bf16 elements
-  constexpr int AI = BM / 64;                 // A glds instructions per thread per tile
-  constexpr int BI = 2;                       // B glds instructions per thread per tile
-  constexpr int G = AI + BI;                  // glds per thread per tile (vmcnt unit)
-  constexpr int RT = BM / 64;                 // 16-row fragments per wave in M
-  static_assert(NBUF >= 3 && NBUF * BUF * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BUF];
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// The K loop shared by the dense and the grouped (MoE) wide kernels: stages A/B tiles through
+// NBUF LDS buffers (LDS-DMA, counted vmcnt, raw barrier) and accumulates acc = A_tile B_tile^T
+// over `nt` 64-deep K-tiles.  srcA/srcB: this lane's staging source for K-tile 0.
+template <int BM, int NBUF, int VAR>
+__device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&srcA)[BM / 64],
+                                              const bf16* const (&srcB)[2], int nt, f32x4 (&acc)[BM / 64][4],
+                                              int wv, int lane) {
+  constexpr int AEL = BM * WBK, BEL = WBN * WBK, BUF = AEL + BEL;
+  constexpr int AI = BM / 64, BI = 2, G = AI + BI, RT = BM / 64;
   const int wm = wv >> 1, wn = wv & 1;
-  const int mtiles = (M + BM - 1) / BM;
-  const int ntiles = SWIGLU ? (N / 2) / 64 : N / WBN;
-  const int total = gridDim.x;
-  // bijective XCD remap: blocks b with b % 8 == x run on XCD x; give XCD x a contiguous run
-  int b = blockIdx.x;
-  {
-    const int q = total >> 3, r = total & 7, x = b & 7;
-    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-  }
-  const int m_t = b % mtiles, rest = b / mtiles;
-  const int split = rest % nsplit, n_t = rest / nsplit;
-  (void)ntiles;
-  const int m0 = m_t * BM;
-  const int kt0 = split * kt_per_split;
-  const int nt = max(0, min(K / WBK, kt0 + kt_per_split) - kt0);
-
-  // per-lane staging sources: instruction i covers tile rows 8i .. 8i+7, lane -> (row, chunk)
-  const bf16* srcA[AI];
-  const bf16* srcB[BI];
-#pragma unroll
-  for (int j = 0; j < AI; ++j) {
-    const int i = wv * AI + j;
-    const int r = 8 * i + (lane >> 3);
-    srcA[j] = A + (size_t)min(m0 + r, M - 1) * K + (size_t)kt0 * WBK + wswz(r, lane & 7) * 8;
-  }
-#pragma unroll
-  for (int j = 0; j < BI; ++j) {
-    const int i = wv * BI + j;
-    const int r = 8 * i + (lane >> 3);
-    srcB[j] = B + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + (size_t)kt0 * WBK + wswz(r, lane & 7) * 8;
-  }
   auto stage = [&](int buf, int t) {
     bf16* base = smem + buf * BUF;
     const int ko = t * WBK;
@@ -164,7 +131,6 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
                                        0, 0);
   };
 
-  f32x4 acc[RT][4];
 #pragma unroll
   for (int a = 0; a < RT; ++a)
 #pragma unroll
@@ -258,7 +224,129 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
     }
   }
 
+}
+
+template <int BM, bool SPLIT, bool SWIGLU, int NBUF, int VAR>
+__global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                           bf16* __restrict__ C, float* __restrict__ P, int M, int N,
+                                                           int K, int kt_per_split, int nsplit) {
+  constexpr int AEL = BM * WBK, BEL = WBN * WBK, BUF = AEL + BEL;   // bf16 elements
+  constexpr int AI = BM / 64;                 // A glds instructions per thread per tile
+  constexpr int BI = 2;                       // B glds instructions per thread per tile
+  constexpr int G = AI + BI;                  // glds per thread per tile (vmcnt unit)
+  constexpr int RT = BM / 64;                 // 16-row fragments per wave in M
+  static_assert(NBUF >= 3 && NBUF * BUF * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int mtiles = (M + BM - 1) / BM;
+  const int ntiles = SWIGLU ? (N / 2) / 64 : N / WBN;
+  const int total = gridDim.x;
+  // bijective XCD remap: blocks b with b % 8 == x run on XCD x; give XCD x a contiguous run
+  int b = blockIdx.x;
+  {
+    const int q = total >> 3, r = total & 7, x = b & 7;
+    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  }
+  const int m_t = b % mtiles, rest = b / mtiles;
+  const int split = rest % nsplit, n_t = rest / nsplit;
+  (void)ntiles;
+  const int m0 = m_t * BM;
+  const int kt0 = split * kt_per_split;
+  const int nt = max(0, min(K / WBK, kt0 + kt_per_split) - kt0);
+
+  // per-lane staging sources: instruction i covers tile rows 8i .. 8i+7, lane -> (row, chunk)
+  const bf16* srcA[AI];
+  const bf16* srcB[BI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int i = wv * AI + j;
+    const int r = 8 * i + (lane >> 3);
+    srcA[j] = A + (size_t)min(m0 + r, M - 1) * K + (size_t)kt0 * WBK + wswz(r, lane & 7) * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int i = wv * BI + j;
+    const int r = 8 * i + (lane >> 3);
+    srcB[j] = B + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + (size_t)kt0 * WBK + wswz(r, lane & 7) * 8;
+  }
+  f32x4 acc[RT][4];
+  wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, nt, acc, wv, lane);
   wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Grouped (MoE) wide GEMM: grid (column tiles, experts).  Expert e owns rows [offsets[e],
+// offsets[e] + counts[e]) of the expert-sorted slot space; its A rows are gathered through
+// `gather` (slot -> token row of X; null = slot rows of X), its weight is W[e] ([N, K], SwiGLU:
+// [2I, K] with the alternating gate/up row groups of the dense kernel).  The row tile is picked
+// per expert from its count (workgroup-uniform): 64 rows up to 64, else 128-row chunks.  This is
+// the decode regime of Mixtral at B >= 128 (32-128 rows per expert), where the weight-streaming
+// grouped kernel (moe.hip) runs its MFMAs at a fraction of the rate.
+// ---------------------------------------------------------------------------------------------
+template <int BM, bool SWIGLU>
+__device__ __forceinline__ void moe_wide_rows(bf16* smem, bf16* __restrict__ Y, const bf16* __restrict__ X,
+                                              const int* __restrict__ gather, const bf16* __restrict__ We, int cnt,
+                                              int off, int N, int K, int n_t, int wv, int lane) {
+  constexpr int AI = BM / 64, BI = 2, RT = BM / 64;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int ldy = SWIGLU ? N / 2 : N;
+  for (int r0 = 0; r0 < cnt; r0 += BM) {
+    const int rows = min(BM, cnt - r0);
+    const bf16* srcA[AI];
+    const bf16* srcB[BI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int r = 8 * (wv * AI + j) + (lane >> 3);
+      const int slot = off + r0 + min(r, rows - 1);
+      const int src = gather ? gather[slot] : slot;
+      srcA[j] = X + (size_t)src * K + wswz(r, lane & 7) * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int r = 8 * (wv * BI + j) + (lane >> 3);
+      srcB[j] = We + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + wswz(r, lane & 7) * 8;
+    }
+    f32x4 acc[RT][4];
+    wide_mainloop<BM, 3, 1>(smem, srcA, srcB, K / WBK, acc, wv, lane);
+    wide_epilogue<BM, false, SWIGLU>(acc, Y + (size_t)(off + r0) * ldy, nullptr, rows, N, 0, n_t, 0, wm, wn, lane);
+    __syncthreads();   // the next chunk's prologue refills buffers other waves may still read
+  }
+}
+
+template <bool SWIGLU>
+__global__ void __launch_bounds__(512, 1) moe_wide_kernel(bf16* __restrict__ Y, const bf16* __restrict__ X,
+                                                          const int* __restrict__ gather, const bf16* __restrict__ W,
+                                                          const int* __restrict__ counts,
+                                                          const int* __restrict__ offsets, int N, int K) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[3 * (128 + WBN) * WBK];
+  const int e = blockIdx.y;
+  const int cnt = counts[e];
+  if (cnt == 0) return;                       // uniform across the workgroup
+  const int off = offsets[e];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bf16* We = W + (size_t)e * N * K;
+  if (cnt <= 64) moe_wide_rows<64, SWIGLU>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+  else moe_wide_rows<128, SWIGLU>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+}
+
+// mode 1 (SwiGLU): W [E, 2I, K] -> Y [slots, I]; mode 0: W [E, N, K] -> Y [slots, N]
+void moe_wide_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets,
+                   int E, int N, int K, int mode, uintptr_t stream) {
+  DLLM_HOST_CHECK(E >= 1, "experts >= 1");
+  DLLM_HOST_CHECK(K % WBK == 0, "K must be a multiple of 64");
+  DLLM_HOST_CHECK(N % 128 == 0, "N must be a multiple of 128");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int ntiles = mode == 1 ? (N / 2) / 64 : N / WBN;
+  if (mode == 1)
+    hipLaunchKernelGGL(moe_wide_kernel<true>, dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
+                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K);
+  else
+    hipLaunchKernelGGL(moe_wide_kernel<false>, dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
+                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K);
+  DLLM_HIP_CHECK(hipGetLastError());
 }
 
 // mode 0: C = A B^T;  mode 1: SwiGLU, C[M, N/2] = silu(A Bg^T) * (A Bu^T) with B = [Bg; Bu];

@@ -22,6 +22,9 @@ from . import reference as ref
 GROUPED_MAX_TOKENS = 256      # beyond this the per-expert row count makes library GEMMs cheaper
 # 0 = pick by expected rows per expert; 1..6 force a kernel variant (bench/moe_bench.py sweeps them)
 GROUPED_VARIANT = int(os.environ.get("DLLM_MOE_VARIANT", "0"))
+# expected rows per expert from which the MFMA-tiled grouped kernel (gemm_wide.hip moe_wide_gemm)
+# replaces the weight-streaming one (moe.hip); 0 disables it
+WIDE_MIN_ROWS = int(os.environ.get("DLLM_MOE_WIDE_MIN_ROWS", "32"))
 
 
 def route(router_logits: torch.Tensor, top_k: int):
@@ -59,10 +62,17 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     if t <= GROUPED_MAX_TOKENS:
         act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
         rows = -(-t * top_k // e)        # expected rows per expert picks the kernel's row tile
-        k.moe_grouped_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
-                           counts.data_ptr(), offsets.data_ptr(), e, two_i, h, 1, rows, GROUPED_VARIANT, st)
-        k.moe_grouped_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), counts.data_ptr(),
-                           offsets.data_ptr(), e, h, inter, 0, rows, GROUPED_VARIANT, st)
+        if 0 < WIDE_MIN_ROWS <= rows and x.dtype == torch.bfloat16 and two_i % 128 == 0 and h % 128 == 0 \
+                and h % 64 == 0 and inter % 64 == 0:
+            k.moe_wide_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
+                            counts.data_ptr(), offsets.data_ptr(), e, two_i, h, 1, st)
+            k.moe_wide_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), counts.data_ptr(),
+                            offsets.data_ptr(), e, h, inter, 0, st)
+        else:
+            k.moe_grouped_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
+                               counts.data_ptr(), offsets.data_ptr(), e, two_i, h, 1, rows, GROUPED_VARIANT, st)
+            k.moe_grouped_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), counts.data_ptr(),
+                               offsets.data_ptr(), e, h, inter, 0, rows, GROUPED_VARIANT, st)
     else:
         xs = x.index_select(0, sorted_tok.long())
         off = offsets.cpu().tolist()          # prefill only: eager, host sync is fine here

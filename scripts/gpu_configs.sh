@@ -8,3 +8,5 @@ run 8b_b64 --batch 64
 run mixtral_b64 --model mixtral-8x7b --batch 64 --steps 2
 run mixtral_b256 --model mixtral-8x7b --batch 256 --steps 2
 run 70b_b64 --model llama3-70b --batch 64 --steps 2
+run 70b_b256 --model llama3-70b --batch 256 --steps 2
+run 8b_b128 --batch 128

@@ -65,3 +65,25 @@ def test_moe_graph_capturable(cuda):
         tw, tid = ref.moe_route(ref.linear(x, wr).float(), k)
         torch.testing.assert_close(out.float(), ref.moe_mlp(x.float(), wgu.float(), wd.float(), tw, tid),
                                    atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("t", [1, 7, 40, 64, 150, 256])
+@pytest.mark.parametrize("skew", [False, True])
+def test_moe_wide_grouped_kernel(cuda, monkeypatch, t, skew):
+    """The MFMA-tiled grouped expert GEMM (gemm_wide.hip moe_wide_gemm) forced for every token
+    count: 64-row tiles, 128-row chunks, multi-chunk experts (skewed routing) and empty experts."""
+    monkeypatch.setattr(moe, "WIDE_MIN_ROWS", 1)
+    e, k, h, i = 8, 2, 512, 384
+    x = _bf(t, h)
+    if skew:
+        x = x.abs()
+        wr = torch.zeros(e, h, device="cuda", dtype=torch.bfloat16)
+        wr[2] = 0.05
+        wr[6] = 0.04
+    else:
+        wr = _bf(e, h, scale=0.1)
+    wgu, wd = _bf(e, 2 * i, h, scale=0.05), _bf(e, h, i, scale=0.05)
+    out = moe.forward(x, wr, wgu, wd, k)
+    tw, tid = ref.moe_route(ref.linear(x, wr).float(), k)
+    expect = ref.moe_mlp(x.float(), wgu.float(), wd.float(), tw, tid)
+    torch.testing.assert_close(out.float(), expect, atol=3e-2, rtol=3e-2)
