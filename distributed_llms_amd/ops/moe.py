@@ -22,9 +22,11 @@ from . import reference as ref
 GROUPED_MAX_TOKENS = 256      # beyond this the per-expert row count makes library GEMMs cheaper
 # 0 = pick by expected rows per expert; 1..6 force a kernel variant (bench/moe_bench.py sweeps them)
 GROUPED_VARIANT = int(os.environ.get("DLLM_MOE_VARIANT", "0"))
-# expected rows per expert from which the MFMA-tiled grouped kernel (gemm_wide.hip moe_wide_gemm)
-# replaces the weight-streaming one (moe.hip); 0 disables it
-WIDE_MIN_ROWS = int(os.environ.get("DLLM_MOE_WIDE_MIN_ROWS", "32"))
+# token-expert pairs (T x top_k) from which the MFMA-tiled grouped kernel (gemm_wide.hip
+# moe_wide_gemm) replaces the weight-streaming one (moe.hip); 0 disables it.  Mixtral-8x7B
+# end to end (scripts/gpu_moe_wide.sh, profiles/moe_wide.md): B=1 0.95x, B=4 1.10x, B=16 1.10x,
+# B=64 1.25x, B=128 1.52x, B=256 2.23x
+WIDE_MIN_PAIRS = int(os.environ.get("DLLM_MOE_WIDE_MIN_PAIRS", "8"))
 
 
 def route(router_logits: torch.Tensor, top_k: int):
@@ -62,7 +64,7 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     if t <= GROUPED_MAX_TOKENS:
         act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
         rows = -(-t * top_k // e)        # expected rows per expert picks the kernel's row tile
-        if 0 < WIDE_MIN_ROWS <= rows and x.dtype == torch.bfloat16 and two_i % 128 == 0 and h % 128 == 0 \
+        if 0 < WIDE_MIN_PAIRS <= t * top_k and x.dtype == torch.bfloat16 and two_i % 128 == 0 and h % 128 == 0 \
                 and h % 64 == 0 and inter % 64 == 0:
             k.moe_wide_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
                             counts.data_ptr(), offsets.data_ptr(), e, two_i, h, 1, st)
