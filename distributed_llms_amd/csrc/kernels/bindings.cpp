@@ -27,6 +27,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("gemm_wide", &dllm::gemm_wide);
   m.def("moe_combine", &dllm::moe_combine);
   m.def("moe_wide_gemm", &dllm::moe_wide_gemm);
+  m.def("moe_router_route", &dllm::moe_router_route);
   m.def("paged_attention_decode", &dllm::paged_attention_decode);
   m.def("paged_attention_decode_rope", &dllm::paged_attention_decode_rope);
   m.def("paged_attention_prefill", &dllm::paged_attention_prefill);

@@ -27,6 +27,8 @@ GROUPED_VARIANT = int(os.environ.get("DLLM_MOE_VARIANT", "0"))
 # end to end (scripts/gpu_moe_wide.sh, profiles/moe_wide.md): B=1 0.95x, B=4 1.10x, B=16 1.10x,
 # B=64 1.25x, B=128 1.52x, B=256 2.23x
 WIDE_MIN_PAIRS = int(os.environ.get("DLLM_MOE_WIDE_MIN_PAIRS", "8"))
+# decode router: fused GEMV + top-k + scatter kernels instead of library GEMM + route kernel
+FUSED_ROUTER = os.environ.get("DLLM_MOE_FUSED_ROUTER", "1") != "0"
 
 
 def route(router_logits: torch.Tensor, top_k: int):
@@ -50,7 +52,6 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     inter = two_i // 2
     if not (x.is_contiguous() and w_gate_up.is_contiguous() and w_down.is_contiguous()):
         raise ValueError("moe: operands must be contiguous")
-    logits = linear(x, w_router)
     dev = x.device
     topk_w = torch.empty(t, top_k, dtype=torch.float32, device=dev)
     topk_ids = torch.empty(t, top_k, dtype=torch.int32, device=dev)
@@ -58,8 +59,15 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     offsets = torch.empty(e + 1, dtype=torch.int32, device=dev)
     sorted_tok = torch.empty(t * top_k, dtype=torch.int32, device=dev)
     inv = torch.empty(t * top_k, dtype=torch.int32, device=dev)
-    k.moe_route(logits.data_ptr(), t, e, top_k, topk_w.data_ptr(), topk_ids.data_ptr(), counts.data_ptr(),
-                offsets.data_ptr(), sorted_tok.data_ptr(), inv.data_ptr(), st)
+    if FUSED_ROUTER and t <= GROUPED_MAX_TOKENS and e in (8, 16) and x.dtype == w_router.dtype == torch.bfloat16 \
+            and w_router.is_contiguous():
+        # decode: router GEMV + softmax/top-k + scatter in two launches (no [T, E] logits round trip)
+        k.moe_router_route(x.data_ptr(), w_router.data_ptr(), t, h, e, top_k, topk_w.data_ptr(), topk_ids.data_ptr(),
+                           counts.data_ptr(), offsets.data_ptr(), sorted_tok.data_ptr(), inv.data_ptr(), st)
+    else:
+        logits = linear(x, w_router)
+        k.moe_route(logits.data_ptr(), t, e, top_k, topk_w.data_ptr(), topk_ids.data_ptr(), counts.data_ptr(),
+                    offsets.data_ptr(), sorted_tok.data_ptr(), inv.data_ptr(), st)
     ys = torch.empty(t * top_k, h, dtype=x.dtype, device=dev)
     if t <= GROUPED_MAX_TOKENS:
         act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
