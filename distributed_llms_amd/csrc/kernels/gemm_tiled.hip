@@ -18,6 +18,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace dllm {
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
@@ -160,10 +162,13 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16* __restrict__ o
 // Bit-identical to splitk_reduce_kernel followed by rms_norm_kernel with a residual (same
 // per-element summation order, same thread -> vector mapping for the sum of squares), minus one
 // launch and the bf16 h round trip through HBM.  One 256-thread workgroup per row.
-template <int MAXV>
+template <int MAXV, int SC>
 __global__ void __launch_bounds__(256) splitk_add_rms_norm_kernel(bf16* __restrict__ y, bf16* __restrict__ residual,
-                                                                  const float* __restrict__ P, int S, int M, int N,
+                                                                  const float* __restrict__ P, int S_, int M, int N,
                                                                   const bf16* __restrict__ w, float eps) {
+  // SC > 0: the slab count is a compile-time constant, so all of a vector's 2*SC slab loads are
+  // issued before the first add (the runtime-S loop waited on each slab in turn)
+  const int S = SC > 0 ? SC : S_;
   __shared__ float red[16];
   const int row = blockIdx.x;
   const int nvec = N >> 3;
@@ -177,9 +182,23 @@ __global__ void __launch_bounds__(256) splitk_add_rms_norm_kernel(bf16* __restri
     if (idx < nvec) {
       const float* p = P + (size_t)row * N + idx * 8;
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < S; ++s) {
-        a0 += *reinterpret_cast<const f32x4*>(p + s * slab);
-        a1 += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
+      if constexpr (SC > 0) {
+        f32x4 l0[SC], l1[SC];
+#pragma unroll
+        for (int s = 0; s < SC; ++s) {
+          l0[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + s * slab));
+          l1[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + s * slab + 4));
+        }
+#pragma unroll
+        for (int s = 0; s < SC; ++s) {   // same slab order as the runtime loop: bit-identical sums
+          a0 += l0[s];
+          a1 += l1[s];
+        }
+      } else {
+        for (int s = 0; s < S; ++s) {
+          a0 += *reinterpret_cast<const f32x4*>(p + s * slab);
+          a1 += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
+        }
       }
       const bf16x8 b = rr[idx];
       bf16x8 r;
@@ -224,10 +243,22 @@ void splitk_add_rms_norm(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, i
                        (const bf16*)w, eps);
   };
   const int nvec = N / 8;
-  if (nvec <= 256) go(splitk_add_rms_norm_kernel<1>);
-  else if (nvec <= 512) go(splitk_add_rms_norm_kernel<2>);
-  else if (nvec <= 1024) go(splitk_add_rms_norm_kernel<4>);
-  else go(splitk_add_rms_norm_kernel<8>);
+  static const bool const_slabs = [] {
+    const char* e = getenv("DLLM_SKN_CONST");
+    return !(e && e[0] == '0');
+  }();
+#define DLLM_SKN(MV)                                                   \
+  do {                                                                 \
+    if (!const_slabs) go(splitk_add_rms_norm_kernel<MV, 0>);           \
+    else if (S == 8) go(splitk_add_rms_norm_kernel<MV, 8>);                 \
+    else if (S == 4) go(splitk_add_rms_norm_kernel<MV, 4>);            \
+    else go(splitk_add_rms_norm_kernel<MV, 0>);                        \
+  } while (0)
+  if (nvec <= 256) DLLM_SKN(1);
+  else if (nvec <= 512) DLLM_SKN(2);
+  else if (nvec <= 1024) DLLM_SKN(4);
+  else DLLM_SKN(8);
+#undef DLLM_SKN
   DLLM_HIP_CHECK(hipGetLastError());
 }
 
