@@ -27,11 +27,12 @@ struct WaveState {
 };
 
 // One 32-key chunk's operands, loaded into registers: K rows as two 16-key A tiles, V^T as
-// the A fragments of the P.V MFMA (two 8-byte halves per lane, k-order permuted to match P).
+// the A fragments of the P.V MFMA (keys 4g..4g+3 and 16+4g..16+4g+3 of lane group g: k-order
+// permuted to match P; one 16-byte load thanks to the vperm32 column order of the cache).
 template <int D>
 struct KVChunk {
   bf16x8 ka[D / 32], kb[D / 32];
-  bf16x4 vlo[D / 16], vhi[D / 16];
+  bf16x8 v[D / 16];
 };
 
 template <int D>
@@ -44,11 +45,8 @@ __device__ __forceinline__ void load_chunk(KVChunk<D>& c, const bf16* __restrict
     c.kb[ks] = *reinterpret_cast<const bf16x8*>(kblk + (16 + r) * D + ks * 32 + 8 * g);
   }
 #pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt) {
-    const bf16* vr = vblk + (dt * 16 + r) * kBS;
-    c.vlo[dt] = *reinterpret_cast<const bf16x4*>(vr + 4 * g);
-    c.vhi[dt] = *reinterpret_cast<const bf16x4*>(vr + 16 + 4 * g);
-  }
+  for (int dt = 0; dt < D / 16; ++dt)
+    c.v[dt] = *reinterpret_cast<const bf16x8*>(vblk + (dt * 16 + r) * kBS + 8 * g);
 }
 
 // Online-softmax update of the wave's 16 columns with one loaded chunk.
@@ -93,10 +91,7 @@ __device__ __forceinline__ void compute_chunk(WaveState<D>& st, const bf16x8 (&q
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt) {
     st.acc[dt] *= alpha;
-    const bf16x4 lo = c.vlo[dt], hi = c.vhi[dt];
-    bf16x8 va;
-    va[0] = lo[0]; va[1] = lo[1]; va[2] = lo[2]; va[3] = lo[3];
-    va[4] = hi[0]; va[5] = hi[1]; va[6] = hi[2]; va[7] = hi[3];
+    const bf16x8 va = c.v[dt];
     st.acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, st.acc[dt], 0, 0, 0);
   }
 }
@@ -259,7 +254,7 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
       }
       if (g == 0) {
 #pragma unroll
-        for (int dt = 0; dt < D / 16; ++dt) v_cache[base + (size_t)(dt * 16 + r) * kBS + off] = vn[dt];
+        for (int dt = 0; dt < D / 16; ++dt) v_cache[base + (size_t)(dt * 16 + r) * kBS + vperm32(off)] = vn[dt];
       }
     }
   };
@@ -304,10 +299,9 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     }
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
-      bf16x4 lo = {};
-      if (g == 0) lo[0] = vn[dt];
-      nc.vlo[dt] = lo;
-      nc.vhi[dt] = bf16x4{};
+      bf16x8 v = {};
+      if (g == 0) v[0] = vn[dt];          // key 0 of the one-key chunk
+      nc.v[dt] = v;
     }
     compute_chunk<D>(st, qf, nc, ctx - 1, ctx - 1, scale_log2, lane);
   }

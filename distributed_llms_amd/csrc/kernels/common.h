@@ -58,3 +58,12 @@ __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x))
 // f32 -> bf16 via the compiler cast: gfx950 emits v_cvt_pk_bf16_f32 (RNE, NaN-preserving).
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+
+// Paged V^T cache, 32-key blocks: key j of a block row is stored at column vperm32(j), order
+// 0-3,16-19,4-7,20-23,...  The P.V MFMA's A fragment of lane group g is keys 4g..4g+3 and
+// 16+4g..16+4g+3, which this places in 16 contiguous bytes: one 16-B load per fragment
+// instead of two 8-B loads.  Other block sizes are stored unpermuted.
+__host__ __device__ __forceinline__ int vperm32(int j) {
+  return j < 16 ? ((j >> 2) << 3) + (j & 3) : (((j - 16) >> 2) << 3) + 4 + (j & 3);
+}
+__host__ __device__ __forceinline__ int vcol(int off, int bs) { return bs == 32 ? vperm32(off) : off; }

@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ q_ou
   const bf16* vsrc = row + (hq + hkv) * d;
   for (int i = threadIdx.x; i < hkv * d; i += blockDim.x) {
     const int h = i / d, e = i % d;
-    v_cache[(((size_t)blk * hkv + h) * d + e) * bs + off] = vsrc[i];
+    v_cache[(((size_t)blk * hkv + h) * d + e) * bs + vcol(off, bs)] = vsrc[i];
   }
 }
 

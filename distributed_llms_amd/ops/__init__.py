@@ -13,6 +13,8 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import os
+
 import torch
 
 from .. import _ext
@@ -173,7 +175,7 @@ def rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, n
 
 
 # ---------------------------------------------------------- K6 / K7
-DECODE_TARGET_WAVES = 1024     # waves the decode split plan aims for (sweep: profiles/attn_decode_sweep.txt)
+DECODE_TARGET_WAVES = int(os.environ.get("DLLM_ATTN_TARGET_WAVES", "1024"))  # sweep: profiles/attn_decode_sweep.txt
 
 
 def decode_split_plan(batch: int, num_kv_heads: int, max_ctx: int, block_size: int = 32,

@@ -10,7 +10,8 @@ transformer-block math.
 
 Paged-KV layout (shared with the HIP kernels, one tensor pair per layer):
   k_cache: [num_blocks, num_kv_heads, block_size, head_dim]
-  v_cache: [num_blocks, num_kv_heads, head_dim, block_size]   (V stored transposed
+  v_cache: [num_blocks, num_kv_heads, head_dim, block_size]   (key j at column vperm32(j) for 32-key blocks;
+                                                              V stored transposed
            so the P·V MFMA reads token-contiguous 16-byte fragments)
 ``slot = block_id * block_size + offset`` addresses one token's K/V.
 """
@@ -118,8 +119,21 @@ def rope_cache_append(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optio
     slots = slot_mapping.long()
     blk, off = slots // bs, slots % bs
     k_cache[blk, :, off, :] = k.to(k_cache.dtype)
-    v_cache[blk, :, :, off] = v.to(v_cache.dtype)
+    v_cache[blk, :, :, _vcol(off, bs)] = v.to(v_cache.dtype)
     return q
+
+
+def _vperm32() -> torch.Tensor:
+    """Column of key j in a 32-key V^T block (csrc/kernels/common.h vperm32)."""
+    j = torch.arange(32)
+    return torch.where(j < 16, (j // 4) * 8 + j % 4, ((j - 16) // 4) * 8 + 4 + j % 4)
+
+
+_VPERM32 = _vperm32()
+
+
+def _vcol(off: torch.Tensor, bs: int) -> torch.Tensor:
+    return _VPERM32.to(off.device)[off] if bs == 32 else off
 
 
 def _gather_kv(k_cache, v_cache, block_table, n):
@@ -127,7 +141,10 @@ def _gather_kv(k_cache, v_cache, block_table, n):
     nb = (n + bs - 1) // bs
     blocks = block_table[:nb].long()
     k = k_cache[blocks].permute(1, 0, 2, 3).reshape(k_cache.shape[1], nb * bs, -1)[:, :n]
-    v = v_cache[blocks].permute(1, 0, 3, 2).reshape(v_cache.shape[1], nb * bs, -1)[:, :n]
+    vb = v_cache[blocks]
+    if bs == 32:
+        vb = vb[..., _VPERM32.to(vb.device)]             # physical columns back to key order
+    v = vb.permute(1, 0, 3, 2).reshape(v_cache.shape[1], nb * bs, -1)[:, :n]
     return k, v  # [Hkv, n, D]
 
 
