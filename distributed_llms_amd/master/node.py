@@ -267,8 +267,32 @@ class MasterNode:
         self.shard_manager = ModelShardManager(self.model_path, num_shards, self.model_config)
         return self.shard_manager.shard_model()
 
+    def stage_weight_bytes(self) -> List[int]:
+        """bf16/fp16 weight bytes each pipeline stage will hold (layers + embedding / LM head)."""
+        from ..parallel.planner import plan_units
+        cfg = self.model_config
+        n = self.num_shards
+        if self.shard_manager is not None:
+            return [os.path.getsize(p) for p in self.shard_manager.get_shard_paths()]
+        up = plan_units(cfg, n, batch=self.config.max_batch, ctx=max(32, self.config.max_seq_len // 2))
+        width = 4 if self.config.dtype == "float32" else 2
+        per_layer = cfg.layer_param_count() * width
+        out = []
+        for i, (a, b) in enumerate(up.ranges):
+            nbytes = (b - a) * per_layer
+            if i == 0 or i == n - 1:
+                nbytes += cfg.head_param_count() * width // (1 if n == 1 else 2)
+            out.append(int(nbytes))
+        return out
+
     def assign_shards(self) -> Dict[str, List[int]]:
-        """Shard i -> stage i -> i-th registered worker (contiguous pipeline order)."""
+        """Stage i -> a registered worker, capacity-aware (SURVEY §2.8 "capacity-aware assignment").
+
+        Candidates are the workers whose device memory can hold the stage's weights plus KV
+        headroom (``memory`` from REGISTER; CPU workers report 0 and only serve CPU configs).  With
+        more workers than stages the largest devices are used; stages keep registration order
+        among equals so pipeline neighbours stay predictable.  The reference assigned round-robin
+        and ignored capabilities (``src/master/node.py:84-104``)."""
         with self._lock:
             if not self.workers:
                 raise ValueError("No workers connected")
@@ -277,7 +301,25 @@ class MasterNode:
             workers = sorted(self.workers, key=lambda k: int(k[1:]))
             if len(workers) < self.num_shards:
                 raise ValueError(f"{self.num_shards} shards need {self.num_shards} workers, have {len(workers)}")
-            self.stage_workers = workers[: self.num_shards]
+            mem = {w: int(self.workers[w].get("capabilities", {}).get("memory", 0) or 0) for w in workers}
+            if any(mem.values()):
+                need = self.stage_weight_bytes()
+                # the largest devices first, registration order among equals
+                pool = sorted(workers, key=lambda w: (-mem[w], int(w[1:])))[: self.num_shards]
+                pool.sort(key=lambda w: int(w[1:]))
+                order = sorted(range(self.num_shards), key=lambda i: -need[i])
+                by_mem = sorted(pool, key=lambda w: (-mem[w], int(w[1:])))
+                chosen = [None] * self.num_shards
+                for i, w in zip(order, by_mem):       # heaviest stage -> largest device
+                    if mem[w] and need[i] * 1.1 > mem[w]:
+                        raise ValueError(f"stage {i} needs {need[i] / 2**30:.1f} GiB of weights; worker {w} "
+                                         f"has {mem[w] / 2**30:.1f} GiB")
+                    chosen[i] = w
+                if sorted(mem[w] for w in pool) == [mem[pool[0]]] * len(pool):
+                    chosen = pool                     # homogeneous node: keep registration order
+                self.stage_workers = chosen
+            else:
+                self.stage_workers = workers[: self.num_shards]
             self.shard_assignments = {wid: [i] for i, wid in enumerate(self.stage_workers)}
             return dict(self.shard_assignments)
 

@@ -170,3 +170,31 @@ def test_metrics_percentiles_and_prometheus():
     seq = _seq(2)
     seq.token_times = [1.0, 1.25, 1.75]
     assert itl_stats([seq])["itl_p50_s"] == pytest.approx(0.375)
+
+
+# ------------------------------------------------------------------ master placement
+def _master_with(workers_mem, model="synthetic:llama3-70b", shards=2):
+    from distributed_llms_amd.master.node import MasterNode
+    m = MasterNode(config=EngineConfig(model=model))
+    m.initialize_model(model, shards)
+    for i, mem in enumerate(workers_mem):
+        m.workers[f"w{i}"] = {"capabilities": {"memory": mem}}
+    return m
+
+
+def test_assign_shards_capacity_aware():
+    gib = 2 ** 30
+    # homogeneous node: registration order
+    m = _master_with([288 * gib] * 3, shards=2)
+    assert m.assign_shards() == {"w0": [0], "w1": [1]}
+    assert sum(m.stage_weight_bytes()) > 125 * gib            # 70B bf16 is ~139-141 GB over the stages
+    # heterogeneous: the small device is skipped when a larger one is free
+    m = _master_with([288 * gib, 24 * gib, 288 * gib], shards=2)
+    assert set(m.assign_shards()) == {"w0", "w2"}
+    # nothing can hold a 70 GB stage
+    m = _master_with([48 * gib, 48 * gib], shards=2)
+    with pytest.raises(ValueError, match="needs"):
+        m.assign_shards()
+    # CPU workers (memory 0): plain registration order, no capacity check
+    m = _master_with([0, 0], model="synthetic:gpt2-small", shards=2)
+    assert m.assign_shards() == {"w0": [0], "w1": [1]}
