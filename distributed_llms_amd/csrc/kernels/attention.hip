@@ -142,9 +142,12 @@ struct RopeArgs {
   long slab = 0;
 };
 
-// 8 consecutive qkv elements starting at row offset `off` of sequence b (bf16 or summed partials)
+// 8 consecutive qkv elements starting at row offset `off` of sequence b (bf16 or summed partials).
+// PARTS is a compile-time choice: a runtime branch here split the kernel's prologue into blocks
+// with vmcnt(0) waits at every merge (cold B=256: 48 us vs 40 us without the fused part).
+template <bool PARTS>
 __device__ __forceinline__ bf16x8 qkv_load8(const RopeArgs& ra, int b, int width, int off) {
-  if (ra.part == nullptr) return *reinterpret_cast<const bf16x8*>(ra.qkv + (size_t)b * width + off);
+  if constexpr (!PARTS) return *reinterpret_cast<const bf16x8*>(ra.qkv + (size_t)b * width + off);
   const float* p = ra.part + (size_t)b * width + off;
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
   for (int s = 0; s < ra.nparts; ++s) {
@@ -160,8 +163,9 @@ __device__ __forceinline__ bf16x8 qkv_load8(const RopeArgs& ra, int b, int width
   return o;
 }
 
+template <bool PARTS>
 __device__ __forceinline__ bf16 qkv_load1(const RopeArgs& ra, int b, int width, int off) {
-  if (ra.part == nullptr) return ra.qkv[(size_t)b * width + off];
+  if constexpr (!PARTS) return ra.qkv[(size_t)b * width + off];
   const float* p = ra.part + (size_t)b * width + off;
   float a = 0.f;
   for (int s = 0; s < ra.nparts; ++s) a += p[s * ra.slab];
@@ -187,7 +191,7 @@ __device__ __forceinline__ void rope_rotate(bf16x8 (&f)[D / 32], const float* cs
   }
 }
 
-template <int D, int WPB, bool FUSED>
+template <int D, int WPB, bool FUSED, bool PARTS = false>
 __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg: min waves per SIMD
     bf16* __restrict__ out, const bf16* __restrict__ q, bf16* __restrict__ k_cache,
     bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
@@ -201,11 +205,17 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
   const int r = lane & 15, g = lane >> 4;
   const int ctx = seq_lens[b];
   const int kbeg = split * split_len;
-  // FUSED: the new key (ctx - 1) is not read from the cache; the split that owns it adds it last
+  // FUSED: the new key (ctx - 1) is not in the cache yet: its chunk is loaded as usual and the
+  // key's K row / V^T column are replaced in registers by the rotated k and v (the split that
+  // owns it also appends them to the cache, after its last KV load)
   const bool owns_new = FUSED && ctx > 0 && (ctx - 1) / split_len == split;
-  const int kend = min(kbeg + split_len, FUSED ? ctx - 1 : ctx);  // exclusive (cache keys)
+  const int kend = min(kbeg + split_len, ctx);     // exclusive
   const int c0 = kbeg / kBS, c1 = kend > kbeg ? (kend + kBS - 1) / kBS : c0;
 
+  // the first pass's block ids go out before the q/k/v loads: the first KV chunk's address
+  // then waits on this one load only (vmcnt retires in issue order), not on the qkv row too
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  const int blk_first = lane < min(64, c1 - c0) ? bt[c0 + lane] : 0;
   // Q^T fragments: column r = head kvh*G + r (zero beyond G)
   bf16x8 qf[D / 32];
   const bool col_ok = r < G;
@@ -216,11 +226,11 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     const int qo = (kvh * G + (col_ok ? r : 0)) * D, ko = (hq + kvh) * D, vo = (hq + hkv + kvh) * D;
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
-      qf[ks] = qkv_load8(ra, b, width, qo + ks * 32 + 8 * g);
-      kn[ks] = qkv_load8(ra, b, width, ko + ks * 32 + 8 * g);
+      qf[ks] = qkv_load8<PARTS>(ra, b, width, qo + ks * 32 + 8 * g);
+      kn[ks] = qkv_load8<PARTS>(ra, b, width, ko + ks * 32 + 8 * g);
     }
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) vn[dt] = qkv_load1(ra, b, width, vo + dt * 16 + r);
+    for (int dt = 0; dt < D / 16; ++dt) vn[dt] = qkv_load1<PARTS>(ra, b, width, vo + dt * 16 + r);
   } else {
     const bf16* qrow = q + ((size_t)b * hq + kvh * G + (col_ok ? r : 0)) * D;
 #pragma unroll
@@ -243,31 +253,38 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
 #pragma unroll
       for (int ks = 0; ks < D / 32; ++ks) qf[ks] = bf16x8{};
     }
-    if (owns_new) {   // append k (row layout) and v^T (column `off`) to the paged cache
-      const int slot = ra.slots[b];
-      const int blk = slot / kBS, off = slot % kBS;
-      const size_t base = ((size_t)blk * hkv + kvh) * kBS * D;
-      if (r == 0) {
+  };
+  // FUSED: put the new key into the registers of its chunk (branch-free: lane masks only)
+  const int cnew = FUSED ? (ctx - 1) / kBS : -1;
+  const int noff = FUSED ? (ctx - 1) % kBS : 0;
+  auto patch = [&](KVChunk<D>& c, int chunk) {
+    if (!FUSED) return;
+    const bool here = ctx > 0 && chunk == cnew;
+    // (two static selects: a runtime choice between ka and kb made hipcc index them through scratch)
+    const bool krow = here && r == (noff & 15);
+    const bool ka_row = krow && noff < 16, kb_row = krow && noff >= 16;
 #pragma unroll
-        for (int ks = 0; ks < D / 32; ++ks)
-          *reinterpret_cast<bf16x8*>(k_cache + base + (size_t)off * D + ks * 32 + 8 * g) = kn[ks];
-      }
-      if (g == 0) {
-#pragma unroll
-        for (int dt = 0; dt < D / 16; ++dt) v_cache[base + (size_t)(dt * 16 + r) * kBS + vperm32(off)] = vn[dt];
-      }
+    for (int ks = 0; ks < D / 32; ++ks) {
+      c.ka[ks] = ka_row ? kn[ks] : c.ka[ks];
+      c.kb[ks] = kb_row ? kn[ks] : c.kb[ks];
     }
+    // V^T fragment of lane group g: keys 4g..4g+3 -> elements 0..3, 16+4g..16+4g+3 -> 4..7
+    const int e = (noff & 3) + (noff >= 16 ? 4 : 0);
+    const bool vcol = here && g == ((noff & 15) >> 2);
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) c.v[dt][i] = (vcol && i == e) ? vn[dt] : c.v[dt][i];
   };
   WaveState<D> st;
   init_state(st);
   const int kmax = kend - 1;
   const size_t kv_head_stride = (size_t)kBS * D;
-  const int32_t* bt = block_tables + (size_t)b * max_blocks;
   const size_t head_off = (size_t)kvh * kv_head_stride;
   const size_t blk_stride = (size_t)hkv * kv_head_stride;
   for (int cb = c0; cb < c1; cb += 64) {            // 64 chunks (2048 keys) of block ids per pass
     const int n = min(64, c1 - cb);
-    const int my_blk = lane < n ? bt[cb + lane] : 0;
+    const int my_blk = cb == c0 ? blk_first : (lane < n ? bt[cb + lane] : 0);
     KVChunk<D> cur, nxt;
     {
       const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, 0) * blk_stride + head_off;
@@ -280,30 +297,38 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
         const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, j + 1) * blk_stride + head_off;
         load_chunk<D>(nxt, k_cache + base, v_cache + base, lane);
       }
+      patch(cur, cb + j);
       compute_chunk<D>(st, qf, cur, (cb + j) * kBS, kmax, scale_log2, lane);
       if (j + 2 < n) {
         const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, j + 2) * blk_stride + head_off;
         load_chunk<D>(cur, k_cache + base, v_cache + base, lane);
       }
+      patch(nxt, cb + j + 1);
       compute_chunk<D>(st, qf, nxt, (cb + j + 1) * kBS, kmax, scale_log2, lane);
     }
-    if (j < n) compute_chunk<D>(st, qf, cur, (cb + j) * kBS, kmax, scale_log2, lane);
+    if (j < n) {
+      patch(cur, cb + j);
+      compute_chunk<D>(st, qf, cur, (cb + j) * kBS, kmax, scale_log2, lane);
+    }
   }
   finish_rope();   // no cache chunk in this split
-  if (owns_new) {   // the new key as a one-key chunk: K row 0 = k, V^T column 0 = v, rest masked
-    KVChunk<D> nc;
+  if (owns_new) {
+    // append k (row layout) and v^T (column vperm32(off)) to the paged cache only now, after the
+    // last KV load: stores count in vmcnt in issue order, so stores issued before the KV stream
+    // made every later chunk wait for their (scattered 2-byte V^T) write acknowledgements
+    // (cold microbench, B=256 ctx 192: 47.8 us fused vs 38.8 us attention alone)
+    const int slot = ra.slots[b];
+    const int blk = slot / kBS, off = slot % kBS;
+    const size_t base = ((size_t)blk * hkv + kvh) * kBS * D;
+    if (r == 0) {
 #pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks) {
-      nc.ka[ks] = r == 0 ? kn[ks] : bf16x8{};
-      nc.kb[ks] = bf16x8{};
+      for (int ks = 0; ks < D / 32; ++ks)
+        *reinterpret_cast<bf16x8*>(k_cache + base + (size_t)off * D + ks * 32 + 8 * g) = kn[ks];
     }
+    if (g == 0) {
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
-      bf16x8 v = {};
-      if (g == 0) v[0] = vn[dt];          // key 0 of the one-key chunk
-      nc.v[dt] = v;
+      for (int dt = 0; dt < D / 16; ++dt) v_cache[base + (size_t)(dt * 16 + r) * kBS + vperm32(off)] = vn[dt];
     }
-    compute_chunk<D>(st, qf, nc, ctx - 1, ctx - 1, scale_log2, lane);
   }
   float lt = st.lsum;
   lt += __shfl_xor(lt, 16, 64);
@@ -431,16 +456,17 @@ static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr
                        (const int32_t*)block_tables, (const int32_t*)seq_lens, (float*)part_o, (float*)part_ml, hq,
                        hkv, max_blocks, split_len, sl2, ra);
   };
-#define DLLM_DEC(DD, FF)                                              \
+#define DLLM_DEC(DD, FF, PP)                                          \
   do {                                                                \
-    if (wpb == 4) go(attn_decode_kernel<DD, 4, FF>, 256);             \
-    else if (wpb == 2) go(attn_decode_kernel<DD, 2, FF>, 128);        \
-    else go(attn_decode_kernel<DD, 1, FF>, 64);                       \
+    if (wpb == 4) go(attn_decode_kernel<DD, 4, FF, PP>, 256);         \
+    else if (wpb == 2) go(attn_decode_kernel<DD, 2, FF, PP>, 128);    \
+    else go(attn_decode_kernel<DD, 1, FF, PP>, 64);                   \
   } while (0)
+  const bool parts = fused && ra.part != nullptr;
   if (d == 128) {
-    if (fused) DLLM_DEC(128, true); else DLLM_DEC(128, false);
+    if (parts) DLLM_DEC(128, true, true); else if (fused) DLLM_DEC(128, true, false); else DLLM_DEC(128, false, false);
   } else {
-    if (fused) DLLM_DEC(64, true); else DLLM_DEC(64, false);
+    if (parts) DLLM_DEC(64, true, true); else if (fused) DLLM_DEC(64, true, false); else DLLM_DEC(64, false, false);
   }
 #undef DLLM_DEC
   DLLM_HIP_CHECK(hipGetLastError());
