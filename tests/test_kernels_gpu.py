@@ -132,8 +132,10 @@ def test_paged_attention_decode_fused_rope(cuda, hq, hkv, d, lens, rope):
     torch.testing.assert_close(v1.float(), v2, atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("version", ["1", "2", "3"])
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 64)])
-def test_paged_attention_prefill(cuda, hq, hkv, d):
+def test_paged_attention_prefill(cuda, monkeypatch, hq, hkv, d, version):
+    monkeypatch.setenv("DLLM_PREFILL_ATTN", version)
     ctx = [37, 128, 300, 5]
     qlen = [37, 64, 1, 5]       # second/third: chunked prefill with prior context
     k, v, bt = _fill_paged(ctx, hkv, d)
