@@ -45,6 +45,9 @@ def parse(argv=None):
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--parallelism", choices=["pp", "dp"], default="pp")
+    ap.add_argument("--pp", type=int, default=0,
+                    help="pipeline depth for --parallelism pp (default: all ranks); world/pp pipelines run as "
+                         "data-parallel replicas, e.g. --gpus 8 --pp 4 = 2 pipelines of 4 stages")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--streams", type=int, default=1, help="1-GPU engine: microbatch slots on separate streams")
     ap.add_argument("--seed", type=int, default=0)
@@ -61,6 +64,13 @@ def make_prompts(n, plen, vocab, seed):
     return rng.integers(100, min(vocab, 30000), size=(n, plen)).tolist()
 
 
+def _par_name(args, world):
+    pp = args.pp if (args.parallelism == "pp" and args.pp) else (world if args.parallelism == "pp" else 1)
+    if args.parallelism == "dp" or pp == 1:
+        return f"dp{world}"
+    return f"pp{pp}" if pp == world else f"dp{world // pp}xpp{pp}"
+
+
 def emit(args, world, elapsed, lat, extra, global_batch=None):
     """global_batch = requests per round over the whole job (default batch x world)."""
     global_batch = global_batch or args.batch * world
@@ -75,7 +85,7 @@ def emit(args, world, elapsed, lat, extra, global_batch=None):
         "p50_latency_ms": round(1000 * statistics.median(lat), 3) if lat else None,
         "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.prompt_len + args.gen_len,
                    "prompt_len": args.prompt_len, "gen_len": args.gen_len,
-                   "parallelism": f"{args.parallelism}{world}"},
+                   "parallelism": _par_name(args, world)},
     }
     rec.update(extra)
     line = json.dumps(rec)

@@ -19,7 +19,7 @@ def _sync(ctx):
 
 
 def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=None):
-    pp = None if args.parallelism == "pp" else 1
+    pp = (getattr(args, "pp", 0) or None) if args.parallelism == "pp" else 1
     ctx = init_distributed(pp=pp)
     world = ctx.world
     # pipeline: prefill in ~8K-token microbatches (M large enough for full-rate GEMMs) so the

@@ -58,3 +58,20 @@ def test_single_process_bench_json_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_lines(r.stdout)[0]
     assert KEYS <= set(rec) and rec["n_gpus"] == 1
+
+
+@pytest.mark.slow
+def test_torchrun_bench_hybrid_dp_pp_cpu():
+    """world 4 = 2 pipelines x 2 stages: each pipeline owns its own scheduler, KV pool and
+    stage-to-stage transport; the job reports the sum over pipelines."""
+    n = 4
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "1", "--warmup", "1", "--model", "tiny-llama", "--batch", "3",
+           "--prompt-len", "6", "--gen-len", "4", "--parallelism", "pp", "--pp", "2"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["config"]["parallelism"] == "dp2xpp2" and rec["n_gpus"] == 4
+    assert rec["microbatch_slots"] == 3 and rec["config"]["global_batch"] == 2 * 3 * 3
