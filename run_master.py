@@ -6,7 +6,9 @@ REPL verbs assign / distribute / inference / exit).  Same verbs, plus flags and 
     python run_master.py --model /path/to/hf_checkpoint --workers 2 --port 65432
     python run_master.py --model synthetic:gpt2-small --workers 2 --device cpu --auto --bench 16
 
-REPL: assign | distribute | inference | generate <n> | status | metrics | exit
+    python run_master.py --model synthetic:llama3-8b --workers 2 --auto --http 8000   # HTTP serving
+
+REPL: assign | distribute | inference | generate <n> | status | metrics | http <port> | exit
 """
 from __future__ import annotations
 
@@ -43,6 +45,10 @@ def parse(argv=None):
     ap.add_argument("--prompt-len", type=int, default=32)
     ap.add_argument("--gen-len", type=int, default=16)
     ap.add_argument("--wait-timeout", type=float, default=300.0)
+    ap.add_argument("--http", type=int, default=-1, metavar="PORT",
+                    help="serve the HTTP API (/generate, /v1/completions, /status, /metrics, /health) on PORT "
+                         "once the pipeline is loaded (0 = any free port); with --auto, serve until Ctrl-C")
+    ap.add_argument("--http-host", default="127.0.0.1")
     ap.add_argument("--log-level", default="INFO")
     return ap.parse_args(argv)
 
@@ -66,6 +72,13 @@ def main(argv=None):
             print("assignments:", master.assign_shards(), flush=True)
             acks = master.distribute_shards()
             print("loaded:", json.dumps({w: x.get("layer_range") for w, x in acks.items()}), flush=True)
+            if a.http >= 0:
+                from distributed_llms_amd.master.http_api import serve_http
+                srv, _ = serve_http(master, a.http_host, a.http)
+                print(f"HTTP API on http://{a.http_host}:{srv.server_address[1]}", flush=True)
+                if not a.bench:
+                    while master.running:        # serve until Ctrl-C
+                        time.sleep(1.0)
             if a.bench:
                 import numpy as np
                 rng = np.random.default_rng(0)
@@ -101,6 +114,10 @@ def main(argv=None):
                 print(json.dumps(master.status(), indent=1, default=str))
             elif cmd == "metrics":
                 print(json.dumps(master.metrics.summary(), indent=1))
+            elif cmd.startswith("http"):
+                from distributed_llms_amd.master.http_api import serve_http
+                srv, _ = serve_http(master, a.http_host, int(cmd.split()[1]) if len(cmd.split()) > 1 else 8000)
+                print(f"HTTP API on http://{a.http_host}:{srv.server_address[1]}")
             elif cmd == "exit":
                 break
             else:

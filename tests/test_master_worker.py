@@ -120,3 +120,47 @@ def test_checkpoint_shards_distributed_by_path(cluster, tmp_path):
     st = ModelStage(cfg, 0, cfg.num_layers, "cpu", __import__("torch").float32).load_hf_state(dict(iter_checkpoint(d)))
     ref = LLMEngine(_cfg(d), st).generate(PROMPTS, SamplingParams(max_new_tokens=5, ignore_eos=True))
     assert [r["tokens"] for r in res] == ref
+
+
+def test_http_api_generate_completions_status_metrics(cluster):
+    """HTTP front end (run_master.py --http): /generate and /v1/completions route through the same
+    request futures as the Python API (identical greedy tokens), /status /metrics /health report."""
+    import json
+    import urllib.request
+
+    from distributed_llms_amd.master.http_api import serve_http
+
+    make, _ = cluster
+    m = make("synthetic:tiny-llama", 2)
+    m.assign_shards()
+    m.distribute_shards(timeout=300)
+    srv, _ = serve_http(m, "127.0.0.1", 0)
+    base = f"http://127.0.0.1:{srv.server_address[1]}"
+
+    def post(path, body):
+        req = urllib.request.Request(base + path, data=json.dumps(body).encode(),
+                                     headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=120) as r:
+            return json.loads(r.read())
+
+    try:
+        expect = m.generate([PROMPTS[0]], max_new_tokens=5, ignore_eos=True, timeout=120)[0]["tokens"]
+        g = post("/generate", {"prompt_ids": PROMPTS[0], "max_new_tokens": 5, "ignore_eos": True})
+        assert g["tokens"] == expect and isinstance(g["text"], str)
+        c = post("/v1/completions", {"prompt": [PROMPTS[0], PROMPTS[1]], "max_tokens": 5, "ignore_eos": True})
+        assert c["object"] == "text_completion" and len(c["choices"]) == 2
+        assert c["choices"][0]["tokens"] == expect and c["usage"]["completion_tokens"] == 10
+        t = post("/v1/completions", {"prompt": "hello world", "max_tokens": 3, "ignore_eos": True})
+        assert len(t["choices"][0]["tokens"]) == 3
+        with urllib.request.urlopen(base + "/health", timeout=30) as r:
+            assert json.loads(r.read())["state"] == "ready"
+        with urllib.request.urlopen(base + "/metrics", timeout=30) as r:
+            assert b"dllm_requests" in r.read()
+        with urllib.request.urlopen(base + "/status", timeout=60) as r:
+            assert json.loads(r.read())["state"] == "ready"
+        bad = urllib.request.Request(base + "/generate", data=b'{"prompt_ids": []}')
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            urllib.request.urlopen(bad, timeout=30)
+        assert ei.value.code == 400
+    finally:
+        srv.shutdown()
