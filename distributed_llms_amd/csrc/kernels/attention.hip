@@ -28,9 +28,9 @@ struct WaveState {
   float lsum;   // lane-partial softmax denominator
 };
 
-// One 32-key chunk's operands, loaded into registers: K rows as two 16-key A tiles, V^T as
-// the A fragments of the P.V MFMA (keys 4g..4g+3 and 16+4g..16+4g+3 of lane group g: k-order
-// permuted to match P; one 16-byte load thanks to the vperm32 column order of the cache).
+// One 32-key chunk's operands, loaded into registers: K rows as two 16-key A tiles (physical
+// rows, see krow32 in common.h), V^T as the A fragments of the P.V MFMA (keys 8g..8g+7 of
+// lane group g: one 16-byte load from the [4][D][8] V^T block).
 template <int D>
 struct KVChunk {
   bf16x8 ka[D / 32], kb[D / 32];
@@ -48,7 +48,7 @@ __device__ __forceinline__ void load_chunk(KVChunk<D>& c, const bf16* __restrict
   }
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt)
-    c.v[dt] = *reinterpret_cast<const bf16x8*>(vblk + (dt * 16 + r) * kBS + 8 * g);
+    c.v[dt] = *reinterpret_cast<const bf16x8*>(vblk + g * 8 * D + (dt * 16 + r) * 8);
 }
 
 // Online-softmax update of the wave's 16 columns with one loaded chunk.
@@ -67,7 +67,7 @@ __device__ __forceinline__ void compute_chunk(WaveState<D>& st, const bf16x8 (&q
   float cm = -INFINITY;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int k0 = t0 + 4 * g + i, k1 = t0 + 16 + 4 * g + i;
+    const int k0 = t0 + 8 * g + i, k1 = t0 + 8 * g + 4 + i;   // S^T rows 4g+i / 16+4g+i (krow32)
     p[i] = (k0 <= kmax_col) ? s0[i] * scale_log2 : -INFINITY;
     p[4 + i] = (k1 <= kmax_col) ? s1[i] * scale_log2 : -INFINITY;
     cm = fmaxf(cm, fmaxf(p[i], p[4 + i]));
@@ -263,16 +263,17 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     if (!FUSED) return;
     const bool here = ctx > 0 && chunk == cnew;
     // (two static selects: a runtime choice between ka and kb made hipcc index them through scratch)
-    const bool krow = here && r == (noff & 15);
-    const bool ka_row = krow && noff < 16, kb_row = krow && noff >= 16;
+    const int prow = krow32(noff);                    // physical K row of the new key
+    const bool krow = here && r == (prow & 15);
+    const bool ka_row = krow && prow < 16, kb_row = krow && prow >= 16;
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
       c.ka[ks] = ka_row ? kn[ks] : c.ka[ks];
       c.kb[ks] = kb_row ? kn[ks] : c.kb[ks];
     }
-    // V^T fragment of lane group g: keys 4g..4g+3 -> elements 0..3, 16+4g..16+4g+3 -> 4..7
-    const int e = (noff & 3) + (noff >= 16 ? 4 : 0);
-    const bool vcol = here && g == ((noff & 15) >> 2);
+    // V^T fragment of lane group g: keys 8g..8g+7 -> elements 0..7
+    const int e = noff & 7;
+    const bool vcol = here && g == (noff >> 3);
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt)
 #pragma unroll
@@ -315,7 +316,7 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
   }
   finish_rope();   // no cache chunk in this split
   if (owns_new) {
-    // append k (row layout) and v^T (column vperm32(off)) to the paged cache only now, after the
+    // append k (row krow32(off)) and v (its [4][D][8] V^T slots) to the paged cache only now, after the
     // last KV load: stores count in vmcnt in issue order, so stores issued before the KV stream
     // made every later chunk wait for their (scattered 2-byte V^T) write acknowledgements
     // (cold microbench, B=256 ctx 192: 47.8 us fused vs 38.8 us attention alone)
@@ -325,11 +326,11 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     if (r == 0) {
 #pragma unroll
       for (int ks = 0; ks < D / 32; ++ks)
-        *reinterpret_cast<bf16x8*>(k_cache + base + (size_t)off * D + ks * 32 + 8 * g) = kn[ks];
+        *reinterpret_cast<bf16x8*>(k_cache + base + (size_t)krow32(off) * D + ks * 32 + 8 * g) = kn[ks];
     }
     if (g == 0) {
 #pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) v_cache[base + (size_t)(dt * 16 + r) * kBS + vperm32(off)] = vn[dt];
+      for (int dt = 0; dt < D / 16; ++dt) v_cache[base + vofs(off, dt * 16 + r, D, kBS)] = vn[dt];
     }
   }
   float lt = st.lsum;

@@ -59,11 +59,19 @@ __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x))
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 
-// Paged V^T cache, 32-key blocks: key j of a block row is stored at column vperm32(j), order
-// 0-3,16-19,4-7,20-23,...  The P.V MFMA's A fragment of lane group g is keys 4g..4g+3 and
-// 16+4g..16+4g+3, which this places in 16 contiguous bytes: one 16-B load per fragment
-// instead of two 8-B loads.  Other block sizes are stored unpermuted.
-__host__ __device__ __forceinline__ int vperm32(int j) {
-  return j < 16 ? ((j >> 2) << 3) + (j & 3) : (((j - 16) >> 2) << 3) + 4 + (j & 3);
+// Paged KV layout of a 32-key block (one kv head), chosen so that the QK^T MFMA output hands
+// every lane group g the probabilities of keys 8g..8g+7 in natural order:
+//   K  [32 rows][D]        key j stored at row krow32(j): 8g+i -> row 4g+i, 8g+4+i -> row 16+4g+i
+//                          (rows 0-15 / 16-31 are the two 16-key MFMA tiles; lane group g of the
+//                          S^T = K Q^T result holds rows 4g..4g+3 of each tile = keys 8g..8g+7)
+//   V^T [4][D][8]          element (key j, dim d) at (j/8)*8D + 8d + j%8: the P.V A-fragment of
+//                          lane (dim d, group g) -- keys 8g..8g+7 of dim d -- is one 16-byte load,
+//                          and a new token's 128 dims land in one 2 KiB span (16 cache lines, not
+//                          64: the per-step append dirties 4x fewer partial lines)
+// Other block sizes (CPU reference path only) use plain rows / a plain [D][bs] V^T.
+__host__ __device__ __forceinline__ int krow32(int j) { return ((j & 4) << 2) + ((j >> 3) << 2) + (j & 3); }
+__host__ __device__ __forceinline__ int krow(int off, int bs) { return bs == 32 ? krow32(off) : off; }
+// element offset of (key off, dim e) inside one head's V^T block of bs keys x d dims
+__host__ __device__ __forceinline__ int vofs(int off, int e, int d, int bs) {
+  return bs == 32 ? (off >> 3) * 8 * d + e * 8 + (off & 7) : e * bs + off;
 }
-__host__ __device__ __forceinline__ int vcol(int off, int bs) { return bs == 32 ? vperm32(off) : off; }

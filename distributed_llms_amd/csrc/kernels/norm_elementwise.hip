@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ q_ou
     if (h < hq) {
       dst = q_out + ((size_t)t * hq + h) * d;
     } else {
-      dst = k_cache + (((size_t)blk * hkv + (h - hq)) * bs + off) * d;
+      dst = k_cache + (((size_t)blk * hkv + (h - hq)) * bs + krow(off, bs)) * d;
     }
     *reinterpret_cast<bf16x4*>(dst + p) = o1;
     *reinterpret_cast<bf16x4*>(dst + half + p) = o2;
@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ q_ou
   const bf16* vsrc = row + (hq + hkv) * d;
   for (int i = threadIdx.x; i < hkv * d; i += blockDim.x) {
     const int h = i / d, e = i % d;
-    v_cache[(((size_t)blk * hkv + h) * d + e) * bs + vcol(off, bs)] = vsrc[i];
+    v_cache[((size_t)blk * hkv + h) * d * bs + vofs(off, e, d, bs)] = vsrc[i];
   }
 }
 

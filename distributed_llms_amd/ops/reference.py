@@ -10,8 +10,9 @@ transformer-block math.
 
 Paged-KV layout (shared with the HIP kernels, one tensor pair per layer):
   k_cache: [num_blocks, num_kv_heads, block_size, head_dim]
-  v_cache: [num_blocks, num_kv_heads, head_dim, block_size]   (key j at column vperm32(j) for 32-key blocks;
-                                                              V stored transposed
+  v_cache: [num_blocks, num_kv_heads, head_dim, block_size]   (32-key blocks: K row / V^T element
+                                                              order of csrc/kernels/common.h krow32 /
+                                                              vofs, a [4][D][8] V^T tile; V stored transposed
            so the P·V MFMA reads token-contiguous 16-byte fragments)
 ``slot = block_id * block_size + offset`` addresses one token's K/V.
 """
@@ -118,33 +119,37 @@ def rope_cache_append(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optio
     bs = k_cache.shape[2]
     slots = slot_mapping.long()
     blk, off = slots // bs, slots % bs
-    k_cache[blk, :, off, :] = k.to(k_cache.dtype)
-    v_cache[blk, :, :, _vcol(off, bs)] = v.to(v_cache.dtype)
+    if bs == 32:
+        k_cache[blk, :, _KROW32.to(off.device)[off], :] = k.to(k_cache.dtype)
+        nb, hkv, d = v_cache.shape[0], v_cache.shape[1], v_cache.shape[2]
+        v_cache.view(nb, hkv, 4, d, 8)[blk, :, off // 8, :, off % 8] = v.to(v_cache.dtype)
+    else:
+        k_cache[blk, :, off, :] = k.to(k_cache.dtype)
+        v_cache[blk, :, :, off] = v.to(v_cache.dtype)
     return q
 
 
-def _vperm32() -> torch.Tensor:
-    """Column of key j in a 32-key V^T block (csrc/kernels/common.h vperm32)."""
+def _krow32() -> torch.Tensor:
+    """Physical row of key j in a 32-key K block (csrc/kernels/common.h krow32)."""
     j = torch.arange(32)
-    return torch.where(j < 16, (j // 4) * 8 + j % 4, ((j - 16) // 4) * 8 + 4 + j % 4)
+    return ((j & 4) << 2) + ((j >> 3) << 2) + (j & 3)
 
 
-_VPERM32 = _vperm32()
-
-
-def _vcol(off: torch.Tensor, bs: int) -> torch.Tensor:
-    return _VPERM32.to(off.device)[off] if bs == 32 else off
+_KROW32 = _krow32()
 
 
 def _gather_kv(k_cache, v_cache, block_table, n):
     bs = k_cache.shape[2]
     nb = (n + bs - 1) // bs
     blocks = block_table[:nb].long()
-    k = k_cache[blocks].permute(1, 0, 2, 3).reshape(k_cache.shape[1], nb * bs, -1)[:, :n]
-    vb = v_cache[blocks]
+    kb, vb = k_cache[blocks], v_cache[blocks]
+    hkv, d = k_cache.shape[1], k_cache.shape[3]
     if bs == 32:
-        vb = vb[..., _VPERM32.to(vb.device)]             # physical columns back to key order
-    v = vb.permute(1, 0, 3, 2).reshape(v_cache.shape[1], nb * bs, -1)[:, :n]
+        kb = kb[:, :, _KROW32.to(kb.device), :]          # physical rows back to key order
+        v = vb.reshape(nb, hkv, 4, d, 8).permute(1, 0, 2, 4, 3).reshape(hkv, nb * bs, d)[:, :n]
+    else:
+        v = vb.permute(1, 0, 3, 2).reshape(hkv, nb * bs, -1)[:, :n]
+    k = kb.permute(1, 0, 2, 3).reshape(hkv, nb * bs, -1)[:, :n]
     return k, v  # [Hkv, n, D]
 
 
