@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--wide", action="store_true", help="three-way: wide-M kernel vs tiled kernel vs hipBLASLt")
     ap.add_argument("--warm", action="store_true", help="no cache flush between calls (in-engine-like)")
     ap.add_argument("--splits", type=int, default=0)
+    ap.add_argument("--variants", type=int, nargs="*", default=[0],
+                    help="--wide: extra gemm_wide variants timed beside the default (1)")
     a = ap.parse_args()
     # a scratch buffer larger than the 256 MiB Infinity Cache to flush it between calls
     flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
@@ -94,7 +96,8 @@ def wide(a, flush):
             # copy (launch overhead out of the measurement, like the engine's captured decode step)
             impls = {
                 "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=1),
-                "wide0": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=0),
+                **{f"v{v}": (lambda w, v=v: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=v))
+                   for v in a.variants},
                 "tiled": lambda w: gemm.linear_tiled(x, w, swiglu=sw),
                 "blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w)),
             }
@@ -122,7 +125,7 @@ def wide(a, flush):
             byt, fl_ = n * k * 2, 2.0 * m * n * k
             print(f"{name:12s} {m:4d} {t['wide']*1e6:8.1f} {byt/t['wide']/1e12:6.2f} {fl_/t['wide']/1e12:6.0f} "
                   f"{t['tiled']*1e6:8.1f} {t['blas']*1e6:8.1f} {t['tiled']/t['wide']:8.2f} {t['blas']/t['wide']:8.2f} "
-                  f"variant0 {t['wide0']*1e6:6.1f}",
+                  + " ".join(f"v{v} {t[f'v{v}']*1e6:6.1f}" for v in a.variants),
                   flush=True)
 
 

@@ -119,16 +119,19 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
   constexpr int AEL = BM * WBK, BEL = WBN * WBK, BUF = AEL + BEL;
   constexpr int AI = BM / 64, BI = 2, G = AI + BI, RT = BM / 64;
   const int wm = wv >> 1, wn = wv & 1;
+  // cache policy of the staging loads (aux: 2 = nt): VAR 2 streams the weights nt, VAR 3 both operands
+  constexpr int BAUX = VAR >= 2 ? 2 : 0, AAUX = VAR == 3 ? 2 : 0;
   auto stage = [&](int buf, int t) {
     bf16* base = smem + buf * BUF;
     const int ko = t * WBK;
 #pragma unroll
     for (int j = 0; j < AI; ++j)
-      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcA[j] + ko), (lds_vptr_w)(base + (wv * AI + j) * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcA[j] + ko), (lds_vptr_w)(base + (wv * AI + j) * 512), 16, 0,
+                                       AAUX);
 #pragma unroll
     for (int j = 0; j < BI; ++j)
       __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcB[j] + ko), (lds_vptr_w)(base + AEL + (wv * BI + j) * 512), 16,
-                                       0, 0);
+                                       0, BAUX);
   };
 
 #pragma unroll
@@ -140,10 +143,11 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
   // one glds piece: p < AI -> A rows, else B rows
   auto piece = [&](bf16* base, int ko, int p) {
     if (p < AI)
-      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcA[p] + ko), (lds_vptr_w)(base + (wv * AI + p) * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcA[p] + ko), (lds_vptr_w)(base + (wv * AI + p) * 512), 16, 0,
+                                       AAUX);
     else
       __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcB[p - AI] + ko),
-                                       (lds_vptr_w)(base + AEL + (wv * BI + p - AI) * 512), 16, 0, 0);
+                                       (lds_vptr_w)(base + AEL + (wv * BI + p - AI) * 512), 16, 0, BAUX);
   };
   // one K-tile of MFMAs from buffer `cur`; with STG the next tile's G LDS-DMA pieces are issued
   // in between the MFMAs (each glds costs ~60-185 issue cycles: issued back to back after the
@@ -285,7 +289,7 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
 // the decode regime of Mixtral at B >= 128 (32-128 rows per expert), where the weight-streaming
 // grouped kernel (moe.hip) runs its MFMAs at a fraction of the rate.
 // ---------------------------------------------------------------------------------------------
-template <int BM, bool SWIGLU>
+template <int BM, bool SWIGLU, int VAR>
 __device__ __forceinline__ void moe_wide_rows(bf16* smem, bf16* __restrict__ Y, const bf16* __restrict__ X,
                                               const int* __restrict__ gather, const bf16* __restrict__ We, int cnt,
                                               int off, int N, int K, int n_t, int wv, int lane) {
@@ -309,7 +313,7 @@ __device__ __forceinline__ void moe_wide_rows(bf16* smem, bf16* __restrict__ Y, 
       srcB[j] = We + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + wswz(r, lane & 7) * 8;
     }
     f32x4 acc[RT][4];
-    wide_mainloop<BM, 3, 1>(smem, srcA, srcB, K / WBK, acc, wv, lane);
+    wide_mainloop<BM, 3, VAR>(smem, srcA, srcB, K / WBK, acc, wv, lane);
     wide_epilogue<BM, false, SWIGLU>(acc, Y + (size_t)(off + r0) * ldy, nullptr, rows, N, 0, n_t, 0, wm, wn, lane);
     __syncthreads();   // the next chunk's prologue refills buffers other waves may still read
   }
@@ -319,7 +323,7 @@ template <bool SWIGLU>
 __global__ void __launch_bounds__(512, 1) moe_wide_kernel(bf16* __restrict__ Y, const bf16* __restrict__ X,
                                                           const int* __restrict__ gather, const bf16* __restrict__ W,
                                                           const int* __restrict__ counts,
-                                                          const int* __restrict__ offsets, int N, int K) {
+                                                          const int* __restrict__ offsets, int N, int K, int nt) {
   __shared__ __attribute__((aligned(16))) bf16 smem[3 * (128 + WBN) * WBK];
   const int e = blockIdx.y;
   const int cnt = counts[e];
@@ -327,8 +331,16 @@ __global__ void __launch_bounds__(512, 1) moe_wide_kernel(bf16* __restrict__ Y, 
   const int off = offsets[e];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bf16* We = W + (size_t)e * N * K;
-  if (cnt <= 64) moe_wide_rows<64, SWIGLU>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
-  else moe_wide_rows<128, SWIGLU>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+  // an expert's weight tile is read once when its rows fit one row tile: stream it nt (variant 2);
+  // with several row chunks the re-reads should hit the caches (default policy)
+  if (cnt <= 64) {
+    if (nt) moe_wide_rows<64, SWIGLU, 2>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+    else moe_wide_rows<64, SWIGLU, 1>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+  } else if (cnt <= 128 && nt) {
+    moe_wide_rows<128, SWIGLU, 2>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+  } else {
+    moe_wide_rows<128, SWIGLU, 1>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+  }
 }
 
 // mode 1 (SwiGLU): W [E, 2I, K] -> Y [slots, I]; mode 0: W [E, N, K] -> Y [slots, N]
@@ -340,12 +352,13 @@ void moe_wide_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uint
   DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ntiles = mode == 1 ? (N / 2) / 64 : N / WBN;
+  static const int nt = [] { const char* e = getenv("DLLM_MOE_WIDE_NT"); return e ? atoi(e) : 1; }();
   if (mode == 1)
     hipLaunchKernelGGL(moe_wide_kernel<true>, dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
-                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K);
+                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt);
   else
     hipLaunchKernelGGL(moe_wide_kernel<false>, dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
-                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K);
+                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt);
   DLLM_HIP_CHECK(hipGetLastError());
 }
 
@@ -372,12 +385,19 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   DLLM_HOST_CHECK(grid >= 1 && grid < (1L << 31), "grid");
   if (S > 1) DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
 
+  // weights nt (variant 2) where the grid has no K split: -3..-5 % on the MLP up projection from
+  // cold caches; on the split-K grids nt costs up to +25 % at M = 128 (profiles/wide_gemm.md)
+  // (variant 4 = variant 1 everywhere, for A/B runs)
+  if (variant == 1 && S == 1) variant = 2;
+  else if (variant == 4) variant = 1;
 #define DLLM_WIDE_GO3(BM_, SPLIT_, SW_, V_)                                                                      \
   hipLaunchKernelGGL((gemm_wide_kernel<BM_, SPLIT_, SW_, 3, V_>), dim3((unsigned)grid), dim3(512), 0, s,          \
                      (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S)
 #define DLLM_WIDE_GO(BM_, SPLIT_, SW_)                                                                          \
   do {                                                                                                         \
     if (variant == 0) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 0);                                                      \
+    else if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 2);                                                 \
+    else if (variant == 3) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 3);                                                 \
     else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 1);                                                                   \
   } while (0)
   if (S == 1) {
