@@ -37,18 +37,24 @@ struct KVChunk {
   bf16x8 v[D / 16];
 };
 
-template <int D>
+template <int D, bool NT = false>
 __device__ __forceinline__ void load_chunk(KVChunk<D>& c, const bf16* __restrict__ kblk,
                                            const bf16* __restrict__ vblk, int lane) {
   const int r = lane & 15, g = lane >> 4;
+// NT: the decode wave reads each K/V line once per step (cold, HBM): nontemporal loads cut the
+// attention alone 41.4 -> 35.3 us at B=256 / ctx 192 (profiles/attn_fused_ablation.md); prefill
+// re-reads a sequence's K/V for every q tile and keeps the default policy
+#define DLLM_KVLD(p) (NT ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p)) \
+                         : *reinterpret_cast<const bf16x8*>(p))
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
-    c.ka[ks] = *reinterpret_cast<const bf16x8*>(kblk + r * D + ks * 32 + 8 * g);
-    c.kb[ks] = *reinterpret_cast<const bf16x8*>(kblk + (16 + r) * D + ks * 32 + 8 * g);
+    c.ka[ks] = DLLM_KVLD(kblk + r * D + ks * 32 + 8 * g);
+    c.kb[ks] = DLLM_KVLD(kblk + (16 + r) * D + ks * 32 + 8 * g);
   }
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt)
-    c.v[dt] = *reinterpret_cast<const bf16x8*>(vblk + g * 8 * D + (dt * 16 + r) * 8);
+    c.v[dt] = DLLM_KVLD(vblk + g * 8 * D + (dt * 16 + r) * 8);
+#undef DLLM_KVLD
 }
 
 // Online-softmax update of the wave's 16 columns with one loaded chunk.
@@ -291,20 +297,20 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     KVChunk<D> cur, nxt;
     {
       const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, 0) * blk_stride + head_off;
-      load_chunk<D>(cur, k_cache + base, v_cache + base, lane);
+      load_chunk<D, true>(cur, k_cache + base, v_cache + base, lane);
     }
     finish_rope();
     int j = 0;
     for (; j + 2 <= n; j += 2) {                    // ping-pong: cur <-> nxt
       {
         const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, j + 1) * blk_stride + head_off;
-        load_chunk<D>(nxt, k_cache + base, v_cache + base, lane);
+        load_chunk<D, true>(nxt, k_cache + base, v_cache + base, lane);
       }
       patch(cur, cb + j);
       compute_chunk<D>(st, qf, cur, (cb + j) * kBS, kmax, scale_log2, lane);
       if (j + 2 < n) {
         const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, j + 2) * blk_stride + head_off;
-        load_chunk<D>(cur, k_cache + base, v_cache + base, lane);
+        load_chunk<D, true>(cur, k_cache + base, v_cache + base, lane);
       }
       patch(nxt, cb + j + 1);
       compute_chunk<D>(st, qf, nxt, (cb + j + 1) * kBS, kmax, scale_log2, lane);

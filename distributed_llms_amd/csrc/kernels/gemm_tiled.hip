@@ -131,9 +131,12 @@ __global__ void __launch_bounds__(256, 2) gemm_tiled_kernel(const bf16* __restri
 }
 
 // out[m, n] = sum_s P[s, m, n] (+ bias[n]);  swiglu: out[m, j] = silu(sum P[m, j]) * sum P[m, I + j]
-template <bool SWIGLU>
+template <bool SWIGLU, int SC>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16* __restrict__ out, const float* __restrict__ P,
-                                                            const bf16* __restrict__ bias, int S, int M, int N) {
+                                                            const bf16* __restrict__ bias, int S_, int M, int N) {
+  // SC > 0: compile-time slab count -> every slab load of a vector is in flight before the first
+  // add (nontemporal: the slabs are read once); SC == 0: runtime loop
+  const int S = SC > 0 ? SC : S_;
   const int ncols = SWIGLU ? N / 2 : N;
   const long total = (long)M * ncols / 4;
   const size_t slab = (size_t)M * N;
@@ -141,9 +144,23 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16* __restrict__ o
     const long e = v * 4;
     const int m = (int)(e / ncols), c = (int)(e % ncols);
     f32x4 a = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < S; ++s) {
-      a += *reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + c);
-      if (SWIGLU) u += *reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + ncols + c);
+    if constexpr (SC > 0) {
+      f32x4 la[SC], lu[SC];
+#pragma unroll
+      for (int s = 0; s < SC; ++s) {
+        la[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + c));
+        if (SWIGLU) lu[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + ncols + c));
+      }
+#pragma unroll
+      for (int s = 0; s < SC; ++s) {   // same slab order as the runtime loop: bit-identical sums
+        a += la[s];
+        if (SWIGLU) u += lu[s];
+      }
+    } else {
+      for (int s = 0; s < S; ++s) {
+        a += *reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + c);
+        if (SWIGLU) u += *reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + ncols + c);
+      }
     }
     bf16x4 o;
 #pragma unroll
@@ -270,13 +287,25 @@ void splitk_reduce_ex(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M,
   long blocks = ((long)M * ncols / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks == 0) return;
-  if (swiglu)
-    hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3((unsigned)blocks), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), (bf16*)out, (const float*)ws, (const bf16*)nullptr, S, M,
-                       N);
-  else
-    hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3((unsigned)blocks), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), (bf16*)out, (const float*)ws, (const bf16*)bias, S, M, N);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bf16* b = swiglu ? nullptr : (const bf16*)bias;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, (bf16*)out, (const float*)ws, b, S, M, N);
+  };
+#define DLLM_SKR(SW)                                                   \
+  do {                                                                 \
+    switch (S) {                                                       \
+      case 2: go(splitk_reduce_kernel<SW, 2>); break;                  \
+      case 3: go(splitk_reduce_kernel<SW, 3>); break;                  \
+      case 4: go(splitk_reduce_kernel<SW, 4>); break;                  \
+      case 5: go(splitk_reduce_kernel<SW, 5>); break;                  \
+      case 6: go(splitk_reduce_kernel<SW, 6>); break;                  \
+      case 8: go(splitk_reduce_kernel<SW, 8>); break;                  \
+      default: go(splitk_reduce_kernel<SW, 0>);                        \
+    }                                                                  \
+  } while (0)
+  if (swiglu) DLLM_SKR(true); else DLLM_SKR(false);
+#undef DLLM_SKR
   DLLM_HIP_CHECK(hipGetLastError());
 }
 
@@ -308,16 +337,7 @@ void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t
                      (float*)ws, M, N, K, kps);
   DLLM_HIP_CHECK(hipGetLastError());
   if (mode == 2) return;
-  const int ncols = mode == 1 ? N / 2 : N;
-  long blocks = ((long)M * ncols / 4 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  if (mode == 1)
-    hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, (bf16*)c,
-                       (const float*)ws, (const bf16*)nullptr, S, M, N);
-  else
-    hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, (bf16*)c,
-                       (const float*)ws, (const bf16*)bias, S, M, N);
-  DLLM_HIP_CHECK(hipGetLastError());
+  splitk_reduce_ex(c, ws, bias, S, M, N, mode == 1, stream);
 }
 
 }  // namespace dllm
