@@ -19,6 +19,11 @@
 namespace dllm {
 
 constexpr int kBS = 32;       // tokens per KV block (== keys per MFMA chunk)
+#ifndef DLLM_VFULL
+#define DLLM_VFULL 1
+#endif
+// fused decode appends v by rewriting its key group's whole V^T tile (see patch() below)
+constexpr bool kVFullLines = DLLM_VFULL;
 constexpr int kWaves = 4;     // waves per workgroup
 
 template <int D>
@@ -265,7 +270,7 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
   // FUSED: put the new key into the registers of its chunk (branch-free: lane masks only)
   const int cnew = FUSED ? (ctx - 1) / kBS : -1;
   const int noff = FUSED ? (ctx - 1) % kBS : 0;
-  auto patch = [&](KVChunk<D>& c, int chunk) {
+  auto patch = [&](KVChunk<D>& c, int chunk, size_t cbase) {
     if (!FUSED) return;
     const bool here = ctx > 0 && chunk == cnew;
     // (two static selects: a runtime choice between ka and kb made hipcc index them through scratch)
@@ -284,6 +289,17 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     for (int dt = 0; dt < D / 16; ++dt)
 #pragma unroll
       for (int i = 0; i < 8; ++i) c.v[dt][i] = (vcol && i == e) ? vn[dt] : c.v[dt][i];
+    if constexpr (kVFullLines) {
+      // append v as WHOLE lines: the 16 lanes of the new key's group hold the group's complete
+      // [D][8] V^T tile (2 KiB, 16 full 128-B lines) with the new key patched in -- no partially
+      // written lines to read-modify-write.  This is the sequence's last chunk: no KV load follows
+      // whose vmcnt wait would include these stores.
+      if (vcol && owns_new) {
+#pragma unroll
+        for (int dt = 0; dt < D / 16; ++dt)
+          *reinterpret_cast<bf16x8*>(v_cache + cbase + g * 8 * D + (dt * 16 + r) * 8) = c.v[dt];
+      }
+    }
   };
   WaveState<D> st;
   init_state(st);
@@ -306,17 +322,17 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
         const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, j + 1) * blk_stride + head_off;
         load_chunk<D, true>(nxt, k_cache + base, v_cache + base, lane);
       }
-      patch(cur, cb + j);
+      patch(cur, cb + j, (size_t)__builtin_amdgcn_readlane(my_blk, j) * blk_stride + head_off);
       compute_chunk<D>(st, qf, cur, (cb + j) * kBS, kmax, scale_log2, lane);
       if (j + 2 < n) {
         const size_t base = (size_t)__builtin_amdgcn_readlane(my_blk, j + 2) * blk_stride + head_off;
         load_chunk<D, true>(cur, k_cache + base, v_cache + base, lane);
       }
-      patch(nxt, cb + j + 1);
+      patch(nxt, cb + j + 1, (size_t)__builtin_amdgcn_readlane(my_blk, j + 1) * blk_stride + head_off);
       compute_chunk<D>(st, qf, nxt, (cb + j + 1) * kBS, kmax, scale_log2, lane);
     }
     if (j < n) {
-      patch(cur, cb + j);
+      patch(cur, cb + j, (size_t)__builtin_amdgcn_readlane(my_blk, j) * blk_stride + head_off);
       compute_chunk<D>(st, qf, cur, (cb + j) * kBS, kmax, scale_log2, lane);
     }
   }
@@ -334,7 +350,7 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
       for (int ks = 0; ks < D / 32; ++ks)
         *reinterpret_cast<bf16x8*>(k_cache + base + (size_t)krow32(off) * D + ks * 32 + 8 * g) = kn[ks];
     }
-    if (g == 0) {
+    if (!kVFullLines && g == 0) {
 #pragma unroll
       for (int dt = 0; dt < D / 16; ++dt) v_cache[base + vofs(off, dt * 16 + r, D, kBS)] = vn[dt];
     }
