@@ -63,6 +63,8 @@ def build_kernels(force=False, jobs=8, verbose=False) -> str:
     incs = [f"-I{p}" for p in _py_includes()] + [f"-I{src_dir}"]
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
               "-mcode-object-version=5"]
+    if os.environ.get("DLLM_PART_TYPE"):        # split-K slab type (common.h); rebuild with force=True
+        common.append(f"-DDLLM_PART_TYPE={int(os.environ['DLLM_PART_TYPE'])}")
     jobs_list = []
     objs = []
     for src in hips:

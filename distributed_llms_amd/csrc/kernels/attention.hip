@@ -148,7 +148,7 @@ struct RopeArgs {
   const int32_t* positions; // [B]
   const float* cos_sin;     // [max_pos, D] (first half cos, second half sin) or null (no RoPE)
   const int32_t* slots;     // [B] cache slot of the new token
-  // optional: the qkv projection as S f32 split-K partial slabs [S][B][(hq + 2 hkv) * D] (qkv
+  // optional: the qkv projection as S split-K partial slabs (common.h part_t) [S][B][(hq + 2 hkv) * D] (qkv
   // unused); summed in slab order and rounded to bf16 -- bit-identical to splitk_reduce + bf16
   const float* part = nullptr;
   int nparts = 0;
@@ -161,11 +161,11 @@ struct RopeArgs {
 template <bool PARTS>
 __device__ __forceinline__ bf16x8 qkv_load8(const RopeArgs& ra, int b, int width, int off) {
   if constexpr (!PARTS) return *reinterpret_cast<const bf16x8*>(ra.qkv + (size_t)b * width + off);
-  const float* p = ra.part + (size_t)b * width + off;
+  const size_t p = (size_t)b * width + off;
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
   for (int s = 0; s < ra.nparts; ++s) {
-    a0 += *reinterpret_cast<const f32x4*>(p + s * ra.slab);
-    a1 += *reinterpret_cast<const f32x4*>(p + s * ra.slab + 4);
+    a0 += part_load4(ra.part, p + s * ra.slab);
+    a1 += part_load4(ra.part, p + s * ra.slab + 4);
   }
   bf16x8 o;
 #pragma unroll
@@ -179,9 +179,9 @@ __device__ __forceinline__ bf16x8 qkv_load8(const RopeArgs& ra, int b, int width
 template <bool PARTS>
 __device__ __forceinline__ bf16 qkv_load1(const RopeArgs& ra, int b, int width, int off) {
   if constexpr (!PARTS) return ra.qkv[(size_t)b * width + off];
-  const float* p = ra.part + (size_t)b * width + off;
+  const size_t p = (size_t)b * width + off;
   float a = 0.f;
-  for (int s = 0; s < ra.nparts; ++s) a += p[s * ra.slab];
+  for (int s = 0; s < ra.nparts; ++s) a += part_load1(ra.part, p + s * ra.slab);
   return f2bf(a);
 }
 

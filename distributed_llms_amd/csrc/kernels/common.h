@@ -75,3 +75,51 @@ __host__ __device__ __forceinline__ int krow(int off, int bs) { return bs == 32 
 __host__ __device__ __forceinline__ int vofs(int off, int e, int d, int bs) {
   return bs == 32 ? (off >> 3) * 8 * d + e * 8 + (off & 7) : e * bs + off;
 }
+
+// ---- split-K partial slabs (the workspace the split GEMMs leave for the next op).
+// DLLM_PART_TYPE selects the slab element (indices are in elements of that type):
+//   0  f32
+//   1  bf16           (8-bit significand: the test tolerances of a 14k-deep sum are exceeded)
+//   2  f16 x 2^-6     (default: 11-bit significand, 3 bits more than the bf16 output; the 2^-6
+//                      scale puts the f16 range at +-4.2e6 and the subnormal step at 3.8e-6)
+// Each K slice still accumulates in f32 MFMA registers and the cross-slice sum is f32; 2 and 1
+// halve the slab bytes the GEMM epilogue writes and the next op reads.
+#ifndef DLLM_PART_TYPE
+#define DLLM_PART_TYPE 2
+#endif
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr float kPartScale = 0.015625f, kPartUnscale = 64.f;
+__device__ __forceinline__ void part_store(float* P, size_t i, float v) {
+#if DLLM_PART_TYPE == 1
+  reinterpret_cast<bf16*>(P)[i] = f2bf(v);
+#elif DLLM_PART_TYPE == 2
+  reinterpret_cast<_Float16*>(P)[i] = (_Float16)(v * kPartScale);
+#else
+  P[i] = v;
+#endif
+}
+__device__ __forceinline__ float part_load1(const float* P, size_t i) {
+#if DLLM_PART_TYPE == 1
+  return bf2f(reinterpret_cast<const bf16*>(P)[i]);
+#elif DLLM_PART_TYPE == 2
+  return (float)reinterpret_cast<const _Float16*>(P)[i] * kPartUnscale;
+#else
+  return P[i];
+#endif
+}
+// 4 consecutive elements (aligned to 4 elements)
+template <bool NT = false>
+__device__ __forceinline__ f32x4 part_load4(const float* P, size_t i) {
+#if DLLM_PART_TYPE == 1
+  const bf16x4* q = reinterpret_cast<const bf16x4*>(reinterpret_cast<const bf16*>(P) + i);
+  const bf16x4 v = NT ? __builtin_nontemporal_load(q) : *q;
+  return f32x4{bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3])};
+#elif DLLM_PART_TYPE == 2
+  const f16x4* q = reinterpret_cast<const f16x4*>(reinterpret_cast<const _Float16*>(P) + i);
+  const f16x4 v = NT ? __builtin_nontemporal_load(q) : *q;
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]} * kPartUnscale;
+#else
+  const f32x4* q = reinterpret_cast<const f32x4*>(P + i);
+  return NT ? __builtin_nontemporal_load(q) : *q;
+#endif
+}

@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(256, 2) gemm_tiled_kernel(const bf16* __restri
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         const int n = n0 + wn * 64 + ct * 16 + fr;
-        if (SPLIT) P[((size_t)split * M + m) * N + n] = acc[rt][ct][i];
+        if (SPLIT) part_store(P, ((size_t)split * M + m) * N + n, acc[rt][ct][i]);
         else C[(size_t)m * N + n] = f2bf(acc[rt][ct][i]);
       }
     }
@@ -148,8 +148,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16* __restrict__ o
       f32x4 la[SC], lu[SC];
 #pragma unroll
       for (int s = 0; s < SC; ++s) {
-        la[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + c));
-        if (SWIGLU) lu[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + ncols + c));
+        la[s] = part_load4<true>(P, s * slab + (size_t)m * N + c);
+        if (SWIGLU) lu[s] = part_load4<true>(P, s * slab + (size_t)m * N + ncols + c);
       }
 #pragma unroll
       for (int s = 0; s < SC; ++s) {   // same slab order as the runtime loop: bit-identical sums
@@ -158,8 +158,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16* __restrict__ o
       }
     } else {
       for (int s = 0; s < S; ++s) {
-        a += *reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + c);
-        if (SWIGLU) u += *reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + ncols + c);
+        a += part_load4(P, s * slab + (size_t)m * N + c);
+        if (SWIGLU) u += part_load4(P, s * slab + (size_t)m * N + ncols + c);
       }
     }
     bf16x4 o;
@@ -197,14 +197,14 @@ __global__ void __launch_bounds__(256) splitk_add_rms_norm_kernel(bf16* __restri
   for (int i = 0; i < MAXV; ++i) {
     const int idx = threadIdx.x + i * 256;
     if (idx < nvec) {
-      const float* p = P + (size_t)row * N + idx * 8;
+      const size_t p = (size_t)row * N + idx * 8;
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
       if constexpr (SC > 0) {
         f32x4 l0[SC], l1[SC];
 #pragma unroll
         for (int s = 0; s < SC; ++s) {
-          l0[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + s * slab));
-          l1[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + s * slab + 4));
+          l0[s] = part_load4<true>(P, p + s * slab);
+          l1[s] = part_load4<true>(P, p + s * slab + 4);
         }
 #pragma unroll
         for (int s = 0; s < SC; ++s) {   // same slab order as the runtime loop: bit-identical sums
@@ -213,8 +213,8 @@ __global__ void __launch_bounds__(256) splitk_add_rms_norm_kernel(bf16* __restri
         }
       } else {
         for (int s = 0; s < S; ++s) {
-          a0 += *reinterpret_cast<const f32x4*>(p + s * slab);
-          a1 += *reinterpret_cast<const f32x4*>(p + s * slab + 4);
+          a0 += part_load4(P, p + s * slab);
+          a1 += part_load4(P, p + s * slab + 4);
         }
       }
       const bf16x8 b = rr[idx];
@@ -320,7 +320,7 @@ void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t
   DLLM_HOST_CHECK(N % TBN == 0, "N must be a multiple of 128");
   DLLM_HOST_CHECK(K % TBK == 0, "K must be a multiple of 64");
   DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
-  DLLM_HOST_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");   // 2: leave f32 partials in ws, no reduce
+  DLLM_HOST_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");   // 2: leave partial slabs in ws, no reduce
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int kps = (K / TBK + splits - 1) / splits * TBK;
   const int S = (K + kps - 1) / kps;

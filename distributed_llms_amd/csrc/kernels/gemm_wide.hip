@@ -21,7 +21,7 @@
 //    alternately from the gate half and the up half of the fused [2I, K] weight, so the same lane
 //    holds gate column j and up column j in neighbouring accumulators and the epilogue writes
 //    silu(g) * u directly (no [M, 2I] intermediate, no separate silu_mul launch);
-//  * optional split-K: f32 partial slabs in natural column order, reduced by the next op
+//  * optional split-K: partial slabs (f16 x 2^-6, common.h) in natural column order, reduced by the next op
 //    (splitk_add_rms_norm) or by splitk_reduce(_swiglu);
 //  * XCD-aware block order (bijective remap): the M tiles and K slices of one N tile run
 //    back-to-back on one XCD;
@@ -101,7 +101,7 @@ __device__ __forceinline__ void wide_epilogue(const f32x4 (&acc)[BM / 64][4], bf
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
           const int n = wide_b_row<SWIGLU>(wn * 64 + ct * 16 + fr, n_t, N / 2);
-          if (SPLIT) P[((size_t)split * M + m) * N + n] = acc[rt][ct][i];
+          if (SPLIT) part_store(P, ((size_t)split * M + m) * N + n, acc[rt][ct][i]);
           else C[(size_t)m * N + n] = f2bf(acc[rt][ct][i]);
         }
       }
@@ -363,7 +363,7 @@ void moe_wide_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uint
 }
 
 // mode 0: C = A B^T;  mode 1: SwiGLU, C[M, N/2] = silu(A Bg^T) * (A Bu^T) with B = [Bg; Bu];
-// mode 2: leave f32 split-K partials in ws (no reduce; S > 1 required).
+// mode 2: leave split-K partial slabs in ws (no reduce; S > 1 required).
 // Returns the effective number of K slices S (the partial slabs a deferred reduce must sum).
 int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
               int mode, int variant, uintptr_t stream) {

@@ -240,7 +240,7 @@ def paged_attention_decode_rope(qkv, positions, cos_sin, k_cache, v_cache, slot_
     attends over the whole context including it.  Same result as ``rope_cache_append`` followed by
     ``paged_attention_decode`` (the new key is folded in last instead of inside its block).
 
-    ``qkv`` may be a :class:`gemm.SplitKPartial`: the kernel then sums the f32 split-K slabs itself
+    ``qkv`` may be a :class:`gemm.SplitKPartial`: the kernel then sums the split-K slabs (f32 sums of f16 x 2^-6 slices) itself
     (bit-identical to reducing first), which removes the reduce launch and the bf16 round trip."""
     part = None
     if isinstance(qkv, gemm.SplitKPartial):

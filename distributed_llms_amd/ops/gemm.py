@@ -95,7 +95,9 @@ def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: 
 
 
 class SplitKPartial:
-    """f32 split-K partial sums of ``x @ w.T`` still in the per-stream workspace (not reduced).
+    """Split-K partial sums of ``x @ w.T`` still in the per-stream workspace (not reduced).  Each K
+    slice accumulates in f32; the slabs hold it as f16 x 2^-6 by default (csrc/kernels/common.h
+    ``DLLM_PART_TYPE``: half the bytes of f32 slabs, 3 significand bits more than the bf16 result).
 
     Returned by ``linear(..., defer=True)`` when the split-K tiled kernel ran, so the NEXT op can
     fuse the reduction (``ops.fused_add_rms_norm`` -> splitk_add_rms_norm); anything else calls

@@ -141,6 +141,20 @@ def test_wide_swiglu(cuda, m, inter, k, splits, variant):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
+def test_splitk_slabs_keep_output_precision(cuda):
+    """Split-K slabs are stored as f16 x 2^-6 (csrc/kernels/common.h, DLLM_PART_TYPE 2): the split
+    result must stay within one bf16 ulp of the exact product (plus half an ulp of the output's typical
+    magnitude, for outputs near zero), with a mean error no worse than 1.25x that of the unsplit
+    kernel (whose only error is the bf16 output rounding)."""
+    x, w = _bf(256, 14336), _bf(4096, 14336, scale=0.02)
+    ref = x.float() @ w.float().t()
+    e1 = (gemm.linear_wide(x, w, splits=1).float() - ref).abs()
+    e8 = (gemm.linear_wide(x, w, splits=8).float() - ref).abs()
+    assert e8.mean() <= 1.25 * e1.mean(), (e8.mean().item(), e1.mean().item())
+    bound = ref.abs() * 2.0 ** -7 + ref.std() * 2.0 ** -8
+    assert bool((e8 <= bound).all()), (e8 - bound).max().item()
+
+
 def test_wide_deferred_splitk_matches_materialized(cuda):
     x, w = _bf(256, 14336), _bf(4096, 14336, scale=0.02)
     p = gemm.linear_wide(x, w, splits=8, defer=True)
