@@ -269,6 +269,11 @@ void splitk_add_rms_norm(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, i
     if (!const_slabs) go(splitk_add_rms_norm_kernel<MV, 0>);           \
     else if (S == 8) go(splitk_add_rms_norm_kernel<MV, 8>);                 \
     else if (S == 4) go(splitk_add_rms_norm_kernel<MV, 4>);            \
+    else if (S == 2) go(splitk_add_rms_norm_kernel<MV, 2>);            \
+    else if (S == 3) go(splitk_add_rms_norm_kernel<MV, 3>);            \
+    else if (S == 5) go(splitk_add_rms_norm_kernel<MV, 5>);            \
+    else if (S == 6) go(splitk_add_rms_norm_kernel<MV, 6>);            \
+    else if (S == 7) go(splitk_add_rms_norm_kernel<MV, 7>);            \
     else go(splitk_add_rms_norm_kernel<MV, 0>);                        \
   } while (0)
   if (nvec <= 256) DLLM_SKN(1);

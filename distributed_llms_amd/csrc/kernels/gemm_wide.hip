@@ -378,7 +378,7 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   const int kts = (ktiles + splits - 1) / splits;
   const int S = (ktiles + kts - 1) / kts;
   DLLM_HOST_CHECK(mode != 2 || S > 1, "mode 2 needs a K split");
-  const int BM = M <= 128 ? 128 : 256;
+  const int BM = M <= 64 ? 64 : M <= 128 ? 128 : 256;
   const int mtiles = (M + BM - 1) / BM;
   const int ntiles = swiglu ? (N / 2) / 64 : N / WBN;
   const long grid = (long)ntiles * mtiles * S;
@@ -401,12 +401,14 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
     else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 1);                                                                   \
   } while (0)
   if (S == 1) {
-    if (BM == 128) { if (swiglu) DLLM_WIDE_GO(128, false, true); else DLLM_WIDE_GO(128, false, false); }
+    if (BM == 64) { if (swiglu) DLLM_WIDE_GO(64, false, true); else DLLM_WIDE_GO(64, false, false); }
+    else if (BM == 128) { if (swiglu) DLLM_WIDE_GO(128, false, true); else DLLM_WIDE_GO(128, false, false); }
     else { if (swiglu) DLLM_WIDE_GO(256, false, true); else DLLM_WIDE_GO(256, false, false); }
     DLLM_HIP_CHECK(hipGetLastError());
     return 1;
   }
-  if (BM == 128) { if (swiglu) DLLM_WIDE_GO(128, true, true); else DLLM_WIDE_GO(128, true, false); }
+  if (BM == 64) { if (swiglu) DLLM_WIDE_GO(64, true, true); else DLLM_WIDE_GO(64, true, false); }
+  else if (BM == 128) { if (swiglu) DLLM_WIDE_GO(128, true, true); else DLLM_WIDE_GO(128, true, false); }
   else { if (swiglu) DLLM_WIDE_GO(256, true, true); else DLLM_WIDE_GO(256, true, false); }
 #undef DLLM_WIDE_GO
 #undef DLLM_WIDE_GO3

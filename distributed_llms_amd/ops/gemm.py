@@ -71,7 +71,7 @@ def _use_tiled(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool
     return GEMM_MODE == "tiled" or k >= 8192 or n <= TILED_NMAX
 
 
-# DLLM_WIDE: which decode-sized (64 < M <= 512) GEMMs the wide-M kernel (gemm_wide.hip) serves:
+# DLLM_WIDE: which decode-sized (M <= 512) GEMMs the wide-M kernel (gemm_wide.hip) serves:
 #   comma list of gate_up (SwiGLU-fused MLP up projection), down (K >= 8192, deferred split-K),
 #   proj (the other projections: qkv, o), all, or none.  Default "auto", from the in-engine A/B
 #   (scripts/gpu_ab_wide.sh, profiles/wide_gemm.md): gate_up + down for M <= 512 (+4.3 % at
@@ -80,8 +80,13 @@ WIDE = {t for t in os.environ.get("DLLM_WIDE", "auto").split(",") if t and t != 
 WIDE_VARIANT = int(os.environ.get("DLLM_WIDE_VARIANT", "1"))
 
 
+# smallest M the wide kernel serves (1: every decode batch; the 64-row tile at M <= 64 streams
+# the weights at 4.5-6.4 TB/s, +15-19 % tok/s over skinny / hipBLASLt at B = 1..64)
+WIDE_MIN_M = int(os.environ.get("DLLM_WIDE_MIN_M", "1"))
+
+
 def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
-    if not WIDE or GEMM_MODE == "blas" or not (64 < m <= 512) or n % 128 or k % 64:
+    if not WIDE or GEMM_MODE == "blas" or not (WIDE_MIN_M <= m <= 512) or n % 128 or k % 64:
         return False
     if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
         return False
@@ -130,12 +135,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     m = x.numel() // k
     if w.shape[1] != k:
         raise ValueError(f"linear: x[..., {k}] vs w {tuple(w.shape)}")
+    # the wide kernel first: with its 64-row tile it streams the weights faster than the skinny
+    # kernel and hipBLASLt at every decode M (profiles/wide_gemm.md, "small M")
+    if bias is None and not force_skinny and _use_wide(m, n, k, x, w):
+        return linear_wide(x, w, defer=defer)
     if skinny_ok(m, n, k, x, w, force=force_skinny) and (bias is None or bias.dtype == torch.bfloat16):
         y = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
         _launch(x, w, bias, y, m, n, k, 0)
         return y
-    if bias is None and _use_wide(m, n, k, x, w):
-        return linear_wide(x, w, defer=defer)
     if _use_tiled(m, n, k, x, w) and (bias is None or bias.dtype == torch.bfloat16):
         if defer and bias is None:
             return linear_tiled(x, w, None, defer=True)
@@ -193,7 +200,7 @@ WIDE_TARGET_WGS = int(os.environ.get("DLLM_WIDE_TARGET", "256"))
 
 def wide_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 0) -> int:
     """K slices for gemm_wide: about one workgroup per CU, >= 8 K-tiles (512) per slice."""
-    tiles = (n // 128) * (-(-m // (128 if m <= 128 else 256)))
+    tiles = (n // 128) * (-(-m // (64 if m <= 64 else 128 if m <= 128 else 256)))
     s = max(1, round((target_wgs or WIDE_TARGET_WGS) / tiles))
     return max(1, min(s, (k // 64) // 8, 16))
 
@@ -230,9 +237,9 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor, force_skinny: bool =
     k = x.shape[-1]
     n = w_gate_up.shape[0]
     m = x.numel() // k
+    if not force_skinny and _use_wide(m, n, k, x, w_gate_up, swiglu=True):
+        return linear_wide(x, w_gate_up, swiglu=True)
     if not skinny_ok(m, n, k, x, w_gate_up, swiglu=True, force=force_skinny):
-        if not force_skinny and _use_wide(m, n, k, x, w_gate_up, swiglu=True):
-            return linear_wide(x, w_gate_up, swiglu=True)
         return None
     y = torch.empty(*x.shape[:-1], n // 2, dtype=x.dtype, device=x.device)
     _launch(x, w_gate_up, None, y, m, n, k, 1)
