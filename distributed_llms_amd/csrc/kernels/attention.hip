@@ -25,6 +25,8 @@ constexpr int kBS = 32;       // tokens per KV block (== keys per MFMA chunk)
 // fused decode appends v by rewriting its key group's whole V^T tile (see patch() below)
 constexpr bool kVFullLines = DLLM_VFULL;
 constexpr int kWaves = 4;     // waves per workgroup
+typedef __attribute__((address_space(3))) void* lds_vptr_a;
+typedef __attribute__((address_space(1))) void* glb_vptr_a;
 
 template <int D>
 struct WaveState {
@@ -548,6 +550,153 @@ __global__ void __launch_bounds__(256, NT == 1 ? 2 : 1) attn_prefill2_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Prefill v4 (flash-style, LDS-shared K/V): a workgroup owns kWaves x NT column tiles
+// (kWaves * NT * 16/G query rows x G heads) of one (sequence, kv head) and streams the
+// sequence's K/V chunks ONCE per workgroup through a 3-deep LDS ring filled by LDS-DMA
+// (global_load_lds, 16 B per lane), instead of once per wave as v2 does (a 128-token prompt:
+// 4x fewer K/V reads at NT = 2, 8x at NT = 4).  Per chunk: counted vmcnt for the chunk's own
+// DMA pieces -> raw s_barrier -> every wave reads the chunk's fragments from LDS into the
+// decode kernel's register layout -> refill the buffer all waves finished two chunks ago ->
+// MFMAs (compute_chunk, shared with decode).  K is stored with a 16-B-slot XOR swizzle
+// (slot ^ (row & 15), applied on the DMA source address, guide rule 21) so the K fragment
+// reads are bank-conflict-free; the V^T image is already conflict-free.  Block ids are
+// staged into the same LDS array first (one __shared__ object: guide trap 4a).
+// ---------------------------------------------------------------------------
+constexpr int kPfMaxChunks = 1024;   // 32k context per sequence
+
+template <int D, int G, int NT>
+__global__ void __launch_bounds__(256, NT >= 4 ? 1 : 2) attn_prefill_lds_kernel(
+    bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
+    const int32_t* __restrict__ cu_seqlens_q, const int32_t* __restrict__ seq_lens, int hq, int hkv,
+    int max_blocks, float scale_log2) {
+  constexpr int R = 16 / G;                       // query rows per column tile
+  constexpr int CH = 2 * kBS * D;                 // bf16 elements per staged chunk (K block + V^T block)
+  constexpr int NB = 3;                           // ring depth
+  constexpr int GL = D / 32;                      // LDS-DMA wave-instructions per wave per chunk
+  constexpr int SLOTS = 2 * D / 16;               // 16-B slots per K row
+  constexpr int ROWS_PER_I = 1024 / (2 * D);      // K rows per 1 KiB wave-instruction
+  __shared__ __attribute__((aligned(16))) bf16 smem[NB * CH + 2 * kPfMaxChunks];
+  int* ids = reinterpret_cast<int*>(smem + NB * CH);
+
+  const int kvh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int qs = cu_seqlens_q[b], ql = cu_seqlens_q[b + 1] - qs;
+  const int wg_row0 = blockIdx.x * kWaves * R * NT;
+  if (wg_row0 >= ql) return;                      // workgroup-uniform
+  const int row0 = wg_row0 + w * R * NT;
+  const bool active = row0 < ql;                  // wave-uniform; inactive waves still stage
+  const int ctx = seq_lens[b];
+  const int qpos0 = ctx - ql;
+  bf16x8 qf[NT][D / 32];
+  int kmax_col[NT];
+  WaveState<D> st[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int crow = row0 + t * R + r / G, ch = r % G;
+    const bool ok = crow < ql;
+    kmax_col[t] = ok ? qpos0 + crow : -1;
+    const bf16* qrow = q + ((size_t)(qs + (ok ? crow : 0)) * hq + kvh * G + ch) * D;
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
+      if (!ok) v = bf16x8{};
+      qf[t][ks] = v;
+    }
+    init_state(st[t]);
+  }
+  const int wg_kmax = qpos0 + min(wg_row0 + kWaves * R * NT, ql) - 1;
+  const int nch = wg_kmax / kBS + 1;
+  const int wave_kmax = active ? qpos0 + min(row0 + R * NT, ql) - 1 : -1;
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  for (int i = threadIdx.x; i < nch; i += 256) ids[i] = bt[i];
+  // retire the q and block-id loads before the first LDS-DMA: their uses inside the loop
+  // would otherwise make hipcc wait vmcnt(0) there, draining the ring every chunk
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) asm volatile("" ::"v"(qf[t][ks]));
+  __syncthreads();
+
+  const size_t kv_head_stride = (size_t)kBS * D;
+  const size_t head_off = (size_t)kvh * kv_head_stride;
+  const size_t blk_stride = (size_t)hkv * kv_head_stride;
+  // wave w issues pieces w*GL .. w*GL+GL-1 of the chunk's 2*GL*kWaves/2... (K: pieces 0..D/16-1)
+  auto stage = [&](int c, int buf) {
+    const size_t base = (size_t)ids[c] * blk_stride + head_off;
+    bf16* dst = smem + buf * CH;
+#pragma unroll
+    for (int j = 0; j < GL; ++j) {
+      const int i = w * GL + j;                   // 1 KiB piece of the 2 * 32 * D * 2 B chunk
+      const bf16* src;
+      if (i < D / 16) {                           // K block, swizzled slots
+        const int rr = i * ROWS_PER_I + lane / SLOTS, cs = lane % SLOTS;
+        src = k_cache + base + (size_t)rr * D + (cs ^ (rr & (SLOTS - 1))) * 8;
+      } else {                                    // V^T block, linear
+        src = v_cache + base + (size_t)(i - D / 16) * 512 + lane * 8;
+      }
+      __builtin_amdgcn_global_load_lds((glb_vptr_a)src, (lds_vptr_a)(dst + i * 512), 16, 0, 0);
+    }
+  };
+  auto read = [&](KVChunk<D>& c, int buf) {
+    const bf16* kb = smem + buf * CH;
+    const bf16* vb = kb + kBS * D;
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) {
+      const int cs = ks * 4 + g;
+      c.ka[ks] = *reinterpret_cast<const bf16x8*>(kb + r * D + (cs ^ (r & (SLOTS - 1))) * 8);
+      c.kb[ks] = *reinterpret_cast<const bf16x8*>(kb + (16 + r) * D + (cs ^ ((16 + r) & (SLOTS - 1))) * 8);
+    }
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) c.v[dt] = *reinterpret_cast<const bf16x8*>(vb + g * 8 * D + (dt * 16 + r) * 8);
+  };
+
+  stage(0, 0);
+  if (nch > 1) stage(1, 1);
+  int buf = 0;
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) {
+      if constexpr (GL == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    KVChunk<D> kc;
+    read(kc, buf);
+    // buffer (c + 2) % NB was read in iteration c - 1, which every wave finished before the
+    // barrier above (its fragments were consumed by MFMAs)
+    if (c + 2 < nch) stage(c + 2, buf == 0 ? NB - 1 : buf - 1);
+    if (c * kBS <= wave_kmax) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) compute_chunk<D>(st[t], qf[t], kc, c * kBS, kmax_col[t], scale_log2, lane);
+    }
+    buf = buf == NB - 1 ? 0 : buf + 1;
+  }
+  if (!active) return;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    float lt = st[t].lsum;
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const int crow = row0 + t * R + r / G, ch = r % G;
+    if (crow < ql) {
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      bf16* orow = out + ((size_t)(qs + crow) * hq + kvh * G + ch) * D;
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = f2bf(st[t].acc[dt][i] * inv);
+        *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = o;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ launchers
 static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache, uintptr_t block_tables,
                           uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml, int batch, int hq, int hkv, int d,
@@ -622,13 +771,22 @@ template <int D>
 static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv, hipStream_t s, uintptr_t out,
                            uintptr_t q, uintptr_t k_cache, uintptr_t v_cache, uintptr_t bt, uintptr_t cu, uintptr_t sl,
                            int hq, int max_blocks, float sl2) {
-  // version 1: v1 kernel; 2: v2 with one tile per wave (2 waves/SIMD); 3: v2 with two tiles per wave
-  const int nt = version == 3 ? 2 : 1;
+  // version 1: v1 kernel; 2: v2 with one tile per wave (2 waves/SIMD); 3: v2 with two tiles per wave;
+  // 4 / 5: the LDS-shared kernel with two / four tiles per wave
+  const int nt = version == 5 ? 4 : (version == 3 || version == 4) ? 2 : 1;
   const int rows_per_wg = kWaves * (16 / g) * nt;
   const dim3 grid((max_q_len + rows_per_wg - 1) / rows_per_wg, hkv, batch);
 #define DLLM_PF(GG)                                                                                         \
   do {                                                                                                      \
-    if (version == 3)                                                                                       \
+    if (version == 4)                                                                                       \
+      hipLaunchKernelGGL((attn_prefill_lds_kernel<D, GG, 2>), grid, dim3(256), 0, s, (bf16*)out,              \
+                         (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,      \
+                         (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2);                  \
+    else if (version == 5)                                                                                  \
+      hipLaunchKernelGGL((attn_prefill_lds_kernel<D, GG, 4>), grid, dim3(256), 0, s, (bf16*)out,              \
+                         (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,      \
+                         (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2);                  \
+    else if (version == 3)                                                                                  \
       hipLaunchKernelGGL((attn_prefill2_kernel<D, GG, 2>), grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,  \
                          (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt, (const int32_t*)cu,   \
                          (const int32_t*)sl, hq, hkv, max_blocks, sl2);                                      \
@@ -664,7 +822,11 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float sl2 = scale * 1.4426950408889634f;
   const char* pe = getenv("DLLM_PREFILL_ATTN");   // A/B and tests; eager (prefill) path only
-  const int version = (pe && pe[0] >= '1' && pe[0] <= '3') ? pe[0] - '0' : 3;
+  // default 4: the LDS-shared kernel (bench/prefill_attn_bench.py: 1.6-1.7x v3 from 128- to
+  // 8192-token prompts); 5 = the same at 4 tiles per wave (one wave per SIMD: slower)
+  int version = (pe && pe[0] >= '1' && pe[0] <= '5') ? pe[0] - '0' : 4;
+  // the LDS kernel stages the block ids of a whole sequence: fall back beyond 32k context
+  if (version >= 4 && max_blocks > kPfMaxChunks) version = 3;
   if (d == 128)
     launch_prefill<128>(G, version, max_q_len, batch, hkv, s, out, q, k_cache, v_cache, block_tables, cu_seqlens_q,
                         seq_lens, hq, max_blocks, sl2);
