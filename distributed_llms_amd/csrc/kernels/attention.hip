@@ -565,8 +565,8 @@ __global__ void __launch_bounds__(256, NT == 1 ? 2 : 1) attn_prefill2_kernel(
 // ---------------------------------------------------------------------------
 constexpr int kPfMaxChunks = 1024;   // 32k context per sequence
 
-template <int D, int G, int NT>
-__global__ void __launch_bounds__(256, NT >= 4 ? 1 : 2) attn_prefill_lds_kernel(
+template <int D, int G, int NT, int WV = kWaves>
+__global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefill_lds_kernel(
     bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
     const int32_t* __restrict__ cu_seqlens_q, const int32_t* __restrict__ seq_lens, int hq, int hkv,
@@ -574,7 +574,8 @@ __global__ void __launch_bounds__(256, NT >= 4 ? 1 : 2) attn_prefill_lds_kernel(
   constexpr int R = 16 / G;                       // query rows per column tile
   constexpr int CH = 2 * kBS * D;                 // bf16 elements per staged chunk (K block + V^T block)
   constexpr int NB = 3;                           // ring depth
-  constexpr int GL = D / 32;                      // LDS-DMA wave-instructions per wave per chunk
+  constexpr int GL = D / 8 / WV;                  // LDS-DMA wave-instructions per wave per chunk
+  static_assert(GL >= 1 && GL * WV * 512 == CH, "chunk pieces");
   constexpr int SLOTS = 2 * D / 16;               // 16-B slots per K row
   constexpr int ROWS_PER_I = 1024 / (2 * D);      // K rows per 1 KiB wave-instruction
   __shared__ __attribute__((aligned(16))) bf16 smem[NB * CH + 2 * kPfMaxChunks];
@@ -584,7 +585,7 @@ __global__ void __launch_bounds__(256, NT >= 4 ? 1 : 2) attn_prefill_lds_kernel(
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int qs = cu_seqlens_q[b], ql = cu_seqlens_q[b + 1] - qs;
-  const int wg_row0 = blockIdx.x * kWaves * R * NT;
+  const int wg_row0 = blockIdx.x * WV * R * NT;
   if (wg_row0 >= ql) return;                      // workgroup-uniform
   const int row0 = wg_row0 + w * R * NT;
   const bool active = row0 < ql;                  // wave-uniform; inactive waves still stage
@@ -607,11 +608,11 @@ __global__ void __launch_bounds__(256, NT >= 4 ? 1 : 2) attn_prefill_lds_kernel(
     }
     init_state(st[t]);
   }
-  const int wg_kmax = qpos0 + min(wg_row0 + kWaves * R * NT, ql) - 1;
+  const int wg_kmax = qpos0 + min(wg_row0 + WV * R * NT, ql) - 1;
   const int nch = wg_kmax / kBS + 1;
   const int wave_kmax = active ? qpos0 + min(row0 + R * NT, ql) - 1 : -1;
   const int32_t* bt = block_tables + (size_t)b * max_blocks;
-  for (int i = threadIdx.x; i < nch; i += 256) ids[i] = bt[i];
+  for (int i = threadIdx.x; i < nch; i += WV * 64) ids[i] = bt[i];
   // retire the q and block-id loads before the first LDS-DMA: their uses inside the loop
   // would otherwise make hipcc wait vmcnt(0) there, draining the ring every chunk
 #pragma unroll
@@ -623,7 +624,7 @@ __global__ void __launch_bounds__(256, NT >= 4 ? 1 : 2) attn_prefill_lds_kernel(
   const size_t kv_head_stride = (size_t)kBS * D;
   const size_t head_off = (size_t)kvh * kv_head_stride;
   const size_t blk_stride = (size_t)hkv * kv_head_stride;
-  // wave w issues pieces w*GL .. w*GL+GL-1 of the chunk's 2*GL*kWaves/2... (K: pieces 0..D/16-1)
+  // wave w issues 1 KiB pieces w*GL .. w*GL+GL-1 of the chunk (pieces 0..D/16-1: K, the rest: V^T)
   auto stage = [&](int c, int buf) {
     const size_t base = (size_t)ids[c] * blk_stride + head_off;
     bf16* dst = smem + buf * CH;
@@ -659,7 +660,8 @@ __global__ void __launch_bounds__(256, NT >= 4 ? 1 : 2) attn_prefill_lds_kernel(
   for (int c = 0; c < nch; ++c) {
     if (c + 1 < nch) {
       if constexpr (GL == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if constexpr (GL == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
