@@ -158,16 +158,33 @@ struct RopeArgs {
 };
 
 // 8 consecutive qkv elements starting at row offset `off` of sequence b (bf16 or summed partials).
-// PARTS is a compile-time choice: a runtime branch here split the kernel's prologue into blocks
+// NP (0 = bf16 qkv, > 0 = that many slabs, -1 = runtime count) is a compile-time choice: a runtime
+// branch here split the kernel's prologue into blocks
 // with vmcnt(0) waits at every merge (cold B=256: 48 us vs 40 us without the fused part).
-template <bool PARTS>
+template <int NP>
 __device__ __forceinline__ bf16x8 qkv_load8(const RopeArgs& ra, int b, int width, int off) {
-  if constexpr (!PARTS) return *reinterpret_cast<const bf16x8*>(ra.qkv + (size_t)b * width + off);
+  if constexpr (NP == 0) return *reinterpret_cast<const bf16x8*>(ra.qkv + (size_t)b * width + off);
   const size_t p = (size_t)b * width + off;
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < ra.nparts; ++s) {
-    a0 += part_load4(ra.part, p + s * ra.slab);
-    a1 += part_load4(ra.part, p + s * ra.slab + 4);
+  if constexpr (NP > 0) {
+    // compile-time slab count: all 2 * NP loads in flight before the first add (a runtime loop
+    // waits on each slab in turn: NP dependent round trips in front of the KV stream)
+    f32x4 l0[NP], l1[NP];
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      l0[s] = part_load4(ra.part, p + s * ra.slab);
+      l1[s] = part_load4(ra.part, p + s * ra.slab + 4);
+    }
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {     // slab order as splitk_reduce: bit-identical sums
+      a0 += l0[s];
+      a1 += l1[s];
+    }
+  } else {
+    for (int s = 0; s < ra.nparts; ++s) {
+      a0 += part_load4(ra.part, p + s * ra.slab);
+      a1 += part_load4(ra.part, p + s * ra.slab + 4);
+    }
   }
   bf16x8 o;
 #pragma unroll
@@ -178,12 +195,20 @@ __device__ __forceinline__ bf16x8 qkv_load8(const RopeArgs& ra, int b, int width
   return o;
 }
 
-template <bool PARTS>
+template <int NP>
 __device__ __forceinline__ bf16 qkv_load1(const RopeArgs& ra, int b, int width, int off) {
-  if constexpr (!PARTS) return ra.qkv[(size_t)b * width + off];
+  if constexpr (NP == 0) return ra.qkv[(size_t)b * width + off];
   const size_t p = (size_t)b * width + off;
   float a = 0.f;
-  for (int s = 0; s < ra.nparts; ++s) a += part_load1(ra.part, p + s * ra.slab);
+  if constexpr (NP > 0) {
+    float l[NP];
+#pragma unroll
+    for (int s = 0; s < NP; ++s) l[s] = part_load1(ra.part, p + s * ra.slab);
+#pragma unroll
+    for (int s = 0; s < NP; ++s) a += l[s];
+  } else {
+    for (int s = 0; s < ra.nparts; ++s) a += part_load1(ra.part, p + s * ra.slab);
+  }
   return f2bf(a);
 }
 
@@ -206,7 +231,7 @@ __device__ __forceinline__ void rope_rotate(bf16x8 (&f)[D / 32], const float* cs
   }
 }
 
-template <int D, int WPB, bool FUSED, bool PARTS = false>
+template <int D, int WPB, bool FUSED, int PARTS = 0>
 __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg: min waves per SIMD
     bf16* __restrict__ out, const bf16* __restrict__ q, bf16* __restrict__ k_cache,
     bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
@@ -732,9 +757,14 @@ static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr
   } while (0)
   const bool parts = fused && ra.part != nullptr;
   if (d == 128) {
-    if (parts) DLLM_DEC(128, true, true); else if (fused) DLLM_DEC(128, true, false); else DLLM_DEC(128, false, false);
+    if (parts) {
+      if (ra.nparts == 5) DLLM_DEC(128, true, 5);
+      else if (ra.nparts == 4) DLLM_DEC(128, true, 4);
+      else if (ra.nparts == 8) DLLM_DEC(128, true, 8);
+      else DLLM_DEC(128, true, -1);
+    } else if (fused) DLLM_DEC(128, true, 0); else DLLM_DEC(128, false, 0);
   } else {
-    if (parts) DLLM_DEC(64, true, true); else if (fused) DLLM_DEC(64, true, false); else DLLM_DEC(64, false, false);
+    if (parts) DLLM_DEC(64, true, -1); else if (fused) DLLM_DEC(64, true, 0); else DLLM_DEC(64, false, 0);
   }
 #undef DLLM_DEC
   DLLM_HIP_CHECK(hipGetLastError());
