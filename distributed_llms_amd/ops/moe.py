@@ -59,7 +59,7 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     offsets = torch.empty(e + 1, dtype=torch.int32, device=dev)
     sorted_tok = torch.empty(t * top_k, dtype=torch.int32, device=dev)
     inv = torch.empty(t * top_k, dtype=torch.int32, device=dev)
-    if FUSED_ROUTER and t <= GROUPED_MAX_TOKENS and e in (8, 16) and x.dtype == w_router.dtype == torch.bfloat16 \
+    if FUSED_ROUTER and t <= GROUPED_MAX_TOKENS and e in (8, 16) and h % 32 == 0 and x.dtype == w_router.dtype == torch.bfloat16 \
             and w_router.is_contiguous():
         # decode: router GEMV + softmax/top-k + scatter in two launches (no [T, E] logits round trip)
         k.moe_router_route(x.data_ptr(), w_router.data_ptr(), t, h, e, top_k, topk_w.data_ptr(), topk_ids.data_ptr(),
