@@ -7,7 +7,7 @@
 // (profiles/llama3_8b_b256_kernels_current.md) -- latency-bound at one workgroup per CU.
 //
 // Structure (gfx950, wave64):
-//  * tile BM x 128 x 64 with BM = 256 (or 128 for M <= 128): ALL decode rows in one tile, so
+//  * tile BM x 128 x 64 with BM = 256 (128 for M <= 128, 64 for M <= 64): ALL decode rows in one tile, so
 //    each weight byte leaves HBM once per step; 512 threads = 8 waves in 4 (M) x 2 (N), wave
 //    tile (BM/4) x 64 = (BM/64) x 4 v_mfma_f32_16x16x32_bf16 accumulators;
 //  * global -> LDS with global_load_lds_dwordx4 (lane-linear 1 KiB per wave-instruction =
