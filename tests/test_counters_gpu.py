@@ -2,7 +2,8 @@
 counters on gfx950").  Each runs bench/kernel_counters.py for one kernel under one --pmc pass
 (kernel trace only -- never combined with sys/runtime tracing) and checks a tiling property:
 
-* split-K tiled GEMM: the XOR-swizzled LDS image has no bank conflicts, and MFMAs issue;
+* wide decode GEMM (split-K down projection): the XOR-swizzled LDS image has no bank conflicts,
+  and MFMAs issue;
 * paged decode attention: HBM reads equal the K/V bytes of the batch (no over-fetch).
 """
 import csv
@@ -44,9 +45,9 @@ def _kernel(per, needle):
     return next(iter(hits.values()))
 
 
-def test_tiled_gemm_lds_conflict_free_and_mfma_busy(tmp_path):
+def test_wide_gemm_lds_conflict_free_and_mfma_busy(tmp_path):
     per = _collect(tmp_path, ["SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"], "gemm")
-    for d in _kernel(per, "gemm_tiled_kernel").values():
+    for d in _kernel(per, "gemm_wide_kernel").values():
         assert d["SQ_LDS_IDX_ACTIVE"] > 0
         assert d["SQ_LDS_BANK_CONFLICT"] <= 0.01 * d["SQ_LDS_IDX_ACTIVE"]
         assert d["SQ_VALU_MFMA_BUSY_CYCLES"] > 0
