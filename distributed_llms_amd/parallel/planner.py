@@ -11,9 +11,9 @@ Two granularities:
   blocks), cost = weight bytes (+ the LM head on the last stage);
 * half layers (:func:`plan_units`) -- runtime pipelines: unit 2l = attention half of layer l
   (norm, qkv, RoPE + KV append, attention, o-proj), unit 2l+1 = its MLP half.  Llama-3-8B on 8
-  stages at batch 256 is capped at ~83 % balance by whole-layer cuts (32 layers + an LM head
-  worth ~1.2 layers of time) and at ~95 % by half-layer cuts.  Costs come from a decode time
-  model calibrated on MI355X kernel profiles (profiles/llama3_8b_b256_kernels.md): each GEMM
+  stages at batch 256 is capped at ~80 % balance by whole-layer cuts (32 layers + an LM head
+  worth ~1.35 layers of time) and at ~93 % by half-layer cuts.  Costs come from a decode time
+  model calibrated on MI355X kernel profiles (profiles/llama3_8b_b256_kernels_current.md): each GEMM
   takes max(weight bytes / HBM rate, FLOPs / achieved MFMA rate), attention reads the KV of
   ``ctx`` tokens per sequence, plus fixed per-half elementwise/norm time.
 """
@@ -24,14 +24,16 @@ from typing import List, Optional, Sequence, Tuple
 
 from ..config import ModelConfig
 
-# ---- decode time model (MI355X, bf16, measured on Llama-3-8B at batch 256, ctx ~192)
+# ---- decode time model (MI355X, bf16, wide decode GEMMs; calibrated on the Llama-3-8B batch-256
+# profile, profiles/llama3_8b_b256_kernels_current.md: attention half 100.6 us, MLP half 99.7 us,
+# LM head 254 us + argmax 19 us per step)
 HBM_B_PER_US = 5.0e6          # weight streaming, bytes / us
-KV_B_PER_US = 4.5e6           # attention KV read, bytes / us
-ATTN_GEMM_FLOP_PER_US = 3.4e8 # qkv + o projections at decode M (0.34 PF achieved)
-MLP_GEMM_FLOP_PER_US = 6.9e8  # gate_up + down (0.69 PF)
-HEAD_FLOP_PER_US = 8.4e8      # LM head (0.84 PF)
-ATTN_FIXED_US = 21.0          # RoPE/KV-append + norm kernels
-MLP_FIXED_US = 17.0           # SwiGLU + norm kernels
+KV_B_PER_US = 5.5e6           # attention KV read (nontemporal), bytes / us
+ATTN_GEMM_FLOP_PER_US = 4.0e8 # qkv + o projections at decode M (0.40 PF achieved, split-K)
+MLP_GEMM_FLOP_PER_US = 9.5e8  # gate_up (SwiGLU fused) + down (0.95 PF)
+HEAD_FLOP_PER_US = 9.85e8     # LM head + argmax (0.99 PF)
+ATTN_FIXED_US = 11.4          # qkv split-K reduce + residual/RMSNorm
+MLP_FIXED_US = 6.3            # residual/RMSNorm (SwiGLU is in the GEMM epilogue)
 
 
 @dataclass(frozen=True)
