@@ -34,12 +34,18 @@ class DecodeGraphRunner:
         self.min_ctx_bucket = min_ctx_bucket
         cfg = stage.cfg
         mb, dev = self.max_batch, self.dev
-        self.ids = torch.zeros(mb, dtype=torch.int32, device=dev)
+        # every int32 graph input lives in ONE device buffer laid out like the pinned staging
+        # buffer -- [ids | positions | slots | seq_lens] x max_batch, then the block table rows --
+        # so a step's inputs go up in a single H2D copy (the first 4 * max_batch + bb * max_blocks
+        # ints) instead of five
+        self.dev_in = torch.zeros(4 * mb + mb * max_blocks, dtype=torch.int32, device=dev)
+        self.ids = self.dev_in[0:mb]
+        self.positions = self.dev_in[mb:2 * mb]
+        self.slots = self.dev_in[2 * mb:3 * mb]
+        self.seq_lens = self.dev_in[3 * mb:4 * mb]
+        self.seq_lens.fill_(1)
+        self.block_tables = self.dev_in[4 * mb:].view(mb, max_blocks)
         self.hidden = None if stage.is_first else torch.zeros(mb, cfg.hidden_size, dtype=stage.dtype, device=dev)
-        self.positions = torch.zeros(mb, dtype=torch.int32, device=dev)
-        self.slots = torch.zeros(mb, dtype=torch.int32, device=dev)
-        self.seq_lens = torch.ones(mb, dtype=torch.int32, device=dev)
-        self.block_tables = torch.zeros(mb, max_blocks, dtype=torch.int32, device=dev)
         max_splits = 64
         self.ws = (torch.empty(mb * cfg.num_heads * max_splits * cfg.head_dim, dtype=torch.float32, device=dev),
                    torch.empty(mb * cfg.num_heads * max_splits * 2, dtype=torch.float32, device=dev))
@@ -98,22 +104,19 @@ class DecodeGraphRunner:
         p = self.pinned
         if self.copy_done is not None:
             self.copy_done.synchronize()   # previous step's H2D may still read the pinned buffer
-        n = bb
-        pv = p[: 4 * n].view(4, n)
-        pv.zero_()
-        pv[3].fill_(1)                                  # seq_lens of padded rows = 1
+        n, mb = bb, self.max_batch
+        pv = p[: 4 * mb].view(4, mb)
+        pv[:, :n].zero_()
+        pv[3, :n].fill_(1)                              # seq_lens of padded rows = 1
         pv[0, :b] = torch.from_numpy(hb.ids)
         pv[1, :b] = torch.from_numpy(hb.positions)
         pv[2, :b] = torch.from_numpy(hb.slots)
         pv[3, :b] = torch.from_numpy(hb.seq_lens)
-        bt = p[4 * n: 4 * n + n * self.max_blocks].view(n, self.max_blocks)
+        bt = p[4 * mb: 4 * mb + n * self.max_blocks].view(n, self.max_blocks)
         bt.zero_()
         bt[:b, :mbk] = torch.from_numpy(hb.block_tables)
-        self.ids[:n].copy_(pv[0], non_blocking=True)
-        self.positions[:n].copy_(pv[1], non_blocking=True)
-        self.slots[:n].copy_(pv[2], non_blocking=True)
-        self.seq_lens[:n].copy_(pv[3], non_blocking=True)
-        self.block_tables[:n].copy_(bt, non_blocking=True)
+        cnt = 4 * mb + n * self.max_blocks
+        self.dev_in[:cnt].copy_(p[:cnt], non_blocking=True)
         if self.copy_done is None:
             self.copy_done = torch.cuda.Event()
         self.copy_done.record()
