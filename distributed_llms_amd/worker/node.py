@@ -321,8 +321,15 @@ class WorkerNode:
                     self._enqueue_request(sock, header, payload)
                 else:
                     self._run_stateless(sock, header, payload)
-            elif command == "SCHEDULE_COMPUTATION":
+            elif command in ("SCHEDULE_COMPUTATION", "TASK_ASSIGN"):
+                # TASK_ASSIGN: the reference's declared-only per-task descriptor (protocol.py:19),
+                # served like SCHEDULE_COMPUTATION (shard ids + tensors in, RESULT out)
                 self._run_stateless(sock, header, payload)
+            elif command == "SHARD_REQUEST":
+                # shard migration (the reference declares SHARD_REQUEST but never sends or handles
+                # it, protocol.py:18): hand a resident shard's tensors to the requester as a
+                # LOAD_SHARD it can apply directly (a replacement worker pulls from a peer, not disk)
+                self._send_shard(sock, header)
             elif command == "ABORT":
                 self._abort(header.get("task_id"))
             elif command == "STATUS":
@@ -382,6 +389,17 @@ class WorkerNode:
                 shard = self.shards[sid]
             out = shard.compute(out)
         return out
+
+    def _send_shard(self, sock, header):
+        sid = int(header["shard_id"])
+        with self._lock:
+            shard = self.shards.get(sid)
+        if shard is None:
+            self.proto.send_message(sock, "ERROR", metadata={"shard_id": sid, "error": "shard not resident"})
+            return
+        meta = {"shard_id": sid, "layer_range": list(shard.layer_range) if shard.layer_range else None,
+                "config": shard.config.to_hf_config() if shard.config is not None else None}
+        self.proto.send_message(sock, "LOAD_SHARD", payload=pack_tensors(shard.parameters), metadata=meta)
 
     def _run_stateless(self, sock, header, payload):
         inputs = unpack_tensors(payload) if payload else {}

@@ -112,3 +112,38 @@ def test_peer_tcp_path():
         s.close()
     finally:
         w.stop()
+
+
+def test_shard_request_migrates_a_shard_between_workers():
+    """SHARD_REQUEST (declared but never sent or handled by the reference, protocol.py:18): a
+    replacement worker pulls a resident shard from a peer and computes the same result;
+    TASK_ASSIGN runs like SCHEDULE_COMPUTATION."""
+    a, b = WorkerNode(device="cpu", port=0), WorkerNode(device="cpu", port=0)
+    a.start(block=False)
+    b.start(block=False)
+    try:
+        sa = socket.create_connection(("127.0.0.1", a.port), timeout=30)
+        MessageProtocol.send_message(sa, "LOAD_SHARD", pack_tensors(_shard_params({0, 1, 2, 3})),
+                                     {"shard_id": 0, "config": CFG.to_hf_config(), "layer_range": [0, 4]})
+        assert MessageProtocol.receive_message(sa, timeout=60)[0]["command"] == "SHARD_LOADED"
+        MessageProtocol.send_message(sa, "SHARD_REQUEST", metadata={"shard_id": 0})
+        h, blob = MessageProtocol.receive_message(sa, timeout=60)
+        assert h["command"] == "LOAD_SHARD" and h["layer_range"] == [0, 4] and blob
+        MessageProtocol.send_message(sa, "SHARD_REQUEST", metadata={"shard_id": 7})
+        assert MessageProtocol.receive_message(sa, timeout=30)[0]["command"] == "ERROR"
+        sb = socket.create_connection(("127.0.0.1", b.port), timeout=30)
+        MessageProtocol.send_message(sb, "LOAD_SHARD", blob, {k: h[k] for k in ("shard_id", "config", "layer_range")})
+        assert MessageProtocol.receive_message(sb, timeout=60)[0]["command"] == "SHARD_LOADED"
+        x = pack_tensors({"input_ids": torch.tensor([[5, 6, 7]])})
+        outs = []
+        for s, cmd in ((sa, "SCHEDULE_COMPUTATION"), (sb, "TASK_ASSIGN")):
+            MessageProtocol.send_message(s, cmd, x, {"task_id": cmd, "shard_ids": [0]})
+            hh, p = MessageProtocol.receive_message(s, timeout=60)
+            assert hh["command"] == "RESULT" and hh["task_id"] == cmd
+            outs.append(unpack_tensors(p)["logits"])
+        torch.testing.assert_close(outs[0], outs[1])
+        sa.close()
+        sb.close()
+    finally:
+        a.stop()
+        b.stop()
