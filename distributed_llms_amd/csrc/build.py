@@ -110,6 +110,23 @@ def build_runtime(force=False, jobs=8, verbose=False) -> str:
     return target
 
 
+def build_runtime_sanitized(out_dir: str) -> str:
+    """The host runtime (``_C_runtime``: block manager, frame codec) built with UBSan
+    (-fsanitize=undefined, no recovery, runtime linked statically so the module loads into a plain
+    interpreter) and libstdc++ assertions (container bounds) -- SURVEY §5.2's sanitizer build.
+    ASan would need the interpreter started with libasan preloaded; UBSan + _GLIBCXX_ASSERTIONS
+    catch out-of-bounds indexing, overflow and misaligned access in-process.  Returns the .so path
+    (import it under the name ``distributed_llms_amd._C_runtime``)."""
+    src_dir = os.path.join(HERE, "runtime")
+    os.makedirs(out_dir, exist_ok=True)
+    target = os.path.join(out_dir, os.path.basename(_ext_path("_C_runtime")))
+    _run([CXX, "-shared", "-fPIC", "-O1", "-g", "-std=c++17", "-fvisibility=hidden",
+          "-fsanitize=undefined", "-fno-sanitize-recover=undefined", "-static-libubsan", "-D_GLIBCXX_ASSERTIONS",
+          *[f"-I{p}" for p in _py_includes()], f"-I{src_dir}",
+          *sorted(glob.glob(os.path.join(src_dir, "*.cpp"))), "-o", target])
+    return target
+
+
 def build_comm(force=False, jobs=8, verbose=False) -> str:
     src = os.path.join(HERE, "comm", "rccl_p2p.cpp")
     out_dir = os.path.join(BUILD, "comm")
