@@ -51,12 +51,14 @@ __device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ ((row >
 // wait until at most `younger` tiles of G LDS-DMA instructions each are still in flight
 template <int G>
 __device__ __forceinline__ void wait_tiles(int younger) {
-  static_assert(G == 3 || G == 4 || G == 6, "G");
+  static_assert(G == 3 || G == 4 || G == 5 || G == 6, "G");
   if (younger <= 0) { DLLM_VM(0); return; }
   if constexpr (G == 3) {
     if (younger == 1) DLLM_VM(3); else if (younger == 2) DLLM_VM(6); else DLLM_VM(9);
   } else if constexpr (G == 4) {
     if (younger == 1) DLLM_VM(4); else if (younger == 2) DLLM_VM(8); else DLLM_VM(12);
+  } else if constexpr (G == 5) {
+    if (younger == 1) DLLM_VM(5); else if (younger == 2) DLLM_VM(10); else DLLM_VM(15);
   } else {
     if (younger == 1) DLLM_VM(6); else if (younger == 2) DLLM_VM(12); else DLLM_VM(18);
   }
@@ -362,6 +364,15 @@ void moe_wide_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uint
   DLLM_HIP_CHECK(hipGetLastError());
 }
 
+static int wide_bm(int M) {
+  if (M <= 64) return 64;
+  if (M <= 128) return 128;
+  if (M <= 192) return 192;
+  if (M <= 256) return 256;
+  if (M <= 384) return 192;
+  return 256;
+}
+
 // mode 0: C = A B^T;  mode 1: SwiGLU, C[M, N/2] = silu(A Bg^T) * (A Bu^T) with B = [Bg; Bu];
 // mode 2: leave split-K partial slabs in ws (no reduce; S > 1 required).
 // Returns the effective number of K slices S (the partial slabs a deferred reduce must sum).
@@ -378,7 +389,9 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   const int kts = (ktiles + splits - 1) / splits;
   const int S = (ktiles + kts - 1) / kts;
   DLLM_HOST_CHECK(mode != 2 || S > 1, "mode 2 needs a K split");
-  const int BM = M <= 64 ? 64 : M <= 128 ? 128 : 256;
+  // row tile: the smallest of 64 / 128 / 192 / 256 that covers M, or 192 for 256 < M <= 384
+  // (two 192-row tiles instead of a half-empty second 256-row tile)
+  const int BM = wide_bm(M);
   const int mtiles = (M + BM - 1) / BM;
   const int ntiles = swiglu ? (N / 2) / 64 : N / WBN;
   const long grid = (long)ntiles * mtiles * S;
@@ -403,12 +416,14 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   if (S == 1) {
     if (BM == 64) { if (swiglu) DLLM_WIDE_GO(64, false, true); else DLLM_WIDE_GO(64, false, false); }
     else if (BM == 128) { if (swiglu) DLLM_WIDE_GO(128, false, true); else DLLM_WIDE_GO(128, false, false); }
+    else if (BM == 192) { if (swiglu) DLLM_WIDE_GO(192, false, true); else DLLM_WIDE_GO(192, false, false); }
     else { if (swiglu) DLLM_WIDE_GO(256, false, true); else DLLM_WIDE_GO(256, false, false); }
     DLLM_HIP_CHECK(hipGetLastError());
     return 1;
   }
   if (BM == 64) { if (swiglu) DLLM_WIDE_GO(64, true, true); else DLLM_WIDE_GO(64, true, false); }
   else if (BM == 128) { if (swiglu) DLLM_WIDE_GO(128, true, true); else DLLM_WIDE_GO(128, true, false); }
+  else if (BM == 192) { if (swiglu) DLLM_WIDE_GO(192, true, true); else DLLM_WIDE_GO(192, true, false); }
   else { if (swiglu) DLLM_WIDE_GO(256, true, true); else DLLM_WIDE_GO(256, true, false); }
 #undef DLLM_WIDE_GO
 #undef DLLM_WIDE_GO3

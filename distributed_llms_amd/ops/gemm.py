@@ -198,9 +198,22 @@ def linear_tiled(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
 WIDE_TARGET_WGS = int(os.environ.get("DLLM_WIDE_TARGET", "256"))
 
 
+def wide_bm(m: int) -> int:
+    """Row tile of gemm_wide for M rows (mirrors wide_bm in csrc/kernels/gemm_wide.hip)."""
+    if m <= 64:
+        return 64
+    if m <= 128:
+        return 128
+    if m <= 192:
+        return 192
+    if m <= 256:
+        return 256
+    return 192 if m <= 384 else 256
+
+
 def wide_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 0) -> int:
     """K slices for gemm_wide: about one workgroup per CU, >= 8 K-tiles (512) per slice."""
-    tiles = (n // 128) * (-(-m // (64 if m <= 64 else 128 if m <= 128 else 256)))
+    tiles = (n // 128) * (-(-m // wide_bm(m)))
     s = max(1, round((target_wgs or WIDE_TARGET_WGS) / tiles))
     return max(1, min(s, (k // 64) // 8, 16))
 
