@@ -384,6 +384,11 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   const bool swiglu = mode == 1;
   DLLM_HOST_CHECK(swiglu ? (N % 128 == 0) : (N % WBN == 0), "N must be a multiple of 128");
   DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
+  // variant bits 8..: optional row tile override (64 / 128 / 192 / 256), 0 = wide_bm(M)
+  const int bm_force = variant >> 8;
+  variant &= 0xff;
+  DLLM_HOST_CHECK(bm_force == 0 || bm_force == 64 || bm_force == 128 || bm_force == 192 || bm_force == 256,
+                  "row tile override must be 64, 128, 192 or 256");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ktiles = K / WBK;
   const int kts = (ktiles + splits - 1) / splits;
@@ -391,7 +396,7 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   DLLM_HOST_CHECK(mode != 2 || S > 1, "mode 2 needs a K split");
   // row tile: the smallest of 64 / 128 / 192 / 256 that covers M, or 192 for 256 < M <= 384
   // (two 192-row tiles instead of a half-empty second 256-row tile)
-  const int BM = wide_bm(M);
+  const int BM = bm_force ? bm_force : wide_bm(M);
   const int mtiles = (M + BM - 1) / BM;
   const int ntiles = swiglu ? (N / 2) / 64 : N / WBN;
   const long grid = (long)ntiles * mtiles * S;

@@ -211,9 +211,23 @@ def wide_bm(m: int) -> int:
     return 192 if m <= 384 else 256
 
 
+# Row tile override for split-K (non-SwiGLU) wide GEMMs with at most WIDE_SMALL_BM_MAXW weight
+# elements: e.g. DLLM_WIDE_SMALL_BM=128 runs an M = 256 o-projection as 2 row tiles x 4 K slices
+# instead of 1 x 8 (half the split-K slab bytes, 2/3 of the per-CU staging bytes per K-tile).
+WIDE_SMALL_BM = int(os.environ.get("DLLM_WIDE_SMALL_BM", "0"))
+WIDE_SMALL_BM_MAXW = int(os.environ.get("DLLM_WIDE_SMALL_BM_MAXW", str(4096 * 4096)))
+
+
+def wide_row_tile(m: int, n: int, k: int, swiglu: bool = False) -> int:
+    """Row tile gemm_wide uses for this shape (the override, else wide_bm)."""
+    if WIDE_SMALL_BM and not swiglu and n * k <= WIDE_SMALL_BM_MAXW and WIDE_SMALL_BM < wide_bm(m):
+        return WIDE_SMALL_BM
+    return wide_bm(m)
+
+
 def wide_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 0) -> int:
     """K slices for gemm_wide: about one workgroup per CU, >= 8 K-tiles (512) per slice."""
-    tiles = (n // 128) * (-(-m // wide_bm(m)))
+    tiles = (n // 128) * (-(-m // wide_row_tile(m, n, k, swiglu)))
     s = max(1, round((target_wgs or WIDE_TARGET_WGS) / tiles))
     return max(1, min(s, (k // 64) // 8, 16))
 
@@ -236,6 +250,9 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
         s = max(1, ws.numel() // (m * n))
     stream = torch.cuda.current_stream().cuda_stream
     v = WIDE_VARIANT if variant < 0 else variant
+    bm = wide_row_tile(m, n, k, swiglu)
+    if bm != wide_bm(m):
+        v |= bm << 8
     if defer and not swiglu and s > 1:
         se = _ext.kernels().gemm_wide(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, v, stream)
         return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)

@@ -161,3 +161,23 @@ def test_wide_deferred_splitk_matches_materialized(cuda):
     assert isinstance(p, gemm.SplitKPartial) and p.splits == 8
     y = p.materialize()
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("bm", [64, 128, 192])
+@pytest.mark.parametrize("m", [100, 256, 384])
+def test_wide_row_tile_override(cuda, bm, m):
+    """gemm_wide with a forced smaller row tile (variant bits 8.., what DLLM_WIDE_SMALL_BM selects):
+    several M tiles per N tile, plain and deferred split-K."""
+    from distributed_llms_amd import _ext
+    x, w = _bf(m, 4096), _bf(4096, 4096, scale=0.05)
+    ref = x.float() @ w.float().t()
+    y = torch.empty(m, 4096, dtype=torch.bfloat16, device="cuda")
+    ws = gemm._workspace(x.device)
+    stream = torch.cuda.current_stream().cuda_stream
+    _ext.kernels().gemm_wide(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, 4096, 4096, 4,
+                             0, 1 | (bm << 8), stream)
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+    s = _ext.kernels().gemm_wide(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, 4096, 4096, 4, 2,
+                                 1 | (bm << 8), stream)
+    p = gemm.SplitKPartial(ws, s, m, 4096, (m, 4096), x.dtype, x.device)
+    torch.testing.assert_close(p.materialize().float(), ref, atol=3e-2, rtol=3e-2)
