@@ -75,7 +75,8 @@ def _use_tiled(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool
 #   comma list of gate_up (SwiGLU-fused MLP up projection), down (K >= 8192, deferred split-K),
 #   proj (the other projections: qkv, o), all, or none.  Default "auto", from the in-engine A/B
 #   (scripts/gpu_ab_wide.sh, profiles/wide_gemm.md): gate_up + down for M <= 512 (+4.3 % at
-#   B=256, +5.8 % at B=128, +1.2 % at B=512), proj only up to M = 256 (it loses at 512).
+#   B=256, +5.8 % at B=128, +1.2 % at B=512), proj only up to M = 256 (it loses at 512), gate_up
+#   only up to M = 256 (DLLM_WIDE_GATE_UP_MAX_M: hipBLASLt + silu_mul is +1.9 % at B=384, +2.5 % at 512).
 WIDE = {t for t in os.environ.get("DLLM_WIDE", "auto").split(",") if t and t != "none"}
 WIDE_VARIANT = int(os.environ.get("DLLM_WIDE_VARIANT", "1"))
 
@@ -83,6 +84,9 @@ WIDE_VARIANT = int(os.environ.get("DLLM_WIDE_VARIANT", "1"))
 # smallest M the wide kernel serves (1: every decode batch; the 64-row tile at M <= 64 streams
 # the weights at 4.5-6.4 TB/s, +15-19 % tok/s over skinny / hipBLASLt at B = 1..64)
 WIDE_MIN_M = int(os.environ.get("DLLM_WIDE_MIN_M", "1"))
+# largest M the SwiGLU-fused gate|up projection runs on the wide kernel under "auto" (above it:
+# hipBLASLt + silu_mul); profiles/wide_gemm.md "gate|up tile / split / cutover"
+WIDE_GATE_UP_MAX_M = int(os.environ.get("DLLM_WIDE_GATE_UP_MAX_M", "256"))
 
 
 def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
@@ -93,7 +97,7 @@ def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: 
     if "all" in WIDE:
         return True
     if "auto" in WIDE:
-        return swiglu or k >= 8192 or m <= 256
+        return (m <= WIDE_GATE_UP_MAX_M) if swiglu else (k >= 8192 or m <= 256)
     if swiglu:
         return "gate_up" in WIDE
     return ("down" in WIDE) if k >= 8192 else ("proj" in WIDE)
