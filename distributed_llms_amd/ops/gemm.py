@@ -87,6 +87,8 @@ WIDE_MIN_M = int(os.environ.get("DLLM_WIDE_MIN_M", "1"))
 # largest M the SwiGLU-fused gate|up projection runs on the wide kernel under "auto" (above it:
 # hipBLASLt + silu_mul); profiles/wide_gemm.md "gate|up tile / split / cutover"
 WIDE_GATE_UP_MAX_M = int(os.environ.get("DLLM_WIDE_GATE_UP_MAX_M", "256"))
+# same for the K >= 8192 (MLP down) projection, whose split-K output defers into the next norm
+WIDE_DOWN_MAX_M = int(os.environ.get("DLLM_WIDE_DOWN_MAX_M", "512"))
 
 
 def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
@@ -97,7 +99,9 @@ def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: 
     if "all" in WIDE:
         return True
     if "auto" in WIDE:
-        return (m <= WIDE_GATE_UP_MAX_M) if swiglu else (k >= 8192 or m <= 256)
+        if swiglu:
+            return m <= WIDE_GATE_UP_MAX_M
+        return m <= WIDE_DOWN_MAX_M if k >= 8192 else m <= 256
     if swiglu:
         return "gate_up" in WIDE
     return ("down" in WIDE) if k >= 8192 else ("proj" in WIDE)
