@@ -89,6 +89,8 @@ WIDE_MIN_M = int(os.environ.get("DLLM_WIDE_MIN_M", "1"))
 WIDE_GATE_UP_MAX_M = int(os.environ.get("DLLM_WIDE_GATE_UP_MAX_M", "256"))
 # same for the K >= 8192 (MLP down) projection, whose split-K output defers into the next norm
 WIDE_DOWN_MAX_M = int(os.environ.get("DLLM_WIDE_DOWN_MAX_M", "512"))
+# and for the other projections (qkv, o)
+WIDE_PROJ_MAX_M = int(os.environ.get("DLLM_WIDE_PROJ_MAX_M", "256"))
 
 
 def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
@@ -101,7 +103,7 @@ def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: 
     if "auto" in WIDE:
         if swiglu:
             return m <= WIDE_GATE_UP_MAX_M
-        return m <= WIDE_DOWN_MAX_M if k >= 8192 else m <= 256
+        return m <= (WIDE_DOWN_MAX_M if k >= 8192 else WIDE_PROJ_MAX_M)
     if swiglu:
         return "gate_up" in WIDE
     return ("down" in WIDE) if k >= 8192 else ("proj" in WIDE)
