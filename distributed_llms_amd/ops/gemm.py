@@ -94,19 +94,19 @@ WIDE_PROJ_MAX_M = int(os.environ.get("DLLM_WIDE_PROJ_MAX_M", "256"))
 
 
 def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
-    if not WIDE or GEMM_MODE == "blas" or not (WIDE_MIN_M <= m <= 512) or n % 128 or k % 64:
+    if not WIDE or GEMM_MODE == "blas" or not (WIDE_MIN_M <= m <= max(512, WIDE_DOWN_MAX_M)) or n % 128 or k % 64:
         return False
     if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
         return False
     if "all" in WIDE:
-        return True
+        return m <= 512 or (k >= 8192 and not swiglu and m <= WIDE_DOWN_MAX_M)
     if "auto" in WIDE:
         if swiglu:
             return m <= WIDE_GATE_UP_MAX_M
         return m <= (WIDE_DOWN_MAX_M if k >= 8192 else WIDE_PROJ_MAX_M)
     if swiglu:
-        return "gate_up" in WIDE
-    return ("down" in WIDE) if k >= 8192 else ("proj" in WIDE)
+        return "gate_up" in WIDE and m <= 512
+    return ("down" in WIDE) if k >= 8192 else ("proj" in WIDE and m <= 512)
 
 
 class SplitKPartial:
