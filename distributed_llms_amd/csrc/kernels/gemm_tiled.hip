@@ -179,8 +179,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16* __restrict__ o
 // Bit-identical to splitk_reduce_kernel followed by rms_norm_kernel with a residual (same
 // per-element summation order, same thread -> vector mapping for the sum of squares), minus one
 // launch and the bf16 h round trip through HBM.  One 256-thread workgroup per row.
-template <int MAXV, int SC>
-__global__ void __launch_bounds__(256) splitk_add_rms_norm_kernel(bf16* __restrict__ y, bf16* __restrict__ residual,
+template <int MAXV, int SC, int NTH = 256>
+__global__ void __launch_bounds__(NTH) splitk_add_rms_norm_kernel(bf16* __restrict__ y, bf16* __restrict__ residual,
                                                                   const float* __restrict__ P, int S_, int M, int N,
                                                                   const bf16* __restrict__ w, float eps) {
   // SC > 0: the slab count is a compile-time constant, so all of a vector's 2*SC slab loads are
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(256) splitk_add_rms_norm_kernel(bf16* __restri
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int idx = threadIdx.x + i * 256;
+    const int idx = threadIdx.x + i * NTH;
     if (idx < nvec) {
       const size_t p = (size_t)row * N + idx * 8;
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(256) splitk_add_rms_norm_kernel(bf16* __restri
   bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)row * N);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int idx = threadIdx.x + i * 256;
+    const int idx = threadIdx.x + i * NTH;
     if (idx < nvec) {
       const bf16x8 g = wv[idx];
       bf16x8 o;
@@ -255,11 +255,24 @@ void splitk_add_rms_norm(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, i
   DLLM_HOST_CHECK(S >= 1 && M >= 0, "S >= 1");
   if (M == 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // DLLM_SKN_THREADS=512: 512-thread workgroups (8 waves per row, one vector per thread at hidden
+  // 4096); the sum of squares is then reduced over 8 wave partials, so the output is no longer
+  // bit-identical to splitk_reduce + rms_norm_kernel (A/B knob, profiles/wide_gemm.md)
+  static const int nth = [] {
+    const char* e = getenv("DLLM_SKN_THREADS");
+    return e && atoi(e) == 512 ? 512 : 256;
+  }();
+  const int nvec = N / 8;
+  const int bth = (nth == 512 && nvec > 256 && nvec <= 512 && S == 8) ? 512 : 256;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(M), dim3(256), 0, s, (bf16*)y, (bf16*)residual, (const float*)ws, S, M, N,
+    hipLaunchKernelGGL(kern, dim3(M), dim3(bth), 0, s, (bf16*)y, (bf16*)residual, (const float*)ws, S, M, N,
                        (const bf16*)w, eps);
   };
-  const int nvec = N / 8;
+  if (bth == 512) {
+    go(splitk_add_rms_norm_kernel<1, 8, 512>);
+    DLLM_HIP_CHECK(hipGetLastError());
+    return;
+  }
   static const bool const_slabs = [] {
     const char* e = getenv("DLLM_SKN_CONST");
     return !(e && e[0] == '0');
