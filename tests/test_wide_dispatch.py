@@ -1,0 +1,53 @@
+"""Decode GEMM routing between the wide-M HIP kernel (csrc/kernels/gemm_wide.hip) and hipBLASLt.
+
+The cutovers are measured in-engine (profiles/wide_gemm.md): gate|up (SwiGLU) and qkv / o on the
+wide kernel up to M = 256, the K >= 8192 down projection up to M = 512.  CPU-only: `_use_wide` is
+pure shape / dtype logic."""
+import pytest
+import torch
+
+from distributed_llms_amd.ops import gemm
+
+
+def _xw(m, n, k):
+    return torch.empty(m, k, dtype=torch.bfloat16), torch.empty(n, k, dtype=torch.bfloat16)
+
+
+@pytest.fixture(autouse=True)
+def _defaults(monkeypatch):
+    monkeypatch.setattr(gemm, "WIDE", {"auto"})
+    monkeypatch.setattr(gemm, "GEMM_MODE", "auto")
+    monkeypatch.setattr(gemm, "WIDE_MIN_M", 1)
+
+
+@pytest.mark.parametrize("m,expect", [(1, True), (64, True), (256, True), (257, False), (384, False), (512, False)])
+def test_gate_up_cutover(m, expect):
+    x, w = _xw(m, 2 * 14336, 4096)
+    assert gemm._use_wide(m, w.shape[0], 4096, x, w, swiglu=True) is expect
+
+
+@pytest.mark.parametrize("m,expect", [(1, True), (256, True), (384, True), (512, True), (513, False), (768, False)])
+def test_down_cutover(m, expect):
+    x, w = _xw(m, 4096, 14336)
+    assert gemm._use_wide(m, 4096, 14336, x, w) is expect
+
+
+@pytest.mark.parametrize("m,expect", [(16, True), (256, True), (257, False), (384, False)])
+def test_proj_cutover(m, expect):
+    x, w = _xw(m, 6144, 4096)
+    assert gemm._use_wide(m, 6144, 4096, x, w) is expect
+
+
+def test_down_cap_can_exceed_512(monkeypatch):
+    monkeypatch.setattr(gemm, "WIDE_DOWN_MAX_M", 768)
+    x, w = _xw(768, 4096, 14336)
+    assert gemm._use_wide(768, 4096, 14336, x, w)
+    xg, wg = _xw(768, 2 * 14336, 4096)
+    assert not gemm._use_wide(768, wg.shape[0], 4096, xg, wg, swiglu=True)
+
+
+def test_blas_mode_and_dtype_disable_wide(monkeypatch):
+    x, w = _xw(128, 4096, 4096)
+    assert not gemm._use_wide(128, 4096, 4096, x.float(), w.float())
+    monkeypatch.setattr(gemm, "GEMM_MODE", "blas")
+    assert not gemm._use_wide(128, 4096, 4096, x, w)
