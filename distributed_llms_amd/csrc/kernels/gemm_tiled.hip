@@ -257,7 +257,10 @@ void splitk_add_rms_norm(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, i
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // DLLM_SKN_THREADS=512: 512-thread workgroups (8 waves per row, one vector per thread at hidden
   // 4096); the sum of squares is then reduced over 8 wave partials, so the output is no longer
-  // bit-identical to splitk_reduce + rms_norm_kernel (A/B knob, profiles/wide_gemm.md)
+  // bit-identical to splitk_reduce + rms_norm_kernel (A/B knob, profiles/wide_gemm.md).  Only
+  // instantiated for S == 8 slabs and 2048 < hidden <= 4096 (256 < N/8 <= 512); every other shape
+  // keeps the 256-thread kernel.  Read once per process (first call).
+  // tests/test_gemm_gpu.py::test_skn_512_threads covers it in a subprocess.
   static const int nth = [] {
     const char* e = getenv("DLLM_SKN_THREADS");
     return e && atoi(e) == 512 ? 512 : 256;

@@ -6,7 +6,7 @@ uploads into its :class:`BatchMeta` device tensors.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -33,6 +33,9 @@ class HostBatch:
     slot: int = 0
     step_id: int = 0
     sampling: Optional[np.ndarray] = None   # [B, 3] int32: temperature*1e4, top_k, top_p*1e4 (None = greedy)
+    # the packed array this batch was unpacked from (its fields are views into it): pack() then
+    # only refreshes the header instead of concatenating everything again
+    raw: Optional[np.ndarray] = field(default=None, repr=False, compare=False)
 
     @property
     def num_tokens(self) -> int:
@@ -45,6 +48,10 @@ class HostBatch:
     # ------------------------------------------------------ wire format
     def pack(self) -> np.ndarray:
         """Flatten to one int32 array: [header(16) | fields...]."""
+        if self.raw is not None:
+            self.raw[6] = self.slot
+            self.raw[7] = self.step_id
+            return self.raw
         b, t = self.num_seqs, self.num_tokens
         mb = self.block_tables.shape[1] if self.block_tables.ndim == 2 else 0
         has_s = 1 if self.sampling is not None else 0
@@ -78,7 +85,7 @@ class HostBatch:
         bt = take(b * mb).reshape(b, mb)
         lidx = take(b)
         samp = take(3 * b).reshape(b, 3) if has_s else None
-        return HostBatch(bool(pf), ids, pos, slots, seq_lens, cu, bt, lidx, mq, mc, slot, sid, samp)
+        return HostBatch(bool(pf), ids, pos, slots, seq_lens, cu, bt, lidx, mq, mc, slot, sid, samp, raw=arr)
 
 
 def next_pow2(x: int, lo: int = 1) -> int:
@@ -90,6 +97,11 @@ def next_pow2(x: int, lo: int = 1) -> int:
 
 def build_host_batch(step: Step, bm, block_size: int, max_blocks: Optional[int] = None,
                      step_id: int = 0) -> HostBatch:
+    """Metadata of one step.  Decode steps of the native batcher arrive packed already (their
+    block-table width is the scheduler's ``max_blocks``); only the step id is stamped here."""
+    if step.packed is not None:
+        step.packed[7] = step_id
+        return HostBatch.unpack(step.packed)
     seqs = step.seqs
     b = len(seqs)
     seq_ids = np.fromiter((s.seq_id for s in seqs), dtype=np.int64, count=b)

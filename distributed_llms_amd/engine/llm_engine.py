@@ -19,10 +19,10 @@ import torch
 from .. import _ext
 from ..config import EngineConfig, resolve_device, torch_dtype
 from ..models.stage import ModelStage
-from .batch import build_decode_batch, build_host_batch
+from .batch import build_host_batch
 from .graphs import SCRATCH_SEQ_ID
 from .runner import StageRunner
-from .sampler import sample, step_sampling_args
+from .sampler import sample
 from .scheduler import Scheduler, Step
 from .sequence import SamplingParams, Sequence
 
@@ -112,7 +112,7 @@ class LLMEngine:
         """Synchronous execution of one step (CPU path / tests)."""
         hb = self._host_batch(step)
         logits = self.runner.execute(hb, slot=step.slot)
-        ids = sample(logits, **step_sampling_args(step.seqs))
+        ids = sample(logits, **hb.sampling_args())
         return ids.cpu().tolist()
 
     def _launch(self, step: Step, hb, slot: int, ids_src: Optional[torch.Tensor] = None, keep=None):
@@ -127,9 +127,10 @@ class LLMEngine:
             ids_dev = None
             if ids_src is not None:
                 ids_dev = ids_src if keep is None else ids_src.index_select(
-                    0, torch.tensor(keep, dtype=torch.int64).pin_memory().to(ids_src.device, non_blocking=True))
+                    0, torch.from_numpy(np.asarray(keep, dtype=np.int64)).pin_memory().to(ids_src.device,
+                                                                                          non_blocking=True))
             logits = self.runner.execute(hb, slot=slot, ids_dev=ids_dev)
-            ids = sample(logits, **step_sampling_args(step.seqs))
+            ids = sample(logits, **hb.sampling_args())
             n = ids.shape[0]
             self.tok_host[slot][i][:n].copy_(ids, non_blocking=True)
             self.events[slot][i].record(s)
@@ -155,36 +156,18 @@ class LLMEngine:
         prev, pslot, pn, _, pids = self.inflight[-1]
         if pslot != slot or prev.is_prefill or len(self.inflight) > 1:
             return False
-        sch = self.scheduler
-        keep, lens = [], []
-        for j, seq in enumerate(prev.seqs):
-            if seq.finished:
-                continue
-            total = len(seq.prompt) + len(seq.output) + 1        # after the in-flight step
-            if len(seq.output) + 1 >= seq.params.max_new_tokens or total >= sch.max_seq_len:
-                continue                                        # finishes by length there
-            keep.append(j)
-            lens.append(total)
-        if not keep:
+        step = self.scheduler.schedule_lookahead(slot)      # native: rows, packed metadata, keep
+        if step is None:
             return False
-        seqs = [prev.seqs[j] for j in keep]
-        seq_ids = np.fromiter((q.seq_id for q in seqs), dtype=np.int64, count=len(seqs))
-        lens_a = np.asarray(lens, dtype=np.int64)
-        if self.bm.ensure_capacity_batch(seq_ids, lens_a) >= 0:
-            return False
-        step = Step(False, seqs, slot)
-        hb = build_decode_batch(seq_ids, lens_a.astype(np.int32), self.bm, self.ecfg.kv_block_size,
-                                self.runner.max_blocks, self.step_id, slot)
-        self.step_id += 1
-        self.num_decode_tokens += len(seqs)
-        self._launch(step, hb, slot, ids_src=pids[:pn], keep=None if len(keep) == pn else keep)
+        hb = self._host_batch(step)
+        self._launch(step, hb, slot, ids_src=pids[:pn], keep=step.keep)
         self.num_lookahead += 1
         return True
 
     def _complete_oldest(self):
         step, slot, n, i, _ = self.inflight.popleft()
         self.events[slot][i].synchronize()
-        self.scheduler.complete(step, self.tok_host[slot][i][:n].tolist(), time.perf_counter())
+        self.scheduler.complete(step, self.tok_host[slot][i][:n].numpy(), time.perf_counter())
         self.busy[slot] = any(e[1] == slot for e in self.inflight)
 
     def step(self) -> List[Sequence]:

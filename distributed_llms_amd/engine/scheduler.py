@@ -7,34 +7,71 @@ microbatch in flight); each call to :meth:`schedule` for a slot returns either a
 prefill step (admitting waiting requests, bounded by ``max_prefill_tokens`` and free KV
 blocks) or a decode step over the slot's running sequences.  KV blocks come from the
 native :class:`BlockManager`; when a decode step cannot grow a sequence the youngest
-running sequence of that slot is preempted (blocks freed, recomputed later).
+running sequence of that slot is preempted (blocks freed, recomputed later).  The decode
+bookkeeping is native (csrc/runtime/slot_batcher.cpp): at batch 256 a decode microbatch costs
+the driver two C++ calls instead of ~0.9 ms of per-sequence Python (bench/host_overhead.py).
 """
 from __future__ import annotations
 
 import collections
 import time
-from dataclasses import dataclass
 from typing import Deque, Dict, List, Optional
 
 import numpy as np
 
+from .. import _ext
 from .sequence import Sequence, SeqStatus
 
 
-@dataclass
 class Step:
-    is_prefill: bool
-    seqs: List[Sequence]
-    slot: int = 0
+    """One microbatch: a prefill over ``seqs`` or a decode step.  Decode steps from the native
+    batcher carry their sequence ids (``rows``), the packed batch metadata (``packed``, the
+    HostBatch wire format) and, for lookahead steps, ``keep`` (positions of the rows in the slot's
+    previous step); ``seqs`` is then resolved lazily from the scheduler's registry."""
+
+    __slots__ = ("is_prefill", "_seqs", "slot", "rows", "packed", "keep", "_live")
+
+    def __init__(self, is_prefill: bool, seqs: Optional[List[Sequence]] = None, slot: int = 0,
+                 rows: Optional[np.ndarray] = None, packed: Optional[np.ndarray] = None,
+                 keep: Optional[np.ndarray] = None, live: Optional[Dict[int, Sequence]] = None):
+        self.is_prefill = is_prefill
+        self._seqs = seqs
+        self.slot = slot
+        self.rows = rows
+        self.packed = packed
+        self.keep = keep
+        self._live = live
+
+    @property
+    def seqs(self) -> List[Sequence]:
+        if self._seqs is None:
+            live = self._live
+            self._seqs = [live[int(i)] for i in self.rows]
+        return self._seqs
+
+    @property
+    def size(self) -> int:
+        """Sequences (= rows) in the step."""
+        return len(self.rows) if self.rows is not None else len(self._seqs)
 
     @property
     def num_tokens(self) -> int:
         if self.is_prefill:
             return sum(s.total_len - s.num_cached for s in self.seqs)
-        return len(self.seqs)
+        return self.size
+
+
+def _eos_of(seq: Sequence) -> int:
+    return -1 if (seq.params.ignore_eos or seq.eos_token_id is None) else int(seq.eos_token_id)
 
 
 class Scheduler:
+    """Admission (prefill) is per-sequence Python; the running decode set of every slot lives in
+    the native :class:`SlotBatcher` (csrc/runtime/slot_batcher.cpp), which builds each decode
+    step's packed metadata and applies its sampled tokens in one call each.  A running sequence's
+    Python ``output`` list is brought up to date when it leaves the running set (finish,
+    preemption, abort); :meth:`sync_output` refreshes it earlier on demand."""
+
     def __init__(self, block_manager, num_slots: int = 1, max_batch: int = 256,
                  max_prefill_tokens: int = 16384, max_seq_len: int = 4096):
         self.bm = block_manager
@@ -42,8 +79,10 @@ class Scheduler:
         self.max_batch = max_batch
         self.max_prefill_tokens = max_prefill_tokens
         self.max_seq_len = max_seq_len
+        self.max_blocks = -(-max_seq_len // block_manager.block_size)    # decode block-table width
+        self.native = _ext.runtime().SlotBatcher(block_manager, self.num_slots, max_seq_len)
+        self.live: Dict[int, Sequence] = {}          # sequences registered with the native batcher
         self.waiting: Deque[Sequence] = collections.deque()
-        self.running: List[List[Sequence]] = [[] for _ in range(self.num_slots)]
         self.finished: List[Sequence] = []
         self.num_preemptions = 0
 
@@ -63,35 +102,39 @@ class Scheduler:
                 s.finish("abort")
                 self.finished.append(s)
                 return True
-        for run in self.running:
-            for s in run:
-                if s.seq_id == seq_id:
-                    run.remove(s)
-                    self.bm.free_sequence(s.seq_id)
-                    s.finish("abort")
-                    self.finished.append(s)
-                    return True
+        if seq_id in self.live and self.native.abort(seq_id):
+            self._sync_finished(time.perf_counter())
+            return True
         return False
 
     def has_work(self) -> bool:
-        return bool(self.waiting) or any(self.running)
+        return bool(self.waiting) or self.native.num_running_total() > 0
 
     def num_running(self) -> int:
-        return sum(len(r) for r in self.running)
+        return self.native.num_running_total()
+
+    @property
+    def running(self) -> List[List[Sequence]]:
+        """Running sequences per slot, oldest first (a snapshot)."""
+        return [[self.live[int(i)] for i in self.native.running_ids(s)] for s in range(self.num_slots)]
+
+    def sync_output(self, seq: Sequence) -> List[int]:
+        """Generated ids of ``seq`` so far, including those still held by the native batcher."""
+        if seq.seq_id in self.live and not seq.finished:
+            return seq.output + self.native.peek_output(seq.seq_id).tolist()
+        return list(seq.output)
 
     def _pick_slot_for_admission(self, slot: int) -> bool:
         """Admit into `slot` only if it is (one of) the least-loaded slots."""
-        n = len(self.running[slot])
-        return n <= min(len(r) for r in self.running)
+        return self.native.num_running(slot) <= self.native.min_running()
 
     # ------------------------------------------------------------ schedule
     def schedule(self, slot: int = 0) -> Optional[Step]:
-        running = self.running[slot]
-        admitted: List[Sequence] = []
+        n_running = self.native.num_running(slot)
         if self.waiting and self._pick_slot_for_admission(slot):
+            admitted: List[Sequence] = []
             tokens = 0
-            per_slot_cap = self.max_batch
-            while self.waiting and len(running) + len(admitted) < per_slot_cap:
+            while self.waiting and n_running + len(admitted) < self.max_batch:
                 seq = self.waiting[0]
                 n = seq.total_len - seq.num_cached
                 if admitted and tokens + n > self.max_prefill_tokens:
@@ -105,56 +148,81 @@ class Scheduler:
                 tokens += n
             if admitted:
                 return Step(True, admitted, slot)
-        if not running:
+        if not n_running:
             return None
-        # decode: every running sequence of the slot needs room for one more token (one native
-        # call for the whole slot; on failure preempt the youngest and retry from there)
-        i = 0
-        while i < len(running):
-            rest = running[i:]
-            ids = np.fromiter((s.seq_id for s in rest), dtype=np.int64, count=len(rest))
-            lens = np.fromiter((len(s.prompt) + len(s.output) for s in rest), dtype=np.int64, count=len(rest))
-            bad = self.bm.ensure_capacity_batch(ids, lens)
-            if bad < 0:
-                break
-            i += bad
-            victim = running.pop()  # youngest
-            self._preempt(victim)
-        if not running:
+        # decode: every running sequence of the slot needs room for one more token; on failure
+        # the native batcher preempts the youngest until the rest fits
+        res = self.native.build_decode(slot, self.max_blocks, 0, False)
+        self._sync_preempted()
+        if res is None:
             return None
-        return Step(False, list(running), slot)
+        packed, rows, _ = res
+        return Step(False, None, slot, rows=rows, packed=packed, live=self.live)
 
-    def _preempt(self, seq: Sequence):
-        self.bm.free_sequence(seq.seq_id)
-        seq.num_cached = 0
-        seq.status = SeqStatus.WAITING
-        self.waiting.appendleft(seq)
-        self.num_preemptions += 1
+    def schedule_lookahead(self, slot: int) -> Optional[Step]:
+        """The slot's next decode step, built while its newest decode step is still in flight
+        (input ids come from the device).  None when the host must catch up first."""
+        if self.waiting:
+            return None
+        res = self.native.build_decode(slot, self.max_blocks, 0, True)
+        if res is None:
+            return None
+        packed, rows, keep = res
+        return Step(False, None, slot, rows=rows, packed=packed, keep=keep, live=self.live)
+
+    def _sync_preempted(self):
+        for sid in self.native.take_preempted():
+            seq = self.live.pop(int(sid))
+            toks, times = self.native.take_output(sid)
+            seq.output.extend(toks.tolist())
+            seq.token_times.extend(times.tolist())
+            seq.num_cached = 0
+            seq.status = SeqStatus.WAITING
+            self.waiting.appendleft(seq)
+            self.num_preemptions += 1
+
+    def _sync_finished(self, now: float) -> List[Sequence]:
+        done = []
+        for sid, reason in self.native.take_finished():
+            seq = self.live.pop(int(sid))
+            toks, times = self.native.take_output(sid)
+            seq.output.extend(toks.tolist())
+            seq.token_times.extend(times.tolist())
+            seq.finish(reason, float(times[-1]) if len(times) else now)
+            self.finished.append(seq)
+            done.append(seq)
+        return done
 
     # ------------------------------------------------------------ results
     def complete(self, step: Step, tokens, now: Optional[float] = None) -> List[Sequence]:
         """Apply sampled tokens of an executed step; returns sequences that finished."""
+        now = time.perf_counter() if now is None else now
+        if not step.is_prefill:
+            toks = np.asarray(tokens, dtype=np.int32)
+            if self.native.complete(step.slot, step.rows, toks, now):
+                return self._sync_finished(now)
+            return []
         done = []
-        running = self.running[step.slot]
         if hasattr(tokens, "tolist"):
             tokens = tokens.tolist()      # python ints once, not a numpy scalar per sequence
-        now = time.perf_counter() if now is None else now
-        prefill = step.is_prefill
         for seq, tok in zip(step.seqs, tokens):
             st = seq.status
             if st is SeqStatus.FINISHED or st is SeqStatus.ABORTED:   # aborted while in flight
                 continue
             seq.num_cached = len(seq.prompt) + len(seq.output)
-            if prefill:
-                running.append(seq)
             if seq.append(tok, now) or seq.num_cached + 1 >= self.max_seq_len:
                 if not seq.finished:
                     seq.finish("max_seq_len", now)
-                if seq in running:
-                    running.remove(seq)
                 self.bm.free_sequence(seq.seq_id)
                 self.finished.append(seq)
                 done.append(seq)
+                continue
+            p = seq.params
+            self.native.admit(step.slot, seq.seq_id, seq.total_len, seq.output[-1],
+                              p.max_new_tokens - len(seq.output), _eos_of(seq),
+                              int(round(p.temperature * 1e4)) if p.temperature > 0 else 0, int(p.top_k),
+                              int(round(p.top_p * 1e4)))
+            self.live[seq.seq_id] = seq
         return done
 
     def pop_finished(self) -> List[Sequence]:

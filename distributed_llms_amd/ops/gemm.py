@@ -1,14 +1,21 @@
 """Dense GEMM dispatch for y = x @ w^T (w is [N, K], nn.Linear layout).
 
-* small M (decode, M <= 2..16 by weight size): hand-written weight-streaming MFMA kernel
-  (csrc/kernels/gemm_skinny.hip), 8 waves per workgroup split K and reduce in LDS; optional
-  fused SwiGLU epilogue;
-* 64 < M <= 512: wide-M kernel (gemm_wide.hip: 256 x 128 tiles with all decode rows, 3-stage
-  LDS-DMA pipeline, fused SwiGLU for the MLP up projection, deferred split-K for the down
-  projection), selected by DLLM_WIDE;
-* otherwise 64 <= M <= 512 with K >= 8192: split-K LDS-tiled MFMA kernel (gemm_tiled.hip);
-* larger M (prefill) or shapes the kernel does not tile: plain library GEMM (hipBLASLt via
-  torch).  That is the only non-HIP GPU path and it is purely shape-based.
+Decode-sized M goes to hand-written gfx950 kernels, per projection role (cutovers measured in
+the engine on Llama-3-8B, profiles/wide_gemm.md; each one is an environment knob):
+
+* wide-M kernel (gemm_wide.hip: 64/128/192/256-row x 128 tiles, 3-stage LDS-DMA pipeline):
+  - gate|up (SwiGLU fused into the epilogue): M <= 256 (DLLM_WIDE_GATE_UP_MAX_M);
+  - down (K >= 8192 and K > N; split-K partials deferred into the next norm): M <= 512
+    (DLLM_WIDE_DOWN_MAX_M, may be raised past 512);
+  - the other projections (qkv, o, LM head): M <= 256 (DLLM_WIDE_PROJ_MAX_M);
+* tiny M outside those (DLLM_WIDE off): weight-streaming MFMA GEMV (gemm_skinny.hip);
+* 64 <= M <= 512 with K >= 8192 when the wide kernel is off: split-K LDS-tiled MFMA kernel
+  (gemm_tiled.hip);
+* everything else (prefill, M above the cutovers): hipBLASLt via torch (TunableOp table in
+  tuning/), the only non-HIP GPU path, chosen purely by shape.
+
+The role is inferred from the shape: "down" = K >= 8192 and K > N, so the square / widening
+K = 8192 projections of 70B-class models (qkv 8192 -> 10240, o 8192 -> 8192) stay "proj".
 """
 from __future__ import annotations
 
@@ -93,20 +100,26 @@ WIDE_DOWN_MAX_M = int(os.environ.get("DLLM_WIDE_DOWN_MAX_M", "512"))
 WIDE_PROJ_MAX_M = int(os.environ.get("DLLM_WIDE_PROJ_MAX_M", "256"))
 
 
+def is_down_proj(n: int, k: int) -> bool:
+    """The MLP down projection's shape: long, narrowing K (8B: 14336 -> 4096, 70B: 28672 -> 8192).
+    A K = 8192 qkv or o projection of a 70B-class model (N >= K) is not one."""
+    return k >= 8192 and k > n
+
+
 def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
     if not WIDE or GEMM_MODE == "blas" or not (WIDE_MIN_M <= m <= max(512, WIDE_DOWN_MAX_M)) or n % 128 or k % 64:
         return False
     if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
         return False
     if "all" in WIDE:
-        return m <= 512 or (k >= 8192 and not swiglu and m <= WIDE_DOWN_MAX_M)
+        return m <= 512 or (is_down_proj(n, k) and not swiglu and m <= WIDE_DOWN_MAX_M)
     if "auto" in WIDE:
         if swiglu:
             return m <= WIDE_GATE_UP_MAX_M
-        return m <= (WIDE_DOWN_MAX_M if k >= 8192 else WIDE_PROJ_MAX_M)
+        return m <= (WIDE_DOWN_MAX_M if is_down_proj(n, k) else WIDE_PROJ_MAX_M)
     if swiglu:
         return "gate_up" in WIDE and m <= 512
-    return ("down" in WIDE) if k >= 8192 else ("proj" in WIDE and m <= 512)
+    return ("down" in WIDE) if is_down_proj(n, k) else ("proj" in WIDE and m <= 512)
 
 
 class SplitKPartial:

@@ -171,7 +171,7 @@ class PipelineDriver:
         with get_tracer().span("pp.wait_tokens", cat="comm", step=sid):
             arr = self.t.recv_tokens()
         self.stall_s += time.perf_counter() - t0
-        if int(arr[0]) != sid or int(arr[1]) != len(step.seqs):
+        if int(arr[0]) != sid or int(arr[1]) != step.size:
             raise RuntimeError(f"pipeline out of order: got step {arr[0]} n={arr[1]}, expected {sid}")
         done = self.scheduler.complete(step, arr[2:2 + int(arr[1])], time.perf_counter())
         self.busy[step.slot] = False

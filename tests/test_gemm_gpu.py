@@ -181,3 +181,70 @@ def test_wide_row_tile_override(cuda, bm, m):
                                  1 | (bm << 8), stream)
     p = gemm.SplitKPartial(ws, s, m, 4096, (m, 4096), x.dtype, x.device)
     torch.testing.assert_close(p.materialize().float(), ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [640, 768])
+def test_wide_linear_past_512_rows(cuda, m):
+    """DLLM_WIDE_DOWN_MAX_M > 512 routes M > 512 down projections to gemm_wide: three 256-row
+    tiles (the 192-row tile is only used up to 384) with an 8-way K split."""
+    x, w = _bf(m, 14336), _bf(4096, 14336, scale=0.05)
+    y = gemm.linear_wide(x, w, splits=8)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
+def test_deferred_down_at_768_rows_into_fused_norm(cuda, monkeypatch):
+    """ops.linear(defer=True) at M = 768 with the down cutover raised: the deferred split-K partial
+    feeds fused_add_rms_norm and matches the fp32 reference."""
+    from distributed_llms_amd.ops import reference as ref
+    monkeypatch.setattr(gemm, "WIDE", {"auto"})
+    monkeypatch.setattr(gemm, "GEMM_MODE", "auto")
+    monkeypatch.setattr(gemm, "WIDE_DOWN_MAX_M", 768)
+    torch.manual_seed(1)
+    m, n, k = 768, 4096, 14336
+    x = (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16)
+    w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(n, device="cuda")).to(torch.bfloat16)
+    res0 = torch.randn(m, n, device="cuda").to(torch.bfloat16)
+    p = ops.linear(x, w, defer=True)
+    assert isinstance(p, gemm.SplitKPartial) and p.splits > 1 and p.m == m
+    r = res0.clone()
+    y, _ = ops.fused_add_rms_norm(p, r, g, 1e-5)
+    h = ref.linear(x.float(), w.float())
+    yr, rr = ref.fused_add_rms_norm(h, res0.float(), g.float(), 1e-5)
+    torch.testing.assert_close(r.float(), rr, atol=6e-2, rtol=3e-2)
+    torch.testing.assert_close(y.float(), yr, atol=6e-2, rtol=3e-2)
+
+
+_SKN_CHILD = r"""
+import torch
+from distributed_llms_amd import ops
+from distributed_llms_amd.ops import gemm, reference as ref
+torch.manual_seed(2)
+m, n, k = 256, 4096, 14336
+x = (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16)
+w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
+g = (1 + 0.1 * torch.randn(n, device="cuda")).to(torch.bfloat16)
+res0 = torch.randn(m, n, device="cuda").to(torch.bfloat16)
+p = gemm.linear_wide(x, w, splits=8, defer=True)
+assert isinstance(p, gemm.SplitKPartial) and p.splits == 8
+r = res0.clone()
+y, _ = ops.fused_add_rms_norm(p, r, g, 1e-5)
+h = gemm.linear_wide(x, w, splits=8, defer=True).materialize()
+yr, rr = ref.fused_add_rms_norm(h.float(), res0.float(), g.float(), 1e-5)
+torch.testing.assert_close(r.float(), rr, atol=3e-2, rtol=3e-2)
+torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+print("SKN512_OK")
+"""
+
+
+def test_skn_512_threads(cuda):
+    """The opt-in 512-thread splitk_add_rms_norm (DLLM_SKN_THREADS=512, read once per process, S == 8
+    and hidden 4096 only) against the fp32 reference, in a fresh process that sets the knob before
+    its first GPU call."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DLLM_SKN_THREADS="512", PYTHONPATH=root)
+    out = subprocess.run([sys.executable, "-c", _SKN_CHILD], env=env, cwd=root, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0 and "SKN512_OK" in out.stdout, out.stdout[-2000:] + out.stderr[-4000:]

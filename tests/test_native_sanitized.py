@@ -1,5 +1,5 @@
 """Host runtime under UBSan + libstdc++ assertions: ``_C_runtime`` (paged-KV block
-manager, wire-frame codec) is rebuilt with -fsanitize=undefined (no recovery) and
+manager, decode-slot batcher, wire-frame codec) is rebuilt with -fsanitize=undefined (no recovery) and
 _GLIBCXX_ASSERTIONS, loaded into a fresh interpreter under its package name, and driven through a
 randomized workload that includes every error path.  Any undefined behaviour or container
 bounds violation aborts the child process, failing the test.  CPU only."""
@@ -59,6 +59,52 @@ CHILD = textwrap.dedent('''
                                           np.array([1], np.int32), np.zeros(1, np.int32)),
                     lambda: bm.fill_block_tables(np.array([0, 1], np.int64), np.zeros((1, 1), np.int32), 0),
                     lambda: rt.BlockManager(0, 16)):
+            try:
+                bad()
+            except Exception:
+                pass
+
+    # ---- slot batcher: random admit / decode (sync + lookahead) / complete / abort over a small
+    # KV pool, so preemption and capacity failures happen
+    for bs in (1, 4, 16):
+        bm = rt.BlockManager(24 + 8 * bs, bs)
+        nslots, max_seq = 3, 24 + rng.randrange(40)
+        sb = rt.SlotBatcher(bm, nslots, max_seq)
+        nxt = 1
+        inflight = {s: [] for s in range(nslots)}
+        for step in range(3000):
+            slot = rng.randrange(nslots)
+            op = rng.random()
+            if op < 0.2 and sb.num_running(slot) < 12:
+                n = rng.randrange(1, max_seq - 1)
+                if bm.ensure_capacity(nxt, n):
+                    sb.admit(slot, nxt, n, rng.randrange(1000), rng.randrange(1, 30),
+                             rng.choice([-1, 3, 7]), rng.choice([0, 0, 5000]), 0, 10000)
+                nxt += 1
+            elif op < 0.6:
+                look = bool(inflight[slot]) and rng.random() < 0.5
+                if not look and inflight[slot]:
+                    continue
+                mb = -(-max_seq // bs) + rng.randrange(2)
+                r = sb.build_decode(slot, mb, step, look)
+                if r is not None:
+                    packed, rows, keep = r
+                    assert packed[2] == len(rows) and packed[3] == mb
+                    inflight[slot].append(rows)
+            elif op < 0.9 and inflight[slot]:
+                rows = inflight[slot].pop(0)
+                sb.complete(slot, rows, np.array([rng.randrange(10) for _ in rows], np.int32), float(step))
+            elif op < 0.95:
+                ids = sb.running_ids(slot)
+                if len(ids) and not inflight[slot]:
+                    sb.abort(int(ids[rng.randrange(len(ids))]))
+            for sid, why in sb.take_finished():
+                sb.take_output(sid)
+            for sid in sb.take_preempted():
+                sb.take_output(sid)
+            assert bm.num_free() >= 0
+        for bad in (lambda: sb.admit(99, 1, 1, 1, 1), lambda: sb.take_output(10 ** 9),
+                    lambda: sb.build_decode(0, 0, 0, False), lambda: rt.SlotBatcher(bm, 1, 1)):
             try:
                 bad()
             except Exception:

@@ -18,6 +18,11 @@ def _defaults(monkeypatch):
     monkeypatch.setattr(gemm, "WIDE", {"auto"})
     monkeypatch.setattr(gemm, "GEMM_MODE", "auto")
     monkeypatch.setattr(gemm, "WIDE_MIN_M", 1)
+    # the cutovers are read from the environment at import time: pin the shipped defaults so an
+    # exported A/B knob (e.g. DLLM_WIDE_DOWN_MAX_M=768) cannot move the boundary cases below
+    monkeypatch.setattr(gemm, "WIDE_GATE_UP_MAX_M", 256)
+    monkeypatch.setattr(gemm, "WIDE_DOWN_MAX_M", 512)
+    monkeypatch.setattr(gemm, "WIDE_PROJ_MAX_M", 256)
 
 
 @pytest.mark.parametrize("m,expect", [(1, True), (64, True), (256, True), (257, False), (384, False), (512, False)])
@@ -36,6 +41,24 @@ def test_down_cutover(m, expect):
 def test_proj_cutover(m, expect):
     x, w = _xw(m, 6144, 4096)
     assert gemm._use_wide(m, 6144, 4096, x, w) is expect
+
+
+# Llama-3-70B: hidden 8192, so qkv (8192 -> 10240) and o (8192 -> 8192) also have K = 8192; they
+# are projections ("proj" cutover), only the narrowing 28672 -> 8192 down projection is "down"
+@pytest.mark.parametrize("n,k,m,expect", [
+    (10240, 8192, 256, True), (10240, 8192, 257, False), (10240, 8192, 512, False),   # qkv
+    (8192, 8192, 256, True), (8192, 8192, 384, False),                                # o
+    (8192, 28672, 384, True), (8192, 28672, 512, True), (8192, 28672, 513, False),    # down
+])
+def test_70b_roles(n, k, m, expect):
+    x, w = _xw(m, n, k)
+    assert gemm._use_wide(m, n, k, x, w) is expect
+
+
+def test_down_role_rule():
+    assert gemm.is_down_proj(4096, 14336) and gemm.is_down_proj(8192, 28672)
+    assert not gemm.is_down_proj(10240, 8192) and not gemm.is_down_proj(8192, 8192)
+    assert not gemm.is_down_proj(4096, 4096) and not gemm.is_down_proj(128256, 4096)
 
 
 def test_down_cap_can_exceed_512(monkeypatch):
