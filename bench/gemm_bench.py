@@ -21,6 +21,7 @@ SHAPES = {  # name: (N, K, swiglu)
     "qkv_8b": (6144, 4096, False), "o_8b": (4096, 4096, False), "gate_up_8b": (28672, 4096, True),
     "down_8b": (4096, 14336, False), "lm_head_8b": (128256, 4096, False),
     "qkv_70b": (10240, 8192, False), "down_70b": (8192, 28672, False),
+    "o_70b": (8192, 8192, False), "gate_up_70b": (57344, 8192, True),
 }
 
 
@@ -47,6 +48,8 @@ def main():
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--variants", type=int, nargs="*", default=[0],
                     help="--wide: extra gemm_wide variants timed beside the default (1)")
+    ap.add_argument("--sq", action="store_true", help="--wide: also time the 256 x 256-tile gemm_sq kernel")
+    ap.add_argument("--sq-alt", type=int, default=0, help="--sq: second gemm_sq variant timed (sq0)")
     a = ap.parse_args()
     # a scratch buffer larger than the 256 MiB Infinity Cache to flush it between calls
     flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
@@ -98,6 +101,8 @@ def wide(a, flush):
                 "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=1),
                 **{f"v{v}": (lambda w, v=v: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=v))
                    for v in a.variants},
+                **({"sq": lambda w: gemm.linear_sq(x, w, swiglu=sw, variant=4),
+                    "sq0": lambda w: gemm.linear_sq(x, w, swiglu=sw, variant=a.sq_alt)} if a.sq and n % 256 == 0 else {}),
                 "tiled": lambda w: gemm.linear_tiled(x, w, swiglu=sw),
                 "blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w)),
             }
@@ -125,7 +130,8 @@ def wide(a, flush):
             byt, fl_ = n * k * 2, 2.0 * m * n * k
             print(f"{name:12s} {m:4d} {t['wide']*1e6:8.1f} {byt/t['wide']/1e12:6.2f} {fl_/t['wide']/1e12:6.0f} "
                   f"{t['tiled']*1e6:8.1f} {t['blas']*1e6:8.1f} {t['tiled']/t['wide']:8.2f} {t['blas']/t['wide']:8.2f} "
-                  + " ".join(f"v{v} {t[f'v{v}']*1e6:6.1f}" for v in a.variants),
+                  + " ".join(f"v{v} {t[f'v{v}']*1e6:6.1f}" for v in a.variants)
+                  + (f" sq {t['sq']*1e6:6.1f} ({t['wide']/t['sq']:.2f}x) sq0 {t['sq0']*1e6:6.1f}" if "sq" in t else ""),
                   flush=True)
 
 

@@ -25,6 +25,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("splitk_add_rms_norm", &dllm::splitk_add_rms_norm);
   m.def("splitk_reduce", &dllm::splitk_reduce);
   m.def("gemm_wide", &dllm::gemm_wide);
+  m.def("gemm_sq", &dllm::gemm_sq);
   m.def("moe_combine", &dllm::moe_combine);
   m.def("moe_wide_gemm", &dllm::moe_wide_gemm);
   m.def("moe_router_route", &dllm::moe_router_route);

@@ -30,6 +30,8 @@ void splitk_reduce_ex(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M,
                       uintptr_t stream);
 int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
               int mode, int variant, uintptr_t stream);
+int gemm_sq(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
+            int mode, int variant, uintptr_t stream);
 
 void moe_route(uintptr_t logits, int T, int E, int k, uintptr_t topk_w, uintptr_t topk_ids, uintptr_t counts,
                uintptr_t offsets, uintptr_t sorted_tok, uintptr_t inv, uintptr_t stream);

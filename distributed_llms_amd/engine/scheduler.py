@@ -85,6 +85,7 @@ class Scheduler:
         self.waiting: Deque[Sequence] = collections.deque()
         self.finished: List[Sequence] = []
         self.num_preemptions = 0
+        self.num_prefilling = 0                       # admitted, prefill step not completed yet
 
     # ------------------------------------------------------------ requests
     def add(self, seq: Sequence) -> None:
@@ -124,17 +125,23 @@ class Scheduler:
             return seq.output + self.native.peek_output(seq.seq_id).tolist()
         return list(seq.output)
 
-    def _pick_slot_for_admission(self, slot: int) -> bool:
-        """Admit into `slot` only if it is (one of) the least-loaded slots."""
-        return self.native.num_running(slot) <= self.native.min_running()
+    def _admission_target(self) -> int:
+        """Sequences a slot should hold: an even share of everything admitted or waiting (capped by
+        max_batch).  Each slot tops itself up to it when its turn comes, so a burst of requests is
+        prefilled in full-size chunks on every slot at once and decode starts at full batch,
+        instead of least-loaded-first admission starting some slots' decode with a quarter of
+        their rows while the others still prefill."""
+        total = self.native.num_running_total() + self.num_prefilling + len(self.waiting)
+        return min(self.max_batch, -(-total // self.num_slots))
 
     # ------------------------------------------------------------ schedule
     def schedule(self, slot: int = 0) -> Optional[Step]:
         n_running = self.native.num_running(slot)
-        if self.waiting and self._pick_slot_for_admission(slot):
+        if self.waiting:
             admitted: List[Sequence] = []
             tokens = 0
-            while self.waiting and n_running + len(admitted) < self.max_batch:
+            target = self._admission_target()
+            while self.waiting and n_running + len(admitted) < target:
                 seq = self.waiting[0]
                 n = seq.total_len - seq.num_cached
                 if admitted and tokens + n > self.max_prefill_tokens:
@@ -147,6 +154,7 @@ class Scheduler:
                 admitted.append(seq)
                 tokens += n
             if admitted:
+                self.num_prefilling += len(admitted)
                 return Step(True, admitted, slot)
         if not n_running:
             return None
@@ -203,6 +211,7 @@ class Scheduler:
                 return self._sync_finished(now)
             return []
         done = []
+        self.num_prefilling -= len(step.seqs)
         if hasattr(tokens, "tolist"):
             tokens = tokens.tolist()      # python ints once, not a numpy scalar per sequence
         for seq, tok in zip(step.seqs, tokens):

@@ -263,6 +263,8 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     k = x.shape[-1]
     n = w.shape[0]
     m = x.numel() // k
+    if splits == 0 and variant < 0 and use_sq(m, n, k, swiglu):
+        return linear_sq(x, w, swiglu=swiglu, defer=defer)
     if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
         raise ValueError("linear_wide: bf16 contiguous operands")
     if n % 128 or k % 64:
@@ -282,6 +284,69 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
     _ext.kernels().gemm_wide(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s,
                              1 if swiglu else 0, v, stream)
+    return y
+
+
+# 256 x 256-tile decode GEMM (gemm_sq.hip) for 128 < M <= 256: a third fewer staged bytes per FLOP
+# than the wide kernel's 256 x 128 tile.  Measured (profiles/wide_gemm.md, "256 x 256 tile"): it
+# wins only where the grid needs no K split -- the LM head (1.05x) and the 70B MLP gate|up (1.07x);
+# split grids (8B qkv / o / gate|up / down) lose 6-20 % to the extra slab traffic.  DLLM_SQ: comma
+# list of roles (gate_up, down, proj, head, all) or none; DLLM_SQ_SPLIT=1 also admits split grids.
+SQ = {t for t in os.environ.get("DLLM_SQ", "all").split(",") if t and t != "none"}
+SQ_MIN_M = int(os.environ.get("DLLM_SQ_MIN_M", "225"))   # at M = 192 it loses 1-6 %
+SQ_SPLIT = os.environ.get("DLLM_SQ_SPLIT", "0") == "1"
+
+
+def sq_role(n: int, k: int, swiglu: bool) -> str:
+    if swiglu:
+        return "gate_up"
+    if is_down_proj(n, k):
+        return "down"
+    return "head" if n > 65536 else "proj"
+
+
+def use_sq(m: int, n: int, k: int, swiglu: bool = False) -> bool:
+    if not SQ or not (SQ_MIN_M <= m <= 256) or n % 256 or k % 64:
+        return False
+    if not SQ_SPLIT and sq_splits(m, n, k) > 1:
+        return False
+    return "all" in SQ or sq_role(n, k, swiglu) in SQ
+
+
+def sq_splits(m: int, n: int, k: int, target_wgs: int = 256) -> int:
+    """K slices for gemm_sq: as many as keep (N / 256) x slices within one workgroup per CU, at
+    least 4 K-tiles (256) per slice."""
+    tiles = (n // 256) * (-(-m // 256))
+    return max(1, min(target_wgs // max(1, tiles), (k // 64) // 4, 16))
+
+
+SQ_VARIANT = int(os.environ.get("DLLM_SQ_VARIANT", "4"))
+
+
+def linear_sq(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = False, defer: bool = False,
+              variant: int = -1):
+    """256 x 256-tile decode GEMM (csrc/kernels/gemm_sq.hip); split-K partials reduced by
+    splitk_reduce(_swiglu), or returned as a :class:`SplitKPartial` with ``defer`` (no SwiGLU)."""
+    k = x.shape[-1]
+    n = w.shape[0]
+    m = x.numel() // k
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        raise ValueError("linear_sq: bf16 contiguous operands")
+    if n % 256 or k % 64:
+        raise ValueError("linear_sq: N % 256 and K % 64")
+    s = splits or sq_splits(m, n, k)
+    ws = _workspace(x.device)
+    if s > 1 and s * m * n > ws.numel():
+        s = max(1, ws.numel() // (m * n))
+    stream = torch.cuda.current_stream().cuda_stream
+    v = SQ_VARIANT if variant < 0 else variant
+    if defer and not swiglu and s > 1:
+        se = _ext.kernels().gemm_sq(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, v,
+                                    stream)
+        return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
+    y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
+    _ext.kernels().gemm_sq(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s,
+                           1 if swiglu else 0, v, stream)
     return y
 
 

@@ -248,3 +248,40 @@ def test_skn_512_threads(cuda):
     out = subprocess.run([sys.executable, "-c", _SKN_CHILD], env=env, cwd=root, capture_output=True, text=True,
                          timeout=300)
     assert out.returncode == 0 and "SKN512_OK" in out.stdout, out.stdout[-2000:] + out.stderr[-4000:]
+
+
+@pytest.mark.parametrize("m", [129, 200, 256])
+@pytest.mark.parametrize("n,k,splits", [(6144, 4096, 0), (4096, 14336, 0), (4096, 4096, 16), (1024, 512, 1),
+                                        (512, 1024, 3)])
+def test_sq_linear(cuda, m, n, k, splits):
+    """256 x 256-tile decode GEMM (gemm_sq.hip) vs fp32, split and unsplit, partial row tile."""
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear_sq(x, w, splits=splits)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [130, 256])
+@pytest.mark.parametrize("inter,k,splits", [(14336, 4096, 0), (1024, 512, 1), (1024, 1024, 2)])
+def test_sq_swiglu(cuda, m, inter, k, splits):
+    """SwiGLU: fused epilogue (1 slice, interleaved gate / up rows) and split-K + SwiGLU reduce."""
+    x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
+    y = gemm.linear_sq(x, w, splits=splits, swiglu=True)
+    gu = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), F.silu(gu[:, :inter]) * gu[:, inter:], atol=3e-2, rtol=3e-2)
+
+
+def test_sq_deferred_into_fused_norm(cuda):
+    from distributed_llms_amd.ops import reference as ref
+    torch.manual_seed(3)
+    m, n, k = 256, 4096, 14336
+    x = (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16)
+    w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(n, device="cuda")).to(torch.bfloat16)
+    res0 = torch.randn(m, n, device="cuda").to(torch.bfloat16)
+    p = gemm.linear_sq(x, w, defer=True)
+    assert isinstance(p, gemm.SplitKPartial) and p.splits == 16
+    r = res0.clone()
+    y, _ = ops.fused_add_rms_norm(p, r, g, 1e-5)
+    yr, rr = ref.fused_add_rms_norm(ref.linear(x.float(), w.float()), res0.float(), g.float(), 1e-5)
+    torch.testing.assert_close(r.float(), rr, atol=6e-2, rtol=3e-2)
+    torch.testing.assert_close(y.float(), yr, atol=6e-2, rtol=3e-2)

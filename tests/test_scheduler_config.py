@@ -119,16 +119,37 @@ def test_scheduler_eos_abort_and_slot_balance():
     for s in (a, b, c):
         sch.add(s)
     st0 = sch.schedule(0)
-    assert len(st0.seqs) == 3                                   # slot 0 takes what fits
-    sch.complete(st0, [42, 5, 6])                               # a: EOS on its first token
+    assert st0.seqs == [a, b]                                   # slot 0 takes its even share (2 of 3)
+    sch.complete(st0, [42, 5])                                  # a: EOS on its first token
     assert a.finished and a.finish_reason == "eos"
     d = _seq(3, 10)
     sch.add(d)
-    assert sch.schedule(0).is_prefill is False                  # slot 0 is fuller than slot 1
+    st0 = sch.schedule(0)                                       # share = ceil((1 running + 2 waiting) / 2)
+    assert st0.is_prefill and st0.seqs == [c]                   # slot 0 tops up to 2
     st1 = sch.schedule(1)
-    assert st1.is_prefill and st1.seqs == [d]                   # admitted into the emptier slot
+    assert st1.is_prefill and st1.seqs == [d]                   # the emptier slot takes the rest
+    sch.complete(st0, [3])
+    assert sch.schedule(0).is_prefill is False and sch.running[0] == [b, c]
     assert sch.abort(b.seq_id) and b.status is SeqStatus.ABORTED
     assert not sch.abort(12345)
+
+
+def test_burst_is_spread_over_slots_in_full_prefill_chunks():
+    """A burst of 8 requests over 2 slots with a 2-request prefill budget: each slot tops itself
+    up to its share of 4 in prefill chunks before decoding (no early decode at a quarter batch)."""
+    bm = make_block_manager(256, 4)
+    sch = Scheduler(bm, num_slots=2, max_batch=8, max_prefill_tokens=8, max_seq_len=64)
+    seqs = [_seq(4, 10) for _ in range(8)]
+    for s in seqs:
+        sch.add(s)
+    kinds = []
+    for rnd in range(3):
+        for slot in (0, 1):
+            st = sch.schedule(slot)
+            kinds.append((slot, st.is_prefill, st.size))
+            sch.complete(st, [1] * st.size)
+    assert kinds == [(0, True, 2), (1, True, 2), (0, True, 2), (1, True, 2), (0, False, 4), (1, False, 4)]
+    assert sch.num_prefilling == 0 and not sch.waiting
 
 
 def test_scheduler_preempts_youngest_when_kv_runs_out():

@@ -74,3 +74,20 @@ def test_blas_mode_and_dtype_disable_wide(monkeypatch):
     assert not gemm._use_wide(128, 4096, 4096, x.float(), w.float())
     monkeypatch.setattr(gemm, "GEMM_MODE", "blas")
     assert not gemm._use_wide(128, 4096, 4096, x, w)
+
+
+def test_sq_only_on_unsplit_grids(monkeypatch):
+    """gemm_sq (256 x 256 tiles) serves 225 <= M <= 256 only where its grid needs no K split: the
+    LM head and the 70B gate|up (profiles/wide_gemm.md)."""
+    monkeypatch.setattr(gemm, "SQ", {"all"})
+    monkeypatch.setattr(gemm, "SQ_MIN_M", 225)
+    monkeypatch.setattr(gemm, "SQ_SPLIT", False)
+    assert gemm.use_sq(256, 128256, 4096) and not gemm.use_sq(192, 128256, 4096)
+    assert gemm.use_sq(256, 57344, 8192, swiglu=True)
+    assert not gemm.use_sq(128, 128256, 4096)                      # 128-row tile of the wide kernel
+    for n, k, sw in ((6144, 4096, False), (4096, 4096, False), (28672, 4096, True), (4096, 14336, False),
+                     (10240, 8192, False), (8192, 28672, False), (32000, 4096, False)):
+        assert not gemm.use_sq(256, n, k, swiglu=sw), (n, k)
+    monkeypatch.setattr(gemm, "SQ_SPLIT", True)
+    assert gemm.use_sq(256, 4096, 14336)
+    assert gemm.sq_splits(256, 4096, 14336) == 16 and gemm.sq_splits(256, 6144, 4096) == 10
