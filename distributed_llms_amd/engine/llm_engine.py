@@ -200,7 +200,10 @@ class LLMEngine:
         done.extend(self.scheduler.pop_finished())
         return done
 
-    def generate(self, prompts: Iterable[List[int]], params: Optional[SamplingParams] = None) -> List[List[int]]:
-        seqs = [self.add_request(p, params) for p in prompts]
+    def generate(self, prompts: Iterable[List[int]], params=None) -> List[List[int]]:
+        """``params``: one SamplingParams for all prompts, or a list (one per prompt)."""
+        prompts = list(prompts)
+        plist = params if isinstance(params, (list, tuple)) else [params] * len(prompts)
+        seqs = [self.add_request(p, q) for p, q in zip(prompts, plist)]
         self.run_until_done()
         return [s.output for s in seqs]

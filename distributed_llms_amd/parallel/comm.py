@@ -3,12 +3,18 @@
 Three message kinds flow along a pipeline:
   meta    stage s -> s+1   packed int32 HostBatch (block tables, slots, ...)   CPU, control group
   hidden  stage s -> s+1   [T, H] bf16 activations                            device, data group
-  tokens  last  -> stage 0 sampled ids (ring closure for the next decode step) CPU, control group
+  ids     last  -> stage 0 sampled ids [B] int32 (ring closure)              device, ring group
 
 ``DistTransport`` rides on torch.distributed: activations on the default group (backend
 "nccl" = RCCL over xGMI on MI355X, gloo on CPU) as point-to-point isend/recv, whose
 launches torch orders against the compute stream with events; control messages on a
-separate gloo group so they never serialise behind GPU work.  ``LoopbackTransport`` is
+separate gloo group so they never serialise behind GPU work.  The ring closure has a group of
+its own ({stage 0, last stage}): a communicator -- and an RCCL stream -- separate from the
+activation pair's, so at pp = 2, where both flows join the same two ranks, a posted ids receive
+never queues an activation send behind it (p2p ops of one communicator are stream-ordered).
+Stage 0 posts each microbatch's ids receive when it issues the microbatch, feeds the device
+ids straight into the slot's next decode step (lookahead) and reads them on the host one step
+later for bookkeeping -- the host is not on the ring's critical path.  ``LoopbackTransport`` is
 the same interface over in-process queues, so N stage threads can share one GPU
 (NCCL-family libraries refuse two ranks of one communicator on one device) -- this is
 how the pipeline schedule is exercised on the single-GPU test box.
@@ -26,6 +32,59 @@ import torch.distributed as dist
 STOP = -1
 
 
+class PendingIds:
+    """One microbatch's sampled ids on their way from the last stage to stage 0.
+
+    ``wait()`` returns the ids tensor once it may be used: on a GPU stage it orders the CURRENT
+    stream after the arrival (no host block); on CPU it blocks.  ``host()`` returns them as numpy
+    (blocking); with a ``copy_stream`` the device -> pinned copy is queued at post time so the
+    host read later finds it done."""
+
+    def __init__(self, tensor: Optional[torch.Tensor] = None, work=None, ready=None, fetch=None,
+                 copy_stream=None):
+        self.tensor = tensor
+        self._work = work          # torch.distributed Work (NCCL: stream-orders; gloo: blocks)
+        self._ready = ready        # torch.cuda.Event recorded when `tensor` was filled
+        self._fetch = fetch        # loopback: blocking getter -> (tensor, event or None)
+        self._host = None
+        self._host_ev = None
+        self._foreign = False
+        if copy_stream is not None and tensor is not None and tensor.is_cuda:
+            with torch.cuda.stream(copy_stream):
+                self.wait()
+                self._host = torch.empty(tensor.shape, dtype=tensor.dtype).pin_memory()
+                self._host.copy_(tensor, non_blocking=True)
+                self._host_ev = torch.cuda.Event()
+                self._host_ev.record(copy_stream)
+
+    def wait(self) -> torch.Tensor:
+        if self._fetch is not None:
+            self.tensor, self._ready = self._fetch()
+            self._fetch = None
+            self._foreign = self.tensor.is_cuda and self._ready is not None   # another thread's stream
+        if self._work is not None:
+            self._work.wait()
+            if not (self.tensor is not None and self.tensor.is_cuda):
+                self._work = None     # CPU: done once
+        if self._ready is not None:
+            cur = torch.cuda.current_stream()
+            cur.wait_event(self._ready)
+            if self._foreign:
+                # allocated on the producer thread's stream: keep the block out of its pool until
+                # this stream is done with it
+                self.tensor.record_stream(cur)
+        return self.tensor
+
+    def host(self) -> np.ndarray:
+        if self._host_ev is not None:
+            self._host_ev.synchronize()
+            return self._host.numpy()
+        t = self.wait()
+        if t.is_cuda:
+            return t.cpu().numpy()       # synchronises this stream; used off the hot path only
+        return t.numpy()
+
+
 class Transport:
     stage: int
     num_stages: int
@@ -34,17 +93,21 @@ class Transport:
     def recv_meta(self) -> np.ndarray: ...
     def send_hidden(self, t: torch.Tensor) -> None: ...
     def recv_hidden(self, rows: int, hidden: int, dtype, device) -> torch.Tensor: ...
-    def send_tokens(self, arr: np.ndarray) -> None: ...
-    def recv_tokens(self) -> np.ndarray: ...
+    def send_ids(self, ids: torch.Tensor) -> None: ...
+    def recv_ids(self, n: int, device) -> PendingIds: ...
 
 
 class DistTransport(Transport):
     """One pipeline = ranks ``ranks[0..pp-1]`` (global ranks), stage = index in that list."""
 
-    def __init__(self, ranks, stage: int, ctrl_group=None, data_group=None):
+    def __init__(self, ranks, stage: int, ctrl_group=None, data_group=None, ring_group=None):
         """``data_group`` None = the default group (RCCL on GPU).  A gloo ``data_group`` with GPU
-        stages means host-staged activations (D2H -> gloo -> H2D): the TCP fallback."""
+        stages means host-staged activations (D2H -> gloo -> H2D): the TCP fallback.
+        ``ring_group``: the {first, last} group of this pipeline for the ids ring closure (None =
+        the data group; fine wherever the activation and ids flows join different rank pairs)."""
         self.ranks = list(ranks)
+        self.ring = ring_group if ring_group is not None else data_group
+        self._copy_stream = None
         self.stage = stage
         self.num_stages = len(self.ranks)
         self.ctrl = ctrl_group
@@ -91,11 +154,38 @@ class DistTransport(Transport):
             hdr = torch.tensor([-1], dtype=torch.int64)
             dist.send(hdr, self.next, group=self.ctrl)
 
-    def send_tokens(self, arr):
-        self._send_arr(arr, self.first)
+    # ---- ring closure: sampled ids, last stage -> stage 0
+    def _ring_staged(self, device) -> bool:
+        return torch.device(device).type == "cuda" and self.ring is not None \
+            and dist.get_backend(self.ring) == "gloo"
 
-    def recv_tokens(self):
-        return self._recv_arr(self.last)
+    def send_ids(self, ids: torch.Tensor):
+        ids = ids.to(torch.int32)
+        if self._ring_staged(ids.device):
+            ids = ids.to("cpu")                  # host-staged fallback
+        else:
+            ids = ids.clone()
+        w = dist.isend(ids, self.first, group=self.ring)
+        self._pending.append((w, ids))
+        self._reap()
+
+    def recv_ids(self, n: int, device) -> PendingIds:
+        dev = torch.device(device)
+        if self._ring_staged(dev):
+            buf = torch.empty(n, dtype=torch.int32)
+            w = dist.irecv(buf, self.last, group=self.ring)
+
+            def fetch():
+                w.wait()
+                return buf.to(dev), None
+            return PendingIds(fetch=fetch)
+        buf = torch.empty(n, dtype=torch.int32, device=dev)
+        w = dist.irecv(buf, self.last, group=self.ring)
+        if dev.type == "cuda":
+            if self._copy_stream is None:
+                self._copy_stream = torch.cuda.Stream(dev)
+            return PendingIds(buf, work=w, copy_stream=self._copy_stream)
+        return PendingIds(buf, work=w)
 
     # ---- data plane (RCCL on GPU, gloo on CPU)
     def send_hidden(self, t: torch.Tensor):
@@ -129,7 +219,7 @@ class LoopbackHub:
         self.num_stages = num_stages
         self.meta = [queue.Queue() for _ in range(num_stages)]     # into stage s
         self.hidden = [queue.Queue() for _ in range(num_stages)]
-        self.tokens = queue.Queue()
+        self.ids = queue.Queue()
 
     def transport(self, stage: int) -> "LoopbackTransport":
         return LoopbackTransport(self, stage)
@@ -168,11 +258,24 @@ class LoopbackTransport(Transport):
         assert t.shape == (rows, hidden), (t.shape, rows, hidden)
         return t
 
-    def send_tokens(self, arr):
-        self.hub.tokens.put(np.array(arr, copy=True))
+    def send_ids(self, ids):
+        ids = ids.to(torch.int32).clone()
+        ev = None
+        if ids.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        self.hub.ids.put((ids, ev))
 
-    def recv_tokens(self):
-        return self.hub.tokens.get()
+    def recv_ids(self, n, device) -> PendingIds:
+        hub = self.hub
+
+        def fetch():
+            t, ev = hub.ids.get()
+            if isinstance(t, BaseException):
+                raise t
+            assert t.shape[0] == n, (t.shape, n)
+            return t, ev
+        return PendingIds(fetch=fetch)
 
     def drain(self):
         pass

@@ -35,6 +35,7 @@ class DistContext:
     ctrl_group: object
     device: str
     data_group: object = None      # None = the default (RCCL) group
+    ring_groups: tuple = ()        # per pipeline: the {stage 0, last stage} group of the ids ring closure
 
     @property
     def host_staged(self) -> bool:
@@ -52,6 +53,10 @@ class DistContext:
     def pipeline_ranks(self):
         p = self.pipeline_id
         return list(range(p * self.pp, (p + 1) * self.pp))
+
+    @property
+    def ring_group(self):
+        return self.ring_groups[self.pipeline_id] if self.ring_groups else None
 
 
 def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
@@ -83,17 +88,22 @@ def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
     pp = pp or world
     if world % pp:
         raise ValueError(f"world {world} not divisible by pp {pp}")
+    # one {first, last} group per pipeline for the sampled-ids ring closure (new_group is
+    # collective: every rank creates every pipeline's group, in the same order)
+    ring_backend = "gloo" if (host_staged or backend == "gloo") else "nccl"
+    rings = tuple(dist.new_group(ranks=[p * pp, p * pp + pp - 1], backend=ring_backend, timeout=tmo)
+                  for p in range(world // pp)) if pp > 1 else ()
     return DistContext(rank, world, local_rank, world // pp, pp, ctrl,
-                       f"cuda:{dev_idx}" if use_gpu else "cpu", data)
+                       f"cuda:{dev_idx}" if use_gpu else "cpu", data, rings)
 
 
-def make_transport(ranks, stage: int, ctrl_group, data_group, device: str):
+def make_transport(ranks, stage: int, ctrl_group, data_group, device: str, ring_group=None):
     """Activation transport for one pipeline stage: torch.distributed's RCCL process group by
-    default; ``DLLM_TRANSPORT=rccl`` selects the native RCCL p2p module (own comm stream)."""
+    default; ``DLLM_TRANSPORT=rccl`` selects the native RCCL p2p module (own comm streams)."""
     if os.environ.get("DLLM_TRANSPORT", "") == "rccl" and data_group is None and str(device).startswith("cuda"):
         from .rccl_transport import RcclTransport
         return RcclTransport(ranks, stage, ctrl_group, device)
-    return DistTransport(ranks, stage, ctrl_group=ctrl_group, data_group=data_group)
+    return DistTransport(ranks, stage, ctrl_group=ctrl_group, data_group=data_group, ring_group=ring_group)
 
 
 def agree_min(ctx: DistContext, value: int) -> int:
@@ -130,7 +140,7 @@ class RankRole:
         else:
             self.runner = StageRunner(stage, ecfg, num_blocks=nb)
             self.transport = make_transport(ctx.pipeline_ranks, ctx.stage, ctx.ctrl_group, ctx.data_group,
-                                            ctx.device)
+                                            ctx.device, ctx.ring_group)
             if ctx.stage == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.runner, self.transport, ecfg, bm)

@@ -6,19 +6,26 @@ between them (``src/master/node.py:256-269``).  Here a pipeline of
 continuous-batching scheduler with ``num_slots`` (>= pp) microbatch slots and issues one
 microbatch after another, so every stage has work in flight:
 
-    stage 0:  schedule(slot) -> meta -> stage-0 forward -> send hidden      (no wait)
-    stage s:  recv meta -> recv hidden -> forward -> send hidden / sample
-    last:     logits -> sample -> tokens back to stage 0 (ring closure)
+    stage 0:  schedule(slot) -> meta -> stage-0 forward -> send hidden -> post ids receive
+    stage s:  recv meta -> recv hidden -> forward -> send hidden
+    last:     ... -> logits -> sample -> send ids to stage 0 (ring closure, device to device)
 
-Stage 0 only blocks on a slot's sampled tokens when it is that slot's turn again, which
-is ``num_slots`` microbatches later -- by then the tokens have normally arrived.
+A slot's next decode step is issued with LOOKAHEAD: its rows and metadata come from the native
+batcher (positions advanced past the step still in flight) and its input ids are the in-flight
+step's sampled ids, received on the device and gathered there.  The host reads those ids one
+step later, for bookkeeping only, so neither the host nor the control plane is on the ring's
+critical path: a slot's round trip is the stages' GPU time plus the hops, against ``num_slots``
+microbatches of stage-0 work.  Steps that need the host first (prefill admission, preemption,
+sampled sequences' stop checks after a prefill) fall back to completing the slot's step before
+scheduling (DLLM_PP_LOOKAHEAD=0: always).
 """
 from __future__ import annotations
 
 import collections
 import logging
+import os
 import time
-from typing import Deque, List, Optional, Tuple
+from typing import Deque, List, Optional
 
 import numpy as np
 import torch
@@ -30,56 +37,17 @@ from ..engine.sampler import sample
 from ..engine.scheduler import Scheduler, Step
 from ..engine.sequence import SamplingParams, Sequence
 from ..utils.tracing import get_tracer
-from .comm import STOP, Transport
+from .comm import STOP, PendingIds, Transport
 
 log = logging.getLogger("dllm.pipeline")
 
 ROUND_END = -2     # control marker: followers return to their caller (bench round barrier)
-FLUSH = -3         # control marker: the last stage must hand back the tokens it still holds
-_MARKERS = (STOP, ROUND_END, FLUSH)
+_MARKERS = (STOP, ROUND_END)
+LOOKAHEAD = os.environ.get("DLLM_PP_LOOKAHEAD", "1") != "0"
 
 
 def _marker(code: int) -> np.ndarray:
     return np.array([code], dtype=np.int32)
-
-
-class _TokenReturn:
-    """Last stage: sampled ids go D2H asynchronously; a microbatch's tokens are sent only after
-    the NEXT microbatch has been launched, so the GPU never idles on the host's sync + send."""
-
-    def __init__(self, transport: Transport, max_rows: int, device):
-        self.t = transport
-        self.cuda = torch.device(device).type == "cuda"
-        self.bufs = [torch.empty(max_rows, dtype=torch.int32).pin_memory() if self.cuda else None for _ in range(2)]
-        self.events = [torch.cuda.Event() if self.cuda else None for _ in range(2)]
-        self.i = 0
-        self.pending = None
-
-    def push(self, step_id: int, ids: torch.Tensor):
-        n = ids.shape[0]
-        if self.cuda:
-            if n > self.bufs[self.i].shape[0]:
-                self.bufs[self.i] = torch.empty(n, dtype=torch.int32).pin_memory()
-            self.bufs[self.i][:n].copy_(ids, non_blocking=True)
-            self.events[self.i].record()
-            item = (step_id, n, self.i)
-            self.i ^= 1
-        else:
-            item = (step_id, n, ids.numpy().astype(np.int32))
-        self.flush()
-        self.pending = item
-
-    def flush(self):
-        if self.pending is None:
-            return
-        step_id, n, ref = self.pending
-        self.pending = None
-        if self.cuda:
-            self.events[ref].synchronize()
-            ids = self.bufs[ref][:n].numpy()
-        else:
-            ids = ref
-        self.t.send_tokens(np.concatenate([np.array([step_id, n], np.int32), ids.astype(np.int32)]))
 
 
 def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_end: bool = True) -> str:
@@ -87,14 +55,11 @@ def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_e
     st = runner.stage
     h = st.cfg.hidden_size
     last = transport.stage == transport.num_stages - 1
-    ret = _TokenReturn(transport, runner.ecfg.max_batch, st.device) if last else None
     tr = get_tracer()
     while True:
         arr = transport.recv_meta()
         if arr.shape[0] == 1 and arr[0] in _MARKERS:
-            if last:
-                ret.flush()
-            else:
+            if not last:
                 transport.send_meta(arr) if arr[0] != STOP else transport.send_stop()
             if arr[0] == STOP:
                 return "stop"
@@ -108,10 +73,19 @@ def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_e
             hidden = transport.recv_hidden(hb.num_tokens, h, st.dtype, st.device)
         out = runner.execute(hb, hidden)
         if last:
-            ret.push(hb.step_id, sample(out, **hb.sampling_args()))
+            # the ids go out as soon as they are sampled; the send is stream-ordered behind them
+            transport.send_ids(sample(out, **hb.sampling_args()))
         else:
             with tr.span("pp.send_hidden", cat="comm", step=hb.step_id):
                 transport.send_hidden(out)
+
+
+class _Issued:
+    """A microbatch stage 0 has issued and not yet completed on the host."""
+    __slots__ = ("step", "sid", "ids")
+
+    def __init__(self, step: Step, sid: int, ids: PendingIds):
+        self.step, self.sid, self.ids = step, sid, ids
 
 
 class PipelineDriver:
@@ -124,18 +98,20 @@ class PipelineDriver:
         self.t = transport
         self.ecfg = ecfg
         self.bm = block_manager
-        # one microbatch per stage keeps every stage busy only if the ring closure (last stage ->
-        # tokens -> stage 0 scheduling) were free; one spare slot hides that turnaround
+        # one microbatch per stage keeps every stage busy only if the ring closure were free;
+        # one spare slot covers the hops
         self.num_slots = num_slots or (ecfg.microbatches if ecfg.microbatches > 0 else transport.num_stages + 1)
         self.scheduler = Scheduler(block_manager, self.num_slots, ecfg.max_batch, ecfg.max_prefill_tokens,
                                    ecfg.max_seq_len)
         self.mcfg = runner.stage.cfg
-        self.inflight: Deque[Tuple[Step, int]] = collections.deque()
-        self.busy = [False] * self.num_slots
+        self.device = runner.stage.device
+        self.inflight: Deque[_Issued] = collections.deque()           # issue order
+        self.per_slot: List[Deque[_Issued]] = [collections.deque() for _ in range(self.num_slots)]
+        self.lookahead = LOOKAHEAD
         self.step_id = 0
         self.num_steps = 0
+        self.num_lookahead = 0
         self.stall_s = 0.0
-        self._flushed = True
 
     def add_request(self, prompt: List[int], params: Optional[SamplingParams] = None,
                     request_id: Optional[str] = None) -> Sequence:
@@ -144,46 +120,65 @@ class PipelineDriver:
         self.scheduler.add(seq)
         return seq
 
-    def _issue(self, slot: int) -> bool:
-        step = self.scheduler.schedule(slot)
-        if step is None:
-            return False
+    def _issue(self, step: Step, ids_dev: Optional[torch.Tensor] = None):
         hb = build_host_batch(step, self.bm, self.ecfg.kv_block_size,
                               None if step.is_prefill else self.runner.max_blocks, self.step_id)
         self.t.send_meta(hb.pack())
-        self._flushed = False
-        out = self.runner.execute(hb)
+        out = self.runner.execute(hb, ids_dev=ids_dev) if ids_dev is not None else self.runner.execute(hb)
         self.t.send_hidden(out)
-        self.inflight.append((step, self.step_id))
-        self.busy[slot] = True
+        # the ids receive is posted right away: receives are matched in issue order
+        it = _Issued(step, self.step_id, self.t.recv_ids(step.size, self.device))
+        self.inflight.append(it)
+        self.per_slot[step.slot].append(it)
         self.step_id += 1
         self.num_steps += 1
-        return True
 
     def _complete_oldest(self) -> List[Sequence]:
-        if len(self.inflight) == 1 and not self._flushed:
-            # the last stage holds the newest step's tokens until the next microbatch arrives;
-            # waiting on that step with nothing else to send would deadlock without a flush
-            self.t.send_meta(_marker(FLUSH))
-            self._flushed = True
-        step, sid = self.inflight.popleft()
+        it = self.inflight.popleft()
+        q = self.per_slot[it.step.slot]
+        assert q[0] is it
+        q.popleft()
         t0 = time.perf_counter()
-        with get_tracer().span("pp.wait_tokens", cat="comm", step=sid):
-            arr = self.t.recv_tokens()
+        with get_tracer().span("pp.wait_tokens", cat="comm", step=it.sid):
+            toks = it.ids.host()
         self.stall_s += time.perf_counter() - t0
-        if int(arr[0]) != sid or int(arr[1]) != step.size:
-            raise RuntimeError(f"pipeline out of order: got step {arr[0]} n={arr[1]}, expected {sid}")
-        done = self.scheduler.complete(step, arr[2:2 + int(arr[1])], time.perf_counter())
-        self.busy[step.slot] = False
-        return done
+        if toks.shape[0] != it.step.size:
+            raise RuntimeError(f"pipeline out of order: step {it.sid} got {toks.shape[0]} ids for {it.step.size} rows")
+        return self.scheduler.complete(it.step, toks, time.perf_counter())
+
+    def _issue_lookahead(self, slot: int) -> bool:
+        """The slot's next decode step on the device ids of its in-flight step (see module doc)."""
+        if not self.lookahead or self.scheduler.waiting:
+            return False
+        q = self.per_slot[slot]
+        if len(q) != 1 or q[0].step.is_prefill:
+            return False
+        step = self.scheduler.schedule_lookahead(slot)
+        if step is None:
+            return False
+        prev = q[0].ids.wait()                   # stream-ordered behind the ids' arrival
+        if step.keep is not None:
+            keep = torch.from_numpy(np.asarray(step.keep, dtype=np.int64))
+            prev = prev.index_select(0, keep.to(prev.device, non_blocking=True) if prev.is_cuda else keep)
+        self._issue(step, ids_dev=prev)
+        self.num_lookahead += 1
+        return True
 
     def poll(self) -> List[Sequence]:
         """One pass over all slots; returns finished sequences."""
         issued = False
         for slot in range(self.num_slots):
-            while self.busy[slot]:
+            if self.per_slot[slot] and self._issue_lookahead(slot):
+                issued = True
+                # at most two steps of a slot in flight: absorb the older one (its ids are needed
+                # on the host only now, one full cycle after they were sampled)
                 self._complete_oldest()
-            if self._issue(slot):
+                continue
+            while self.per_slot[slot]:
+                self._complete_oldest()
+            step = self.scheduler.schedule(slot)
+            if step is not None:
+                self._issue(step)
                 issued = True
         if not issued and self.inflight:
             self._complete_oldest()
@@ -207,8 +202,10 @@ class PipelineDriver:
         if hasattr(self.t, "drain"):
             self.t.drain()
 
-    def generate(self, prompts, params: Optional[SamplingParams] = None) -> List[List[int]]:
-        seqs = [self.add_request(p, params) for p in prompts]
+    def generate(self, prompts, params=None) -> List[List[int]]:
+        """``params``: one SamplingParams for all prompts, or a list (one per prompt)."""
+        plist = params if isinstance(params, (list, tuple)) else [params] * len(prompts)
+        seqs = [self.add_request(p, q) for p, q in zip(prompts, plist)]
         self.run_until_done()
         return [s.output for s in seqs]
 
@@ -245,7 +242,7 @@ def run_loopback_pipeline(ecfg: EngineConfig, num_stages: int, prompts, params: 
                 stage_worker_loop(runners[s], hub.transport(s), stop_on_round_end=False)
         except BaseException as e:  # pragma: no cover - surfaced below
             errors.append(e)
-            hub.tokens.put(np.array([-99, 0], np.int32))
+            hub.ids.put((RuntimeError(f"stage {s} failed"), None))
 
     threads = [threading.Thread(target=follower, args=(s,), daemon=True) for s in range(1, num_stages)]
     for th in threads:

@@ -443,7 +443,8 @@ class WorkerNode:
         else:
             self.stage_runner = StageRunner(stage, ecfg, num_blocks=nb)
             from ..parallel.dist_engine import make_transport
-            transport = make_transport(list(range(world)), stage_idx, ctx.ctrl_group, ctx.data_group, self.device)
+            transport = make_transport(list(range(world)), stage_idx, ctx.ctrl_group, ctx.data_group, self.device,
+                                       ctx.ring_group)
             if stage_idx == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.stage_runner, transport, ecfg, bm)
@@ -466,12 +467,12 @@ class WorkerNode:
         """Count executed microbatches (heartbeat load report) and inject a crash if asked to."""
         inner = runner.execute
 
-        def execute(hb, hidden=None, slot=0):
+        def execute(hb, hidden=None, slot=0, ids_dev=None):
             self._steps += 1
             if self.fail_after_steps and self._steps > self.fail_after_steps:
                 log.error("fault injection: worker exiting after %d steps", self._steps - 1)
                 os._exit(17)
-            return inner(hb, hidden, slot)
+            return inner(hb, hidden, slot, ids_dev)
 
         runner.execute = execute
 

@@ -3,6 +3,7 @@
 Both must reproduce the single-process engine's greedy tokens exactly (same fp32 math,
 layers just split across stages).
 """
+import dataclasses
 import os
 import socket
 
@@ -152,3 +153,23 @@ def test_kv_plan_covers_all_pipeline_slots():
         assert plan_kv_blocks(cfg, 1, e, "cpu") == 16 * slots * per_seq + 2
     e = EngineConfig(model="tiny-llama", device="cpu", max_batch=16, max_seq_len=288, num_workers=8, microbatches=4)
     assert plan_kv_blocks(cfg, 1, e, "cpu") == 16 * 4 * per_seq + 2
+
+
+@pytest.mark.parametrize("stages", [2, 3])
+def test_lookahead_pipeline_with_eos_and_mixed_lengths(monkeypatch, stages):
+    """Device-side ring closure + lookahead: sequences stopping by EOS inside a lookahead step (a
+    throw-away row) and by length at different steps; tokens must match the single engine."""
+    from distributed_llms_amd import config
+    free = LLMEngine(_ecfg()).generate(PROMPTS, SamplingParams(max_new_tokens=12, ignore_eos=True))
+    params = [SamplingParams(max_new_tokens=3 + (i % 10), ignore_eos=(i % 3 == 2)) for i in range(len(PROMPTS))]
+    eos = free[9][5]                                 # prompt 9: max_new 12, EOS honoured
+    monkeypatch.setitem(config.PRESETS, "tiny-llama", dataclasses.replace(config.PRESETS["tiny-llama"],
+                                                                             eos_token_id=eos))
+    exp = LLMEngine(_ecfg()).generate(PROMPTS, params)
+    # some sequences stop by EOS before their length limit, the rest by length
+    assert any(o and o[-1] == eos and len(o) < q.max_new_tokens for o, q in zip(exp, params))
+    assert any(len(o) == q.max_new_tokens for o, q in zip(exp, params))
+    outs, drv, _ = run_loopback_pipeline(_ecfg(), stages, PROMPTS, params)
+    assert outs == exp
+    assert drv.num_lookahead > 0 and not drv.inflight
+    assert drv.bm.num_free() == drv.bm.num_blocks - 1               # every KV block back (scratch kept)
