@@ -14,8 +14,9 @@ torch.cuda.synchronize() on every rank; the max over ranks is reported.
   p50 latency = median request latency (submit -> last token) over the timed rounds
 
 Parallelism: ``pp`` (default, BASELINE config 3: N workers each own a contiguous slice
-of layers; activations hop stage->stage over RCCL/xGMI with N microbatches in flight)
-or ``dp`` (N independent replicas).  Per-GPU batch is fixed, so scaling is weak.
+of layers; activations hop stage->stage over RCCL/xGMI with N + 1 microbatches in flight),
+``dp`` (N independent replicas) or ``tp`` (N-way tensor parallel groups, all-reduce per layer
+half; ``--tp K`` = N/K replicas of K).  The microbatch size is fixed per GPU, so scaling is weak.
 Weights are random-init (seeded, generated on device); prompts are synthetic ids.
 """
 from __future__ import annotations
@@ -44,7 +45,9 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="sequences per GPU per round")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=128)
-    ap.add_argument("--parallelism", choices=["pp", "dp"], default="pp")
+    ap.add_argument("--parallelism", choices=["pp", "dp", "tp"], default="pp")
+    ap.add_argument("--tp", type=int, default=0,
+                    help="tensor-parallel group size for --parallelism tp (default: all ranks)")
     ap.add_argument("--pp", type=int, default=0,
                     help="pipeline depth for --parallelism pp (default: all ranks); world/pp pipelines run as "
                          "data-parallel replicas, e.g. --gpus 8 --pp 4 = 2 pipelines of 4 stages")
@@ -65,6 +68,9 @@ def make_prompts(n, plen, vocab, seed):
 
 
 def _par_name(args, world):
+    if args.parallelism == "tp":
+        tp = args.tp or world
+        return f"tp{tp}" if tp == world else f"dp{world // tp}xtp{tp}"
     pp = args.pp if (args.parallelism == "pp" and args.pp) else (world if args.parallelism == "pp" else 1)
     if args.parallelism == "dp" or pp == 1:
         return f"dp{world}"

@@ -38,12 +38,12 @@ def make_block_manager(num_blocks: int, block_size: int):
 
 
 def build_stage(ecfg: EngineConfig, layer_start: int = 0, layer_end: Optional[int] = None,
-                device: Optional[str] = None, shard_state=None, units=None) -> ModelStage:
+                device: Optional[str] = None, shard_state=None, units=None, tp=None) -> ModelStage:
     mcfg = ecfg.model_config()
     layer_end = mcfg.num_layers if layer_end is None else layer_end
     dev = resolve_device(device or ecfg.device)
     dtype = torch_dtype(ecfg.dtype)
-    stage = ModelStage(mcfg, layer_start, layer_end, device=dev, dtype=dtype, units=units)
+    stage = ModelStage(mcfg, layer_start, layer_end, device=dev, dtype=dtype, units=units, tp=tp)
     if shard_state is not None:
         stage.load_hf_state(shard_state)
     else:
@@ -60,6 +60,12 @@ class LLMEngine:
             raise ValueError("LLMEngine needs a stage owning every layer")
         self.mcfg = self.stage.cfg
         gpu = self.stage.device.type == "cuda"
+        # tensor parallel leader: every step's metadata goes to the group before it runs, and the
+        # followers join its collectives (parallel/tensor_parallel.py); synchronous steps, one
+        # slot, eager launches (collectives stay out of graph capture)
+        self.tp = self.stage.tp if self.stage.tp.enabled else None
+        if self.tp is not None:
+            ecfg = self.ecfg = ecfg.apply_overrides(use_graphs=False, streams=1)
         self.num_slots = max(1, ecfg.streams) if gpu else 1
         self.runner = StageRunner(self.stage, ecfg, num_slots=self.num_slots)
         self.bm = make_block_manager(self.runner.num_blocks, ecfg.kv_block_size)
@@ -75,7 +81,7 @@ class LLMEngine:
         # lookahead: issue a slot's next decode step before completing the one in flight (input
         # ids gathered on device from the in-flight step's samples), so the host's complete /
         # schedule / build work overlaps the GPU instead of idling it (DLLM_LOOKAHEAD=0: off)
-        self.lookahead = gpu and os.environ.get("DLLM_LOOKAHEAD", "1") != "0"
+        self.lookahead = gpu and os.environ.get("DLLM_LOOKAHEAD", "1") != "0" and self.tp is None
         self.num_lookahead = 0
         if gpu:
             dev = self.stage.device
@@ -101,6 +107,8 @@ class LLMEngine:
     def _host_batch(self, step: Step):
         hb = build_host_batch(step, self.bm, self.ecfg.kv_block_size,
                               None if step.is_prefill else self.runner.max_blocks, self.step_id)
+        if self.tp is not None:
+            self.tp.bcast_meta(hb.pack())
         self.step_id += 1
         if step.is_prefill:
             self.num_prefill_tokens += hb.num_tokens
@@ -112,8 +120,14 @@ class LLMEngine:
         """Synchronous execution of one step (CPU path / tests)."""
         hb = self._host_batch(step)
         logits = self.runner.execute(hb, slot=step.slot)
-        ids = sample(logits, **hb.sampling_args())
+        ids = self._sample(logits, hb)
         return ids.cpu().tolist()
+
+    def _sample(self, logits, hb):
+        if self.tp is not None:
+            from ..parallel.tensor_parallel import tp_sample
+            return tp_sample(logits, self.tp, hb.sampling_args())
+        return sample(logits, **hb.sampling_args())
 
     def _launch(self, step: Step, hb, slot: int, ids_src: Optional[torch.Tensor] = None, keep=None):
         """``ids_src`` (lookahead): the in-flight step's sampled ids on the device, rows ``keep``
@@ -130,7 +144,7 @@ class LLMEngine:
                     0, torch.from_numpy(np.asarray(keep, dtype=np.int64)).pin_memory().to(ids_src.device,
                                                                                           non_blocking=True))
             logits = self.runner.execute(hb, slot=slot, ids_dev=ids_dev)
-            ids = sample(logits, **hb.sampling_args())
+            ids = self._sample(logits, hb)
             n = ids.shape[0]
             self.tok_host[slot][i][:n].copy_(ids, non_blocking=True)
             self.events[slot][i].record(s)
@@ -199,6 +213,17 @@ class LLMEngine:
             done.extend(self.step())
         done.extend(self.scheduler.pop_finished())
         return done
+
+    def end_round(self):
+        """Tensor-parallel leader: release the followers' step loops (bench round barrier)."""
+        if self.tp is not None:
+            from ..parallel.tensor_parallel import ROUND_END
+            self.tp.bcast_meta(np.array([ROUND_END], np.int32))
+
+    def shutdown(self):
+        if self.tp is not None:
+            from ..parallel.tensor_parallel import STOP
+            self.tp.bcast_meta(np.array([STOP], np.int32))
 
     def generate(self, prompts: Iterable[List[int]], params=None) -> List[List[int]]:
         """``params``: one SamplingParams for all prompts, or a list (one per prompt)."""

@@ -19,8 +19,10 @@ from .graphs import DecodeGraphRunner
 log = logging.getLogger("dllm.runner")
 
 
-def plan_kv_blocks(mcfg: ModelConfig, num_layers: int, ecfg: EngineConfig, device) -> int:
-    """KV blocks for a stage: enough for max_batch x max_seq_len (+ scratch), capped by free HBM."""
+def plan_kv_blocks(mcfg: ModelConfig, num_layers: int, ecfg: EngineConfig, device,
+                   num_kv_heads: Optional[int] = None) -> int:
+    """KV blocks for a stage: enough for max_batch x max_seq_len (+ scratch), capped by free HBM.
+    ``num_kv_heads``: the heads this rank caches (its share under tensor parallelism)."""
     bs = ecfg.kv_block_size
     if ecfg.num_kv_blocks > 0:
         return ecfg.num_kv_blocks
@@ -28,7 +30,7 @@ def plan_kv_blocks(mcfg: ModelConfig, num_layers: int, ecfg: EngineConfig, devic
     # microbatch slots in flight: the pipeline driver runs pp + 1 (parallel/pipeline.py)
     slots = ecfg.microbatches or (ecfg.num_workers + 1 if ecfg.num_workers > 1 else 1)
     want = ecfg.max_batch * slots * per_seq + 2
-    per_block = max(1, KVCache.bytes_per_block(num_layers, mcfg.num_kv_heads, mcfg.head_dim, bs))
+    per_block = max(1, KVCache.bytes_per_block(num_layers, num_kv_heads or mcfg.num_kv_heads, mcfg.head_dim, bs))
     dev = torch.device(device)
     if dev.type == "cuda":
         free, _total = torch.cuda.mem_get_info(dev)
@@ -53,7 +55,7 @@ class StageRunner:
         if stage.device.type == "cuda":
             enable_tuned_gemms()          # before any graph capture fixes the GEMM solutions
         self.block_size = ecfg.kv_block_size
-        nb = num_blocks or plan_kv_blocks(stage.cfg, stage.num_layers, ecfg, stage.device)
+        nb = num_blocks or plan_kv_blocks(stage.cfg, stage.num_layers, ecfg, stage.device, stage.hkv)
         stage.allocate_kv(nb, self.block_size)
         self.num_blocks = nb
         self.max_blocks = -(-ecfg.max_seq_len // self.block_size)

@@ -82,7 +82,16 @@ class ModelStage:
     stage hand-off is always the closed residual stream (one [T, H] tensor)."""
 
     def __init__(self, cfg: ModelConfig, layer_start: int, layer_end: int, device="cpu",
-                 dtype=torch.bfloat16, units: Optional[tuple] = None):
+                 dtype=torch.bfloat16, units: Optional[tuple] = None, tp=None):
+        """``tp``: a :class:`~distributed_llms_amd.parallel.tensor_parallel.TPGroup` -- this rank then
+        holds its column / row / vocab shard of every layer (parallel/tensor_parallel.py)."""
+        from ..parallel.tensor_parallel import TPGroup, check_divisible
+        self.tp = tp if tp is not None else TPGroup(0, 1)
+        check_divisible(cfg, self.tp.size)
+        # heads this rank computes (all of them without TP)
+        self.hq = cfg.num_heads // self.tp.size
+        self.hkv = cfg.num_kv_heads // self.tp.size
+        self.q_size_local = self.hq * cfg.head_dim
         if units is None:
             units = (2 * layer_start, 2 * layer_end)
         u0, u1 = int(units[0]), int(units[1])
@@ -122,19 +131,39 @@ class ModelStage:
     def needs_embed(self) -> bool:
         return self.is_first or (self.is_last and self.cfg.tie_embeddings)
 
+    def _shard(self):
+        """Keep this tensor-parallel rank's shard of every layer and of the LM head (the full
+        tensors are generated / loaded first, so shards are slices of the same model)."""
+        if not self.tp.enabled:
+            return
+        from ..parallel.tensor_parallel import shard_block, shard_vocab
+        r, n = self.tp.rank, self.tp.size
+        self.layers = [shard_block(self.cfg, lw, r, n) for lw in self.layers]
+        if self.is_last:
+            self.head["lm_head_tp"] = shard_vocab(self.lm_head_weight(full=True), r, n)
+            self.head.pop("lm_head", None)
+
     def init_synthetic(self, seed: int = 0) -> "ModelStage":
         """Seeded random-init weights generated directly on the stage's device."""
         cfg = self.cfg
         self.layers = []
         for l in range(self.layer_start, self.layer_end):
             shapes = {n: s for n, s in W.block_shapes(cfg).items() if self._keep(l, n)}
-            self.layers.append({n: W.synth_tensor(seed, l, n, s, self.dtype, self.device) for n, s in shapes.items()})
+            lw = {n: W.synth_tensor(seed, l, n, s, self.dtype, self.device) for n, s in shapes.items()}
+            if self.tp.enabled:
+                from ..parallel.tensor_parallel import shard_block
+                lw = shard_block(cfg, lw, self.tp.rank, self.tp.size)     # one full layer at a time
+            self.layers.append(lw)
         if self.needs_embed():
             self.embed = W.synth_embed(cfg, seed, self.dtype, self.device)
             if not self.is_first:
                 self.embed.pop("pos_embed", None)
         if self.is_last:
             self.head = W.synth_head(cfg, seed, self.dtype, self.device)
+            if self.tp.enabled:
+                from ..parallel.tensor_parallel import shard_vocab
+                self.head["lm_head_tp"] = shard_vocab(self.lm_head_weight(full=True), self.tp.rank, self.tp.size)
+                self.head.pop("lm_head", None)
         return self
 
     def load_hf_state(self, sd: Dict[str, torch.Tensor]) -> "ModelStage":
@@ -150,6 +179,7 @@ class ModelStage:
             self.embed = {k: conv(sd[n]) for k, n in names.items()}
         if self.is_last:
             self.head = {k: conv(sd[n]) for k, n in W.hf_head_names(cfg).items()}
+        self._shard()
         return self
 
     def weight_bytes(self) -> int:
@@ -160,11 +190,14 @@ class ModelStage:
 
     def allocate_kv(self, num_blocks: int, block_size: int) -> KVCache:
         cfg = self.cfg
-        self.kv = KVCache(self.num_layers, num_blocks, cfg.num_kv_heads, cfg.head_dim, block_size,
+        self.kv = KVCache(self.num_layers, num_blocks, self.hkv, cfg.head_dim, block_size,
                           self.dtype, self.device)
         return self.kv
 
-    def lm_head_weight(self) -> torch.Tensor:
+    def lm_head_weight(self, full: bool = False) -> torch.Tensor:
+        """The LM head rows this rank computes (its vocab shard under TP; ``full``: all rows)."""
+        if not full and "lm_head_tp" in self.head:
+            return self.head["lm_head_tp"]
         return self.embed["embed"] if self.cfg.tie_embeddings else self.head["lm_head"]
 
     # --------------------------------------------------------------- forward
@@ -187,26 +220,29 @@ class ModelStage:
             qkv = qkv.materialize()
         if fused:
             o = ops.paged_attention_decode_rope(qkv, meta.positions, self.cos_sin, k_cache, v_cache, meta.slot_mapping,
-                                                meta.block_tables, meta.seq_lens, cfg.num_heads, cfg.num_kv_heads,
+                                                meta.block_tables, meta.seq_lens, self.hq, self.hkv,
                                                 cfg.head_dim, self.scale, max_ctx=meta.max_ctx or None,
                                                 workspace=meta.attn_workspace)
-            return o.view(o.shape[0], cfg.q_size)
+            return o.view(o.shape[0], self.q_size_local)
         q = ops.rope_cache_append(qkv, meta.positions, self.cos_sin, k_cache, v_cache, meta.slot_mapping,
-                                  cfg.num_heads, cfg.num_kv_heads, cfg.head_dim)
+                                  self.hq, self.hkv, cfg.head_dim)
         if meta.is_prefill:
             o = ops.paged_attention_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_seqlens_q,
                                             meta.seq_lens, self.scale, max_q_len=meta.max_q_len)
         else:
             o = ops.paged_attention_decode(q, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.scale,
                                            max_ctx=meta.max_ctx or None, workspace=meta.attn_workspace)
-        return o.view(o.shape[0], cfg.q_size)
+        return o.view(o.shape[0], self.q_size_local)
 
     def _mlp(self, h: torch.Tensor, lw: Dict[str, torch.Tensor]) -> torch.Tensor:
         if self.cfg.is_moe:
-            return ops.moe_forward(h, lw["router"], lw["experts_gate_up"], lw["experts_down"],
-                                   self.cfg.experts_per_token)
+            out = ops.moe_forward(h, lw["router"], lw["experts_gate_up"], lw["experts_down"],
+                                  self.cfg.experts_per_token)
+            return self.tp.all_reduce_(out) if self.tp.enabled else out
         # defer: the down projection's split-K reduce is fused into the next residual-add + RMSNorm
-        return ops.linear(ops.linear_swiglu(h, lw["w_gate_up"]), lw["w_down"], defer=True)
+        # (under TP the partial [T, H] is all-reduced first, so it is materialised)
+        out = ops.linear(ops.linear_swiglu(h, lw["w_gate_up"]), lw["w_down"], defer=not self.tp.enabled)
+        return self.tp.all_reduce_(out) if self.tp.enabled else out
 
     def _units(self):
         for u in range(self.unit_start, self.unit_end):
@@ -227,7 +263,11 @@ class ModelStage:
             if is_attn:
                 a = self._attention(ops.linear(x, lw["wqkv"], defer=DEFER_QKV), self.kv_index[l], meta)
                 # defer: a split-K o-projection's reduce is fused into the MLP half's add + RMSNorm
-                h = ops.linear(a, lw["wo"], defer=DEFER_O)
+                # (TP: row-parallel partial sums, all-reduced over the group)
+                if self.tp.enabled:
+                    h = self.tp.all_reduce_(ops.linear(a, lw["wo"]))
+                else:
+                    h = ops.linear(a, lw["wo"], defer=DEFER_O)
             else:
                 h = self._mlp(x, lw)
         if isinstance(h, ops.gemm.SplitKPartial):

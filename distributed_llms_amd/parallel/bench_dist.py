@@ -20,15 +20,18 @@ def _sync(ctx):
 
 def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=None):
     pp = (getattr(args, "pp", 0) or None) if args.parallelism == "pp" else 1
-    ctx = init_distributed(pp=pp)
+    tp = (getattr(args, "tp", 0) or int(os.environ.get("WORLD_SIZE", "1"))) if args.parallelism == "tp" else 1
+    ctx = init_distributed(pp=pp, tp=tp)
     world = ctx.world
     # pipeline: prefill in ~8K-token microbatches (M large enough for full-rate GEMMs) so the
     # fill/drain bubble of the prefill phase is (pp-1) x ~8K-token stage times, not (pp-1) x a
     # whole slot's prompts (256 x 128 = 32K tokens per microbatch would idle ~15 % of a round at pp8)
     pf_tokens = max(16384, args.batch * args.prompt_len) if ctx.pp == 1 else max(8192, args.prompt_len)
+    # tensor parallel: synchronous eager steps (collectives stay out of graph capture)
     ecfg = EngineConfig(model=f"synthetic:{args.model}", max_batch=args.batch,
                         max_prefill_tokens=pf_tokens,
-                        max_seq_len=args.prompt_len + args.gen_len + 32, use_graphs=not args.no_graphs,
+                        max_seq_len=args.prompt_len + args.gen_len + 32,
+                        use_graphs=not args.no_graphs and ctx.tp == 1,
                         num_workers=ctx.pp, seed=args.seed)
     t0 = time.perf_counter()
     role = RankRole(ctx, ecfg)

@@ -36,6 +36,8 @@ class DistContext:
     device: str
     data_group: object = None      # None = the default (RCCL) group
     ring_groups: tuple = ()        # per pipeline: the {stage 0, last stage} group of the ids ring closure
+    tp: int = 1                    # tensor-parallel degree (pp == 1 when > 1)
+    tpg: object = None             # this rank's TPGroup (parallel/tensor_parallel.py)
 
     @property
     def host_staged(self) -> bool:
@@ -60,7 +62,7 @@ class DistContext:
 
 
 def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
-                     timeout_s: float = 1800) -> DistContext:
+                     timeout_s: float = 1800, tp: int = 1) -> DistContext:
     """Environment knobs (tests / rehearsal only):
       DLLM_SHARE_GPU=1       ranks share the visible GPUs round-robin (local_rank % device_count)
       DLLM_DATA_BACKEND=gloo activations go host-staged over a gloo group instead of RCCL -- the
@@ -85,6 +87,25 @@ def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
         dist.init_process_group(**kw)
     ctrl = dist.new_group(backend="gloo", timeout=tmo) if backend != "gloo" else dist.group.WORLD
     data = dist.new_group(backend="gloo", timeout=tmo) if host_staged else None
+    tp = max(1, int(tp or 1))
+    if tp > 1:
+        # tensor parallel groups of `tp` consecutive ranks (dp = world / tp replicas); combining
+        # them with a layer pipeline is not supported yet
+        if pp not in (None, 1):
+            raise ValueError("tensor parallelism with pp > 1 is not supported")
+        if world % tp:
+            raise ValueError(f"world {world} not divisible by tp {tp}")
+        from .tensor_parallel import TPGroup
+        data_backend = "gloo" if (host_staged or backend == "gloo") else "nccl"
+        tpg = None
+        for d in range(world // tp):
+            ranks = list(range(d * tp, (d + 1) * tp))
+            g = dist.new_group(ranks=ranks, backend=data_backend, timeout=tmo)
+            c = dist.new_group(ranks=ranks, backend="gloo", timeout=tmo)
+            if rank in ranks:
+                tpg = TPGroup(rank - d * tp, tp, g, c, d * tp)
+        return DistContext(rank, world, local_rank, world // tp, 1, ctrl,
+                           f"cuda:{dev_idx}" if use_gpu else "cpu", data, (), tp, tpg)
     pp = pp or world
     if world % pp:
         raise ValueError(f"world {world} not divisible by pp {pp}")
@@ -125,6 +146,13 @@ class RankRole:
         self.ctx = ctx
         self.ecfg = ecfg
         mcfg = ecfg.model_config()
+        self.engine = None
+        self.driver = None
+        self.runner = None
+        self.tp_follower = False
+        if ctx.tp > 1:
+            self._init_tp(ctx, ecfg, mcfg, hf_state)
+            return
         self.plan = plan_units(mcfg, ctx.pp, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2))
         a, b = self.plan.ranges[ctx.stage]
         stage = build_stage(ecfg, a, b, device=ctx.device, shard_state=hf_state,
@@ -147,6 +175,22 @@ class RankRole:
         log.info("rank %d: pipeline %d stage %d layers [%d,%d) kv_blocks=%d", ctx.rank, ctx.pipeline_id,
                  ctx.stage, a, b, nb)
 
+    def _init_tp(self, ctx, ecfg, mcfg, hf_state):
+        """dp x tp: every rank holds a TP shard of all layers; group rank 0 runs the engine."""
+        from .planner import StagePlan
+        stage = build_stage(ecfg, 0, mcfg.num_layers, device=ctx.device, shard_state=hf_state, tp=ctx.tpg)
+        nb = plan_kv_blocks(mcfg, stage.num_layers, ecfg, stage.device, stage.hkv)
+        nb = agree_min(ctx, nb)        # the leader's block ids index every rank's cache
+        e = ecfg.apply_overrides(num_kv_blocks=nb, use_graphs=False)
+        self.plan = StagePlan(((0, mcfg.num_layers),), (0.0,))
+        if ctx.tpg.rank == 0:
+            self.engine = LLMEngine(e, stage)
+        else:
+            self.runner = StageRunner(stage, e, num_blocks=nb)
+            self.tp_follower = True
+        log.info("rank %d: tp rank %d/%d of replica %d, kv_blocks=%d", ctx.rank, ctx.tpg.rank, ctx.tp,
+                 ctx.rank // ctx.tp, nb)
+
     @property
     def is_driver(self) -> bool:
         return self.engine is not None or self.driver is not None
@@ -157,8 +201,14 @@ class RankRole:
     def run_round(self):
         """Drivers: run all queued requests to completion, then release followers.
         Followers: serve microbatches until the driver's ROUND_END."""
+        if self.tp_follower:
+            from .tensor_parallel import tp_follower_loop
+            tp_follower_loop(self.runner, self.ctx.tpg, stop_on_round_end=True)
+            return []
         if self.engine is not None:
-            return self.engine.run_until_done()
+            done = self.engine.run_until_done()
+            self.engine.end_round()
+            return done
         if self.driver is not None:
             done = self.driver.run_until_done()
             self.driver.end_round()
@@ -167,7 +217,12 @@ class RankRole:
         return []
 
     def shutdown(self):
-        if self.driver is not None:
+        if self.tp_follower:
+            from .tensor_parallel import tp_follower_loop
+            tp_follower_loop(self.runner, self.ctx.tpg, stop_on_round_end=False)
+        elif self.engine is not None:
+            self.engine.shutdown()
+        elif self.driver is not None:
             self.driver.shutdown()
         elif self.runner is not None:
             stage_worker_loop(self.runner, self.transport, stop_on_round_end=False)

@@ -26,7 +26,7 @@ def _json_lines(out):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("n,par,trace", [(2, "pp", True), (3, "pp", False), (2, "dp", False)])
+@pytest.mark.parametrize("n,par,trace", [(2, "pp", True), (3, "pp", False), (2, "dp", False), (2, "tp", False)])
 def test_torchrun_bench_cpu(n, par, trace, tmp_path):
     env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -45,6 +45,8 @@ def test_torchrun_bench_cpu(n, par, trace, tmp_path):
     if par == "pp":
         assert rec["microbatch_slots"] == n + 1
         assert rec["config"]["global_batch"] == 3 * (n + 1)
+    if par == "tp":                 # one TP group: one engine's batch
+        assert rec["config"]["global_batch"] == 3
     if trace:   # every rank wrote a timeline; every stage reports its busy fraction
         assert sorted(os.listdir(tmp_path)) == [f"trace_rank{r}.json" for r in range(n)]
         assert len(rec["stage_busy_frac"]) == n and all(0 < b <= 1.0 for b in rec["stage_busy_frac"])
