@@ -47,7 +47,8 @@ def parse(argv=None):
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--parallelism", choices=["pp", "dp", "tp"], default="pp")
     ap.add_argument("--tp", type=int, default=0,
-                    help="tensor-parallel group size for --parallelism tp (default: all ranks)")
+                    help="tensor-parallel group size (--parallelism tp: default all ranks; with pp: "
+                         "every pipeline stage is a TP group of this size, dp x pp x tp)")
     ap.add_argument("--pp", type=int, default=0,
                     help="pipeline depth for --parallelism pp (default: all ranks); world/pp pipelines run as "
                          "data-parallel replicas, e.g. --gpus 8 --pp 4 = 2 pipelines of 4 stages")
@@ -68,13 +69,15 @@ def make_prompts(n, plen, vocab, seed):
 
 
 def _par_name(args, world):
-    if args.parallelism == "tp":
-        tp = args.tp or world
-        return f"tp{tp}" if tp == world else f"dp{world // tp}xtp{tp}"
-    pp = args.pp if (args.parallelism == "pp" and args.pp) else (world if args.parallelism == "pp" else 1)
-    if args.parallelism == "dp" or pp == 1:
-        return f"dp{world}"
-    return f"pp{pp}" if pp == world else f"dp{world // pp}xpp{pp}"
+    tp = args.tp or (world if args.parallelism == "tp" else 1)
+    if args.parallelism == "pp":
+        pp = args.pp or world // tp
+    else:
+        pp = 1
+    dp = world // (pp * tp)
+    parts = [f"dp{dp}" if dp > 1 else "", f"pp{pp}" if pp > 1 else "", f"tp{tp}" if tp > 1 else ""]
+    name = "x".join(p for p in parts if p)
+    return name or f"dp{world}"
 
 
 def emit(args, world, elapsed, lat, extra, global_batch=None):

@@ -27,6 +27,11 @@ log = logging.getLogger("dllm.dist")
 
 @dataclass
 class DistContext:
+    """Rank layout: ``rank = (d * pp + s) * tp + t`` -- replica d, pipeline stage s, tensor-
+    parallel rank t.  Lane (d, t) is the chain of the t-th TP ranks of replica d's stages: the
+    activations and the sampled-ids ring of TP rank t travel along it (after a stage's
+    all-reduce every TP rank holds the same hidden state, so each lane carries its own copy over
+    its own xGMI links)."""
     rank: int
     world: int
     local_rank: int
@@ -35,26 +40,35 @@ class DistContext:
     ctrl_group: object
     device: str
     data_group: object = None      # None = the default (RCCL) group
-    ring_groups: tuple = ()        # per pipeline: the {stage 0, last stage} group of the ids ring closure
-    tp: int = 1                    # tensor-parallel degree (pp == 1 when > 1)
-    tpg: object = None             # this rank's TPGroup (parallel/tensor_parallel.py)
+    ring_groups: tuple = ()        # per lane: the {stage 0, last stage} group of the ids ring closure
+    tp: int = 1                    # tensor-parallel degree
+    tpg: object = None             # this rank's TPGroup (parallel/tensor_parallel.py), None if tp == 1
 
     @property
     def host_staged(self) -> bool:
         return self.data_group is not None
 
     @property
+    def replica(self) -> int:
+        return self.rank // (self.pp * self.tp)
+
+    @property
+    def tp_rank(self) -> int:
+        return self.rank % self.tp
+
+    @property
     def pipeline_id(self) -> int:
-        return self.rank // self.pp
+        """Lane index (replica * tp + TP rank): one PipelineDriver per lane 0 of each replica."""
+        return self.replica * self.tp + self.tp_rank
 
     @property
     def stage(self) -> int:
-        return self.rank % self.pp
+        return (self.rank // self.tp) % self.pp
 
     @property
     def pipeline_ranks(self):
-        p = self.pipeline_id
-        return list(range(p * self.pp, (p + 1) * self.pp))
+        d, t = self.replica, self.tp_rank
+        return [(d * self.pp + s) * self.tp + t for s in range(self.pp)]
 
     @property
     def ring_group(self):
@@ -63,7 +77,9 @@ class DistContext:
 
 def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
                      timeout_s: float = 1800, tp: int = 1) -> DistContext:
-    """Environment knobs (tests / rehearsal only):
+    """dp x pp x tp over the launched world (dp = world / (pp * tp); pp None = world / tp).
+
+    Environment knobs (tests / rehearsal only):
       DLLM_SHARE_GPU=1       ranks share the visible GPUs round-robin (local_rank % device_count)
       DLLM_DATA_BACKEND=gloo activations go host-staged over a gloo group instead of RCCL -- the
                              cross-host TCP fallback, and the only way to run several GPU ranks on
@@ -88,34 +104,32 @@ def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
     ctrl = dist.new_group(backend="gloo", timeout=tmo) if backend != "gloo" else dist.group.WORLD
     data = dist.new_group(backend="gloo", timeout=tmo) if host_staged else None
     tp = max(1, int(tp or 1))
+    if world % tp:
+        raise ValueError(f"world {world} not divisible by tp {tp}")
+    pp = pp or world // tp
+    if world % (pp * tp):
+        raise ValueError(f"world {world} not divisible by pp {pp} x tp {tp}")
+    dp = world // (pp * tp)
+    p2p_backend = "gloo" if (host_staged or backend == "gloo") else "nccl"
+    # new_group is collective: every rank creates every group, in the same order
+    tpg = None
     if tp > 1:
-        # tensor parallel groups of `tp` consecutive ranks (dp = world / tp replicas); combining
-        # them with a layer pipeline is not supported yet
-        if pp not in (None, 1):
-            raise ValueError("tensor parallelism with pp > 1 is not supported")
-        if world % tp:
-            raise ValueError(f"world {world} not divisible by tp {tp}")
         from .tensor_parallel import TPGroup
-        data_backend = "gloo" if (host_staged or backend == "gloo") else "nccl"
-        tpg = None
-        for d in range(world // tp):
-            ranks = list(range(d * tp, (d + 1) * tp))
-            g = dist.new_group(ranks=ranks, backend=data_backend, timeout=tmo)
-            c = dist.new_group(ranks=ranks, backend="gloo", timeout=tmo)
-            if rank in ranks:
-                tpg = TPGroup(rank - d * tp, tp, g, c, d * tp)
-        return DistContext(rank, world, local_rank, world // tp, 1, ctrl,
-                           f"cuda:{dev_idx}" if use_gpu else "cpu", data, (), tp, tpg)
-    pp = pp or world
-    if world % pp:
-        raise ValueError(f"world {world} not divisible by pp {pp}")
-    # one {first, last} group per pipeline for the sampled-ids ring closure (new_group is
-    # collective: every rank creates every pipeline's group, in the same order)
-    ring_backend = "gloo" if (host_staged or backend == "gloo") else "nccl"
-    rings = tuple(dist.new_group(ranks=[p * pp, p * pp + pp - 1], backend=ring_backend, timeout=tmo)
-                  for p in range(world // pp)) if pp > 1 else ()
-    return DistContext(rank, world, local_rank, world // pp, pp, ctrl,
-                       f"cuda:{dev_idx}" if use_gpu else "cpu", data, rings)
+        for d in range(dp):
+            for s in range(pp):
+                ranks = [(d * pp + s) * tp + t for t in range(tp)]
+                g = dist.new_group(ranks=ranks, backend=p2p_backend, timeout=tmo)
+                c = dist.new_group(ranks=ranks, backend="gloo", timeout=tmo)
+                if rank in ranks:
+                    tpg = TPGroup(rank - ranks[0], tp, g, c, ranks[0])
+    # one {first, last} group per lane for the sampled-ids ring closure
+    rings = ()
+    if pp > 1:
+        rings = tuple(dist.new_group(ranks=[(d * pp) * tp + t, (d * pp + pp - 1) * tp + t], backend=p2p_backend,
+                                     timeout=tmo)
+                      for d in range(dp) for t in range(tp))
+    return DistContext(rank, world, local_rank, dp, pp, ctrl, f"cuda:{dev_idx}" if use_gpu else "cpu", data,
+                       rings, tp, tpg)
 
 
 def make_transport(ranks, stage: int, ctrl_group, data_group, device: str, ring_group=None):
@@ -140,7 +154,8 @@ def agree_max(ctx: DistContext, value: float) -> float:
 
 
 class RankRole:
-    """What this rank runs: a full engine (pp == 1), a pipeline driver (stage 0), or a follower."""
+    """What this rank runs: a full engine (pp == 1), a pipeline driver (stage 0, TP rank 0), a
+    stage-0 TP peer of the driver, a pipeline follower, or a TP follower (pp == 1)."""
 
     def __init__(self, ctx: DistContext, ecfg: EngineConfig, hf_state=None):
         self.ctx = ctx
@@ -149,19 +164,19 @@ class RankRole:
         self.engine = None
         self.driver = None
         self.runner = None
-        self.tp_follower = False
-        if ctx.tp > 1:
+        self.tp_follower = False        # dp x tp follower (pp == 1)
+        self.lane_follower = False      # pp x tp: stage 0, TP rank > 0
+        if ctx.tp > 1 and ctx.pp == 1:
             self._init_tp(ctx, ecfg, mcfg, hf_state)
             return
         self.plan = plan_units(mcfg, ctx.pp, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2))
         a, b = self.plan.ranges[ctx.stage]
         stage = build_stage(ecfg, a, b, device=ctx.device, shard_state=hf_state,
-                            units=self.plan.unit_range(ctx.stage))
-        nb = plan_kv_blocks(mcfg, stage.num_layers, ecfg, stage.device)
+                            units=self.plan.unit_range(ctx.stage), tp=ctx.tpg)
+        nb = plan_kv_blocks(mcfg, stage.num_layers, ecfg, stage.device, stage.hkv)
         nb = agree_min(ctx, nb)        # every stage of a pipeline must hold the same block ids
-        self.engine = None
-        self.driver = None
-        self.runner = None
+        if ctx.tp > 1:
+            ecfg = ecfg.apply_overrides(use_graphs=False)      # collectives stay out of graph capture
         if ctx.pp == 1:
             ecfg1 = ecfg.apply_overrides(num_kv_blocks=nb)
             self.engine = LLMEngine(ecfg1, stage)
@@ -169,11 +184,13 @@ class RankRole:
             self.runner = StageRunner(stage, ecfg, num_blocks=nb)
             self.transport = make_transport(ctx.pipeline_ranks, ctx.stage, ctx.ctrl_group, ctx.data_group,
                                             ctx.device, ctx.ring_group)
-            if ctx.stage == 0:
+            if ctx.stage == 0 and ctx.tp_rank == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.runner, self.transport, ecfg, bm)
-        log.info("rank %d: pipeline %d stage %d layers [%d,%d) kv_blocks=%d", ctx.rank, ctx.pipeline_id,
-                 ctx.stage, a, b, nb)
+            elif ctx.stage == 0:
+                self.lane_follower = True
+        log.info("rank %d: lane %d stage %d tp %d/%d layers [%d,%d) kv_blocks=%d", ctx.rank, ctx.pipeline_id,
+                 ctx.stage, ctx.tp_rank, ctx.tp, a, b, nb)
 
     def _init_tp(self, ctx, ecfg, mcfg, hf_state):
         """dp x tp: every rank holds a TP shard of all layers; group rank 0 runs the engine."""
@@ -205,6 +222,10 @@ class RankRole:
             from .tensor_parallel import tp_follower_loop
             tp_follower_loop(self.runner, self.ctx.tpg, stop_on_round_end=True)
             return []
+        if self.lane_follower:
+            from .pipeline import stage0_tp_follower_loop
+            stage0_tp_follower_loop(self.runner, self.transport, self.ctx.tpg, stop_on_round_end=True)
+            return []
         if self.engine is not None:
             done = self.engine.run_until_done()
             self.engine.end_round()
@@ -220,6 +241,9 @@ class RankRole:
         if self.tp_follower:
             from .tensor_parallel import tp_follower_loop
             tp_follower_loop(self.runner, self.ctx.tpg, stop_on_round_end=False)
+        elif self.lane_follower:
+            from .pipeline import stage0_tp_follower_loop
+            stage0_tp_follower_loop(self.runner, self.transport, self.ctx.tpg, stop_on_round_end=False)
         elif self.engine is not None:
             self.engine.shutdown()
         elif self.driver is not None:

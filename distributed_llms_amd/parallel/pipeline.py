@@ -74,7 +74,11 @@ def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_e
         out = runner.execute(hb, hidden)
         if last:
             # the ids go out as soon as they are sampled; the send is stream-ordered behind them
-            transport.send_ids(sample(out, **hb.sampling_args()))
+            if st.tp.enabled:       # vocab-parallel head: every TP rank derives the same ids
+                from .tensor_parallel import tp_sample
+                transport.send_ids(tp_sample(out, st.tp, hb.sampling_args()))
+            else:
+                transport.send_ids(sample(out, **hb.sampling_args()))
         else:
             with tr.span("pp.send_hidden", cat="comm", step=hb.step_id):
                 transport.send_hidden(out)
@@ -108,6 +112,8 @@ class PipelineDriver:
         self.inflight: Deque[_Issued] = collections.deque()           # issue order
         self.per_slot: List[Deque[_Issued]] = [collections.deque() for _ in range(self.num_slots)]
         self.lookahead = LOOKAHEAD
+        # pp x tp: the stage-0 TP peers replay every issue on their own lanes
+        self.tp = runner.stage.tp if runner.stage.tp.enabled else None
         self.step_id = 0
         self.num_steps = 0
         self.num_lookahead = 0
@@ -123,6 +129,8 @@ class PipelineDriver:
     def _issue(self, step: Step, ids_dev: Optional[torch.Tensor] = None):
         hb = build_host_batch(step, self.bm, self.ecfg.kv_block_size,
                               None if step.is_prefill else self.runner.max_blocks, self.step_id)
+        if self.tp is not None:
+            self.tp.bcast_meta(_tp_issue_msg(hb.pack(), ids_dev is not None, step.keep))
         self.t.send_meta(hb.pack())
         out = self.runner.execute(hb, ids_dev=ids_dev) if ids_dev is not None else self.runner.execute(hb)
         self.t.send_hidden(out)
@@ -195,9 +203,13 @@ class PipelineDriver:
         return done
 
     def end_round(self):
+        if self.tp is not None:
+            self.tp.bcast_meta(_marker(ROUND_END))
         self.t.send_meta(_marker(ROUND_END))
 
     def shutdown(self):
+        if self.tp is not None:
+            self.tp.bcast_meta(_marker(STOP))
         self.t.send_stop()
         if hasattr(self.t, "drain"):
             self.t.drain()
@@ -208,6 +220,51 @@ class PipelineDriver:
         seqs = [self.add_request(p, q) for p, q in zip(prompts, plist)]
         self.run_until_done()
         return [s.output for s in seqs]
+
+
+def _tp_issue_msg(packed: np.ndarray, lookahead: bool, keep) -> np.ndarray:
+    """[kind, n_keep, keep..., packed HostBatch...]: kind 1 = ids in the batch, 2 = lookahead on
+    the device ids of the slot's previous step (n_keep -1: every row)."""
+    keep = np.asarray(keep, dtype=np.int32) if keep is not None else np.zeros(0, np.int32)
+    head = np.array([2 if lookahead else 1, keep.shape[0] if keep.shape[0] else -1], np.int32)
+    return np.concatenate([head, keep, packed])
+
+
+def stage0_tp_follower_loop(runner: StageRunner, transport: Transport, tp, stop_on_round_end: bool = True) -> str:
+    """pp x tp, stage 0, TP rank > 0: replay each microbatch the driver (TP rank 0 of the same
+    stage) issues -- same metadata, same lookahead -- on this rank's own lane: its own activation
+    hop to the next stage's TP rank, its own ids ring from the last stage's TP rank."""
+    newest = {}                                   # slot -> PendingIds of its newest step
+    while True:
+        msg = tp.bcast_meta(None)
+        if msg.shape[0] == 1 and int(msg[0]) in _MARKERS:
+            if int(msg[0]) == STOP:
+                transport.send_stop()
+                if hasattr(transport, "drain"):
+                    transport.drain()
+                return "stop"
+            transport.send_meta(msg.copy())
+            if stop_on_round_end:
+                return "round"
+            continue
+        kind, n_keep = int(msg[0]), int(msg[1])
+        keep = msg[2:2 + max(n_keep, 0)].astype(np.int64)
+        packed = msg[2 + max(n_keep, 0):].copy()
+        hb = HostBatch.unpack(packed)
+        transport.send_meta(packed)
+        if kind == 2:
+            prev = newest[hb.slot].wait()
+            if n_keep >= 0:
+                k = torch.from_numpy(keep)
+                prev = prev.index_select(0, k.to(prev.device) if prev.is_cuda else k)
+            out = runner.execute(hb, ids_dev=prev)
+        else:
+            out = runner.execute(hb)
+        transport.send_hidden(out)
+        old = newest.get(hb.slot)
+        newest[hb.slot] = transport.recv_ids(hb.num_seqs, runner.stage.device)
+        if old is not None and not runner.stage.device.type == "cuda":
+            old.wait()                           # CPU (gloo): let the receive complete before dropping it
 
 
 def run_loopback_pipeline(ecfg: EngineConfig, num_stages: int, prompts, params: SamplingParams,

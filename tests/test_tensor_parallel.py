@@ -80,15 +80,15 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, tp, model, port, out_q):
+def _rank_main(rank, world, tp, model, port, out_q, pp=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     import torch.distributed as dist
     from distributed_llms_amd.parallel.dist_engine import RankRole, init_distributed
     try:
-        ctx = init_distributed(pp=1, backend="gloo", tp=tp)
-        role = RankRole(ctx, _ecfg(model))
+        ctx = init_distributed(pp=pp, backend="gloo", tp=tp)
+        role = RankRole(ctx, _ecfg(model, num_workers=pp))
         res = []
         for rnd in range(2):       # followers return on ROUND_END and serve the next round
             seqs = [role.add_request(p, PARAMS) for p in PROMPTS] if role.is_driver else []
@@ -124,3 +124,28 @@ def test_multiprocess_tensor_parallel_matches_single(model, world, tp):
     for r in range(0, world, tp):               # every replica's leader
         for rnd in results[r]:
             assert rnd == expected
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("model,world,pp,tp", [("tiny-llama", 4, 2, 2), ("tiny-mixtral", 4, 2, 2)])
+def test_pipeline_of_tensor_parallel_stages_matches_single(model, world, pp, tp):
+    """pp x tp: every stage is a TP group; lane t (the t-th TP rank of each stage) carries its own
+    activation hops and sampled-ids ring; the stage-0 TP peer replays the driver's issues."""
+    expected = LLMEngine(_ecfg(model)).generate(PROMPTS, PARAMS)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, tp, model, port, q, pp)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        r, res, err = q.get(timeout=300)
+        assert err is None, f"rank {r}: {err}"
+        results[r] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r for r in results if results[r] is not None] == [0]     # one driver: stage 0, TP rank 0
+    for rnd in results[0]:
+        assert rnd == expected
