@@ -105,10 +105,12 @@ def build_host_batch(step: Step, bm, block_size: int, max_blocks: Optional[int] 
     seqs = step.seqs
     b = len(seqs)
     seq_ids = np.fromiter((s.seq_id for s in seqs), dtype=np.int64, count=b)
-    seq_lens = np.fromiter((s.total_len for s in seqs), dtype=np.int32, count=b)
     if step.is_prefill:
+        # chunked prefill: a sequence computes [num_cached, num_cached + prefill_len) and attends to
+        # everything before it already in the KV cache (seq_lens = context after this step)
         starts = np.fromiter((s.num_cached for s in seqs), dtype=np.int32, count=b)
-        qlens = seq_lens - starts
+        qlens = np.fromiter((s.prefill_len for s in seqs), dtype=np.int32, count=b)
+        seq_lens = starts + qlens
         cu = np.zeros(b + 1, dtype=np.int32)
         np.cumsum(qlens, out=cu[1:])
         t = int(cu[-1])
@@ -116,11 +118,13 @@ def build_host_batch(step: Step, bm, block_size: int, max_blocks: Optional[int] 
         positions = np.empty(t, dtype=np.int32)
         for i, s in enumerate(seqs):
             toks = s.all_tokens()
-            ids[cu[i]:cu[i + 1]] = toks[s.num_cached:]
-            positions[cu[i]:cu[i + 1]] = np.arange(s.num_cached, s.total_len, dtype=np.int32)
+            a, e = s.num_cached, s.num_cached + int(qlens[i])
+            ids[cu[i]:cu[i + 1]] = toks[a:e]
+            positions[cu[i]:cu[i + 1]] = np.arange(a, e, dtype=np.int32)
         logits_idx = (cu[1:] - 1).astype(np.int32)
         max_q_len = int(qlens.max()) if b else 0
     else:
+        seq_lens = np.fromiter((s.total_len for s in seqs), dtype=np.int32, count=b)
         starts = seq_lens - 1
         qlens = np.ones(b, dtype=np.int32)
         cu = np.arange(b + 1, dtype=np.int32)

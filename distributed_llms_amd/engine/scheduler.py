@@ -57,7 +57,7 @@ class Step:
     @property
     def num_tokens(self) -> int:
         if self.is_prefill:
-            return sum(s.total_len - s.num_cached for s in self.seqs)
+            return sum(s.prefill_len for s in self.seqs)
         return self.size
 
 
@@ -66,11 +66,14 @@ def _eos_of(seq: Sequence) -> int:
 
 
 class Scheduler:
-    """Admission (prefill) is per-sequence Python; the running decode set of every slot lives in
+    """Admission (prefill, chunked for prompts longer than the step's token budget) is
+    per-sequence Python; the running decode set of every slot lives in
     the native :class:`SlotBatcher` (csrc/runtime/slot_batcher.cpp), which builds each decode
     step's packed metadata and applies its sampled tokens in one call each.  A running sequence's
     Python ``output`` list is brought up to date when it leaves the running set (finish,
     preemption, abort); :meth:`sync_output` refreshes it earlier on demand."""
+
+    MIN_CHUNK = 32          # smallest chunk worth starting in a step whose budget is nearly used
 
     def __init__(self, block_manager, num_slots: int = 1, max_batch: int = 256,
                  max_prefill_tokens: int = 16384, max_seq_len: int = 4096):
@@ -100,6 +103,7 @@ class Scheduler:
         for s in list(self.waiting):
             if s.seq_id == seq_id:
                 self.waiting.remove(s)
+                self.bm.free_sequence(s.seq_id)       # a partly prefilled prompt holds blocks
                 s.finish("abort")
                 self.finished.append(s)
                 return True
@@ -144,9 +148,18 @@ class Scheduler:
             while self.waiting and n_running + len(admitted) < target:
                 seq = self.waiting[0]
                 n = seq.total_len - seq.num_cached
-                if admitted and tokens + n > self.max_prefill_tokens:
-                    break
-                if not self.bm.ensure_capacity(seq.seq_id, seq.total_len):
+                budget = self.max_prefill_tokens - tokens
+                if n > budget:
+                    # chunked prefill: a prompt longer than what is left of this step's token
+                    # budget contributes a chunk; the rest follows in later steps
+                    if admitted and budget < min(n, self.MIN_CHUNK):
+                        break
+                    if budget <= 0:
+                        break
+                    n = budget
+                seq.chunk = n if n < seq.total_len - seq.num_cached else 0
+                if not self.bm.ensure_capacity(seq.seq_id, seq.num_cached + n):
+                    seq.chunk = 0
                     break
                 self.waiting.popleft()
                 seq.status = SeqStatus.RUNNING
@@ -217,6 +230,15 @@ class Scheduler:
         for seq, tok in zip(step.seqs, tokens):
             st = seq.status
             if st is SeqStatus.FINISHED or st is SeqStatus.ABORTED:   # aborted while in flight
+                seq.chunk = 0
+                continue
+            if seq.chunk:
+                # a non-final chunk: its KV is cached, its sampled token is meaningless; the rest of
+                # the prompt goes first in line for the next step
+                seq.num_cached += seq.chunk
+                seq.chunk = 0
+                seq.status = SeqStatus.WAITING
+                self.waiting.appendleft(seq)
                 continue
             seq.num_cached = len(seq.prompt) + len(seq.output)
             if seq.append(tok, now) or seq.num_cached + 1 >= self.max_seq_len:

@@ -51,6 +51,7 @@ class Sequence:
     output: List[int] = field(default_factory=list)
     status: SeqStatus = SeqStatus.WAITING
     num_cached: int = 0              # tokens whose K/V are in the paged cache
+    chunk: int = 0                   # prefill tokens scheduled in the current step (0 = all the rest)
     slot: int = -1                   # pipeline microbatch slot
     arrival: float = field(default_factory=time.perf_counter)
     first_token_time: Optional[float] = None
@@ -66,6 +67,12 @@ class Sequence:
     @property
     def total_len(self) -> int:
         return len(self.prompt) + len(self.output)
+
+    @property
+    def prefill_len(self) -> int:
+        """Tokens the current prefill step computes for this sequence (a chunk of a long prompt,
+        or everything not yet in the KV cache)."""
+        return self.chunk or (self.total_len - self.num_cached)
 
     def all_tokens(self) -> List[int]:
         return self.prompt + self.output

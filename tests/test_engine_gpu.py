@@ -84,3 +84,31 @@ def test_lookahead_decode_matches_synchronous(cuda, graphs):
     la_e, _ = run(True, eos)
     assert la_e == sync_e
     assert any(len(o) < n for o, n in zip(sync_e, lens)), "EOS never fired"
+
+
+@pytest.mark.parametrize("name", ["tiny-llama-d128", "tiny-mixtral"])
+def test_chunked_prefill_gpu_matches_cpu_logits(cuda, name):
+    """A 300-token prompt prefilled in 64-token chunks on the GPU (each chunk's attention reads the
+    earlier chunks from the paged cache) vs the CPU fp32 whole-prompt prefill: the last chunk's
+    logits agree."""
+    cfg = get_model_config(name)
+    sd = W.synth_hf_state_dict(cfg, seed=5, dtype=torch.float32)
+    prompt = [(13 * j) % 400 + 3 for j in range(300)]
+    e_cpu = LLMEngine(EngineConfig(model=name, dtype="float32", device="cpu", max_batch=2, max_seq_len=512,
+                                   use_graphs=False),
+                      ModelStage(cfg, 0, cfg.num_layers, "cpu", torch.float32).load_hf_state(sd))
+    e_gpu = LLMEngine(EngineConfig(model=name, dtype="bfloat16", device="cuda", max_batch=2, max_seq_len=512,
+                                   use_graphs=False, num_kv_blocks=64, max_prefill_tokens=64),
+                      ModelStage(cfg, 0, cfg.num_layers, "cuda", torch.bfloat16).load_hf_state(sd))
+    logits = []
+    for eng in (e_cpu, e_gpu):
+        eng.add_request(prompt, SamplingParams(max_new_tokens=1))
+        while True:
+            st = eng.scheduler.schedule(0)
+            out = eng.runner.execute(build_host_batch(st, eng.bm, 32))
+            final = st.seqs[0].chunk == 0
+            eng.scheduler.complete(st, [0])
+            if final:
+                logits.append(out.float().cpu())
+                break
+    torch.testing.assert_close(logits[1], logits[0], atol=6e-2, rtol=5e-2)

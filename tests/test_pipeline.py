@@ -173,3 +173,19 @@ def test_lookahead_pipeline_with_eos_and_mixed_lengths(monkeypatch, stages):
     assert outs == exp
     assert drv.num_lookahead > 0 and not drv.inflight
     assert drv.bm.num_free() == drv.bm.num_blocks - 1               # every KV block back (scratch kept)
+
+
+@pytest.mark.parametrize("stages", [1, 2])
+def test_chunked_prefill_matches_whole_prompt_prefill(stages):
+    """Long prompts prefilled in chunks (max_prefill_tokens below the prompt length) generate the
+    same greedy tokens as whole-prompt prefill, in the engine and in a pipeline."""
+    prompts = [[(7 * i + j) % 500 + 3 for j in range(40 + 9 * i)] for i in range(5)]
+    params = SamplingParams(max_new_tokens=5, ignore_eos=True)
+    whole = LLMEngine(_ecfg(max_prefill_tokens=4096)).generate(prompts, params)
+    cfg = _ecfg(max_prefill_tokens=24)
+    if stages == 1:
+        eng = LLMEngine(cfg)
+        out = eng.generate(prompts, params)
+    else:
+        out, _, _ = run_loopback_pipeline(cfg, stages, prompts, params)
+    assert out == whole

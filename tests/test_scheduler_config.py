@@ -219,3 +219,41 @@ def test_assign_shards_capacity_aware():
     # CPU workers (memory 0): plain registration order, no capacity check
     m = _master_with([0, 0], model="synthetic:gpt2-small", shards=2)
     assert m.assign_shards() == {"w0": [0], "w1": [1]}
+
+
+def test_chunked_prefill_of_a_long_prompt():
+    """A prompt longer than max_prefill_tokens is prefilled in chunks over several steps (each
+    attending to the KV its earlier chunks cached); only the last chunk's token counts."""
+    bm = make_block_manager(64, 4)
+    sch = Scheduler(bm, num_slots=1, max_batch=4, max_prefill_tokens=40, max_seq_len=256)
+    sch.MIN_CHUNK = 8
+    long_, short = _seq(100, 3), _seq(10, 3)
+    sch.add(long_)
+    sch.add(short)
+    st = sch.schedule(0)
+    assert st.is_prefill and st.seqs == [long_] and long_.chunk == 40 and st.num_tokens == 40
+    hb = build_host_batch(st, bm, 4)
+    assert hb.positions.tolist() == list(range(40)) and hb.seq_lens.tolist() == [40]
+    assert sch.complete(st, [99]) == [] and long_.output == [] and long_.num_cached == 40
+    assert sch.waiting[0] is long_
+    st = sch.schedule(0)
+    hb = build_host_batch(st, bm, 4)
+    assert st.seqs == [long_] and hb.positions[0] == 40 and hb.seq_lens.tolist() == [80]
+    sch.complete(st, [98])
+    st = sch.schedule(0)                                # the last 20 tokens + the short prompt
+    assert st.seqs == [long_, short] and long_.chunk == 0 and st.num_tokens == 30
+    hb = build_host_batch(st, bm, 4)
+    assert hb.seq_lens.tolist() == [100, 10] and hb.logits_idx.tolist() == [19, 29]
+    sch.complete(st, [5, 6])
+    assert long_.output == [5] and short.output == [6] and sch.num_running() == 2
+    assert bm.block_table(long_.seq_id) and len(bm.block_table(long_.seq_id)) == 25
+
+
+def test_abort_of_a_partly_prefilled_prompt_frees_its_blocks():
+    bm = make_block_manager(64, 4)
+    sch = Scheduler(bm, num_slots=1, max_batch=4, max_prefill_tokens=16, max_seq_len=256)
+    s = _seq(50, 3)
+    sch.add(s)
+    sch.complete(sch.schedule(0), [1])
+    assert s.num_cached == 16 and bm.num_free() == 63 - 4
+    assert sch.abort(s.seq_id) and bm.num_free() == 63
