@@ -122,7 +122,7 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
   constexpr int AI = BM / 64, BI = 2, G = AI + BI, RT = BM / 64;
   const int wm = wv >> 1, wn = wv & 1;
   // cache policy of the staging loads (aux: 2 = nt): VAR 2 streams the weights nt, VAR 3 both operands
-  constexpr int BAUX = VAR >= 2 ? 2 : 0, AAUX = VAR == 3 ? 2 : 0;
+  constexpr int BAUX = (VAR & 7) >= 2 ? 2 : 0, AAUX = (VAR & 7) == 3 ? 2 : 0;
   auto stage = [&](int buf, int t) {
     bf16* base = smem + buf * BUF;
     const int ko = t * WBK;
@@ -212,7 +212,7 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       // buffer (t-1) % NBUF was last read in iteration t-1, which every wave finished before
       // this barrier: refill it with tile t + NBUF - 1
       const int nb = cur == 0 ? NBUF - 1 : cur - 1;
-      if constexpr (VAR == 0) {
+      if constexpr ((VAR & 7) == 0) {
         stage(nb, t + NBUF - 1);
         ktile(cur, smem, 0, std::false_type{});
       } else {
@@ -260,7 +260,9 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
   (void)ntiles;
   const int m0 = m_t * BM;
   const int kt0 = split * kt_per_split;
-  const int nt = max(0, min(K / WBK, kt0 + kt_per_split) - kt0);
+  // ablations (timing only, wrong results): VAR & 16 skips the K loop (launch + epilogue cost),
+  // VAR & 8 skips the epilogue stores (kept behind a never-true runtime test so the MFMAs stay)
+  const int nt = (VAR & 16) ? 0 : max(0, min(K / WBK, kt0 + kt_per_split) - kt0);
 
   // per-lane staging sources: instruction i covers tile rows 8i .. 8i+7, lane -> (row, chunk)
   const bf16* srcA[AI];
@@ -279,6 +281,7 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
   }
   f32x4 acc[RT][4];
   wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, nt, acc, wv, lane);
+  if ((VAR & 8) && nsplit >= 0) return;
   wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
 }
 
@@ -406,6 +409,9 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   // weights nt (variant 2) where the grid has no K split: -3..-5 % on the MLP up projection from
   // cold caches; on the split-K grids nt costs up to +25 % at M = 128 (profiles/wide_gemm.md)
   // (variant 4 = variant 1 everywhere, for A/B runs)
+  // ablations (A/B timing only): variant | 8 = no epilogue stores, | 16 = no K loop
+  const int abl = variant & 24;
+  variant &= 7;
   if (variant == 1 && S == 1) variant = 2;
   else if (variant == 4) variant = 1;
 #define DLLM_WIDE_GO3(BM_, SPLIT_, SW_, V_)                                                                      \
@@ -413,7 +419,9 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
                      (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S)
 #define DLLM_WIDE_GO(BM_, SPLIT_, SW_)                                                                          \
   do {                                                                                                         \
-    if (variant == 0) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 0);                                                      \
+    if (abl == 8) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 10); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 9); } \
+    else if (abl == 16) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 18); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 17); } \
+    else if (variant == 0) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 0);                                                 \
     else if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 2);                                                 \
     else if (variant == 3) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 3);                                                 \
     else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 1);                                                                   \
