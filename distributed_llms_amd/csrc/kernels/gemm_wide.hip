@@ -26,7 +26,10 @@
 //  * XCD-aware block order (bijective remap): the M tiles and K slices of one N tile run
 //    back-to-back on one XCD;
 //  * the next tile's LDS-DMA pieces are issued between the MFMAs (pinned with
-//    sched_group_barrier): +9 % on the MLP up projection over issuing them after the barrier.
+//    sched_group_barrier): +9 % on the MLP up projection over issuing them after the barrier;
+//  * variant bit 32 (the engine default): fragment reads in inline asm with one lgkmcnt wait per
+//    MFMA row, substep 1's reads issued under substep 0's MFMAs (hipcc otherwise waits
+//    lgkmcnt(0) for all 16 reads before a K-tile's first MFMA): 1-2 % per GEMM, bit-exact.
 // Measured and dropped (profiles/wide_gemm.md): BK = 32 with 6 stages and a fragment software
 // pipeline (slower: twice the barriers), 4/5 stages at BM = 128, weights pre-tiled into
 // contiguous 16 KiB tiles (+0-3 %), setprio, other read/MFMA/VMEM orders.  Ablations at M = 256:
@@ -64,6 +67,36 @@ __device__ __forceinline__ void wait_tiles(int younger) {
   }
 }
 #undef DLLM_VM
+
+// Fragment reads the compiler does not count (inline asm), for the SPLITRD K-tile: hipcc waits
+// lgkmcnt(0) before the first MFMA of a K-tile whenever LDS-DMA shares the loop, exposing the
+// latency of all 16 fragment reads of every wave at once; here each MFMA row waits only for its
+// own fragments (`+v` on the wait statement orders the MFMAs after it, guide §5.7 item 1 (ii)).
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_frag(uint32_t addr) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+#define DLLM_LGKM_W1(n) if constexpr (N == n) asm volatile("s_waitcnt lgkmcnt(" #n ")" : "+v"(a));
+#define DLLM_LGKM_W5(n) \
+  if constexpr (N == n) asm volatile("s_waitcnt lgkmcnt(" #n ")" : "+v"(a), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+template <int N>
+__device__ __forceinline__ void lgkm_wait1(bf16x8& a) {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt");
+  DLLM_LGKM_W1(0) DLLM_LGKM_W1(1) DLLM_LGKM_W1(2) DLLM_LGKM_W1(3) DLLM_LGKM_W1(4) DLLM_LGKM_W1(5) DLLM_LGKM_W1(6)
+  DLLM_LGKM_W1(7) DLLM_LGKM_W1(8) DLLM_LGKM_W1(9) DLLM_LGKM_W1(10) DLLM_LGKM_W1(11) DLLM_LGKM_W1(12)
+  DLLM_LGKM_W1(13) DLLM_LGKM_W1(14) DLLM_LGKM_W1(15)
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait5(bf16x8& a, bf16x8& b0, bf16x8& b1, bf16x8& b2, bf16x8& b3) {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt");
+  DLLM_LGKM_W5(0) DLLM_LGKM_W5(1) DLLM_LGKM_W5(2) DLLM_LGKM_W5(3) DLLM_LGKM_W5(4) DLLM_LGKM_W5(5) DLLM_LGKM_W5(6)
+  DLLM_LGKM_W5(7) DLLM_LGKM_W5(8) DLLM_LGKM_W5(9) DLLM_LGKM_W5(10) DLLM_LGKM_W5(11) DLLM_LGKM_W5(12)
+  DLLM_LGKM_W5(13) DLLM_LGKM_W5(14) DLLM_LGKM_W5(15)
+}
+#undef DLLM_LGKM_W1
+#undef DLLM_LGKM_W5
 }  // namespace
 
 // B-tile row r (0..127) -> row of the weight matrix.
@@ -198,6 +231,65 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
     }
   };
 
+  // SPLITRD (VAR & 32): the same K-tile with asm fragment reads and per-row lgkmcnt waits:
+  // substep 0's reads, its first MFMA row, substep 1's reads (overlapping substep 0's MFMAs),
+  // then each row waits only for its own A fragment; the G staging pieces are spread over rows.
+  // Per-lane LDS byte offsets: fragment (rt | ct) of substep s sits at base_s + (rt | ct) * 2 KiB.
+  const uint32_t lds0 = (uint32_t)(size_t)(lds_vptr_w)smem;
+  uint32_t aoff[2], boff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int ra = wm * (BM / 4) + fr, rb = wn * 64 + fr;
+    aoff[s] = (uint32_t)(ra * WBK + wswz(ra, 4 * s + fq) * 8) * 2;
+    boff[s] = (uint32_t)(AEL + rb * WBK + wswz(rb, 4 * s + fq) * 8) * 2;
+  }
+  auto ktile_sr = [&](int cur, bf16* dst, int ko, auto stg) {
+    constexpr bool STG = decltype(stg)::value;
+    constexpr int ROWS = 2 * RT;
+    const uint32_t base = lds0 + (uint32_t)(cur * BUF * 2);
+    bf16x8 fa[2][RT], fb[2][4];
+    auto reads = [&](int s) {
+      const uint32_t ab = base + aoff[s], bb = base + boff[s];
+      fb[s][0] = lds_frag<0>(bb);
+      fb[s][1] = lds_frag<2048>(bb);
+      fb[s][2] = lds_frag<4096>(bb);
+      fb[s][3] = lds_frag<6144>(bb);
+      fa[s][0] = lds_frag<0>(ab);
+      if constexpr (RT > 1) fa[s][1] = lds_frag<2048>(ab);
+      if constexpr (RT > 2) fa[s][2] = lds_frag<4096>(ab);
+      if constexpr (RT > 3) fa[s][3] = lds_frag<6144>(ab);
+    };
+    auto row = [&](int s, int rt) {
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+        acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][rt], fb[s][ct], acc[rt][ct], 0, 0, 0);
+      if constexpr (STG) {
+        const int r = s * RT + rt;
+#pragma unroll
+        for (int p = 0; p < G; ++p)
+          if ((p * ROWS) / G == r) piece(dst, ko, p);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    reads(0);
+    lgkm_wait5<RT - 1>(fa[0][0], fb[0][0], fb[0][1], fb[0][2], fb[0][3]);
+    __builtin_amdgcn_sched_barrier(0);
+    row(0, 0);
+    reads(1);
+    __builtin_amdgcn_sched_barrier(0);
+    // rows 1.. of substep 0: younger outstanding reads = the rest of fa[0] + all of substep 1
+    if constexpr (RT > 1) { lgkm_wait1<RT - 2 + RT + 4>(fa[0][1]); __builtin_amdgcn_sched_barrier(0); row(0, 1); }
+    if constexpr (RT > 2) { lgkm_wait1<RT - 3 + RT + 4>(fa[0][2]); __builtin_amdgcn_sched_barrier(0); row(0, 2); }
+    if constexpr (RT > 3) { lgkm_wait1<RT - 4 + RT + 4>(fa[0][3]); __builtin_amdgcn_sched_barrier(0); row(0, 3); }
+    lgkm_wait5<RT - 1>(fa[1][0], fb[1][0], fb[1][1], fb[1][2], fb[1][3]);
+    __builtin_amdgcn_sched_barrier(0);
+    row(1, 0);
+    if constexpr (RT > 1) { lgkm_wait1<RT - 2>(fa[1][1]); __builtin_amdgcn_sched_barrier(0); row(1, 1); }
+    if constexpr (RT > 2) { lgkm_wait1<RT - 3>(fa[1][2]); __builtin_amdgcn_sched_barrier(0); row(1, 2); }
+    if constexpr (RT > 3) { lgkm_wait1<RT - 4>(fa[1][3]); __builtin_amdgcn_sched_barrier(0); row(1, 3); }
+  };
+  constexpr bool SPLITRD = (VAR & 32) != 0 && RT <= 4;
+
   if (nt > 0) {
 #pragma unroll
     for (int p = 0; p < NBUF - 1; ++p)
@@ -212,7 +304,9 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       // buffer (t-1) % NBUF was last read in iteration t-1, which every wave finished before
       // this barrier: refill it with tile t + NBUF - 1
       const int nb = cur == 0 ? NBUF - 1 : cur - 1;
-      if constexpr ((VAR & 7) == 0) {
+      if constexpr (SPLITRD) {
+        ktile_sr(cur, smem + nb * BUF, (t + NBUF - 1) * WBK, std::true_type{});
+      } else if constexpr ((VAR & 7) == 0) {
         stage(nb, t + NBUF - 1);
         ktile(cur, smem, 0, std::false_type{});
       } else {
@@ -225,7 +319,8 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       wait_tiles<G>(nt - 1 - t);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      ktile(cur, smem, 0, std::false_type{});
+      if constexpr (SPLITRD) ktile_sr(cur, smem, 0, std::false_type{});
+      else ktile(cur, smem, 0, std::false_type{});
       cur = cur == NBUF - 1 ? 0 : cur + 1;
     }
   }
@@ -409,8 +504,9 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   // weights nt (variant 2) where the grid has no K split: -3..-5 % on the MLP up projection from
   // cold caches; on the split-K grids nt costs up to +25 % at M = 128 (profiles/wide_gemm.md)
   // (variant 4 = variant 1 everywhere, for A/B runs)
+  // variant | 32: per-row fragment waits (SPLITRD in wide_mainloop; the engine default);
   // ablations (A/B timing only): variant | 8 = no epilogue stores, | 16 = no K loop
-  const int abl = variant & 24;
+  const int abl = variant & 56;
   variant &= 7;
   if (variant == 1 && S == 1) variant = 2;
   else if (variant == 4) variant = 1;
@@ -421,6 +517,7 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   do {                                                                                                         \
     if (abl == 8) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 10); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 9); } \
     else if (abl == 16) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 18); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 17); } \
+    else if (abl == 32) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 34); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 33); } \
     else if (variant == 0) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 0);                                                 \
     else if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 2);                                                 \
     else if (variant == 3) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 3);                                                 \

@@ -85,7 +85,10 @@ def _use_tiled(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool
 #   B=256, +5.8 % at B=128, +1.2 % at B=512), proj only up to M = 256 (it loses at 512), gate_up
 #   only up to M = 256 (DLLM_WIDE_GATE_UP_MAX_M: hipBLASLt + silu_mul is +1.9 % at B=384, +2.5 % at 512).
 WIDE = {t for t in os.environ.get("DLLM_WIDE", "auto").split(",") if t and t != "none"}
-WIDE_VARIANT = int(os.environ.get("DLLM_WIDE_VARIANT", "1"))
+# gemm_wide variant: 1 = LDS-DMA pieces interleaved with the MFMAs (weights nt where the grid has no
+# K split); | 32 = fragment reads in asm with one lgkmcnt wait per MFMA row instead of hipcc's
+# lgkmcnt(0) before a K-tile's first MFMA (+0.8 % tok/s on 8B, +0.5 % on 70B at B = 256; bit-exact)
+WIDE_VARIANT = int(os.environ.get("DLLM_WIDE_VARIANT", "33"))
 
 
 # smallest M the wide kernel serves (1: every decode batch; the 64-row tile at M <= 64 streams

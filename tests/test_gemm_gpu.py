@@ -141,6 +141,18 @@ def test_wide_swiglu(cuda, m, inter, k, splits, variant):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("m", [1, 37, 128, 200, 256, 300])
+@pytest.mark.parametrize("n,k,splits,swiglu", [(6144, 4096, 5, False), (4096, 14336, 8, False),
+                                               (1024, 512, 1, False), (2048, 512, 1, True)])
+def test_wide_split_fragment_waits_bit_exact(cuda, m, n, k, splits, swiglu):
+    """Variant bit 32 (fragment reads in asm, one lgkmcnt wait per MFMA row) runs the same MFMAs
+    in the same order as the default K-tile: bit-identical outputs."""
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    a = gemm.linear_wide(x, w, splits=splits, swiglu=swiglu, variant=1)
+    b = gemm.linear_wide(x, w, splits=splits, swiglu=swiglu, variant=1 | 32)
+    assert torch.equal(a, b)
+
+
 def test_splitk_slabs_keep_output_precision(cuda):
     """Split-K slabs are stored as f16 x 2^-6 (csrc/kernels/common.h, DLLM_PART_TYPE 2): the split
     result must stay within one bf16 ulp of the exact product (plus half an ulp of the output's typical
