@@ -6,8 +6,9 @@
   plus the pybind11 binding TU, linked into ``distributed_llms_amd/_C_kernels<EXT_SUFFIX>``.
 * ``_C_runtime``: host-only C++17 (``csrc/runtime/*.cpp``), paged-KV block manager and
   wire-frame codec, linked into ``distributed_llms_amd/_C_runtime<EXT_SUFFIX>``.
-* ``_C_rccl``: native RCCL p2p transport (``csrc/comm/rccl_p2p.cpp``), linked against
-  ``librccl.so.1`` -- at run time the copy PyTorch already loaded (one RCCL per process).
+* ``_C_rccl``: native RCCL p2p transport (``csrc/comm/rccl_p2p.cpp``) and the HIP-IPC
+  peer-write data plane (``csrc/comm/ipc_p2p.cpp``), linked against ``librccl.so.1`` -- at run
+  time the copy PyTorch already loaded (one RCCL per process).
 
 Objects go to ``build/`` (git-ignored); the ``.so`` files land in the package
 directory so they travel to the GPU box with the repo snapshot.
@@ -128,17 +129,20 @@ def build_runtime_sanitized(out_dir: str) -> str:
 
 
 def build_comm(force=False, jobs=8, verbose=False) -> str:
-    src = os.path.join(HERE, "comm", "rccl_p2p.cpp")
     out_dir = os.path.join(BUILD, "comm")
     os.makedirs(out_dir, exist_ok=True)
-    obj = os.path.join(out_dir, "rccl_p2p.o")
     rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
-    if force or _stale(obj, [src]):
-        _run([CXX, "-c", src, "-o", obj, "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
-              "-D__HIP_PLATFORM_AMD__", f"-I{rocm}/include"] + [f"-I{p}" for p in _py_includes()])
+    objs = []
+    for name in ("rccl_p2p", "ipc_p2p"):
+        src = os.path.join(HERE, "comm", name + ".cpp")
+        obj = os.path.join(out_dir, name + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src]):
+            _run([CXX, "-c", src, "-o", obj, "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
+                  "-D__HIP_PLATFORM_AMD__", f"-I{rocm}/include"] + [f"-I{p}" for p in _py_includes()])
     target = _ext_path("_C_rccl")
-    if force or _stale(target, [obj]):
-        _run([CXX, "-shared", "-fPIC", "-o", target, obj, f"-L{rocm}/lib", "-lrccl", "-lamdhip64"])
+    if force or _stale(target, objs):
+        _run([CXX, "-shared", "-fPIC", "-o", target, *objs, f"-L{rocm}/lib", "-lrccl", "-lamdhip64"])
     return target
 
 

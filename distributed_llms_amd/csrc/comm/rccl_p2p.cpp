@@ -97,8 +97,11 @@ class RcclComm {
 
 }  // namespace
 
+void register_ipc(py::module_& m);   // ipc_p2p.cpp (N6)
+
 PYBIND11_MODULE(_C_rccl, m) {
-  m.doc() = "Native RCCL p2p transport (pipeline activations over xGMI)";
+  m.doc() = "Native RCCL p2p transport and HIP-IPC peer-write data plane (pipeline activations over xGMI)";
+  register_ipc(m);
   m.def("unique_id", &unique_id);
   m.def("version", []() {
     int v = 0;

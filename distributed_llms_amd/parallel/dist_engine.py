@@ -132,10 +132,18 @@ def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
                        rings, tp, tpg)
 
 
-def make_transport(ranks, stage: int, ctrl_group, data_group, device: str, ring_group=None):
+def make_transport(ranks, stage: int, ctrl_group, data_group, device: str, ring_group=None, hop=None):
     """Activation transport for one pipeline stage: torch.distributed's RCCL process group by
-    default; ``DLLM_TRANSPORT=rccl`` selects the native RCCL p2p module (own comm streams)."""
-    if os.environ.get("DLLM_TRANSPORT", "") == "rccl" and data_group is None and str(device).startswith("cuda"):
+    default; ``DLLM_TRANSPORT=rccl`` selects the native RCCL p2p module (own comm streams),
+    ``DLLM_TRANSPORT=ipc`` the HIP-IPC peer-write data plane (parallel/ipc_transport.py; also
+    between processes sharing one GPU).  ``hop`` = (max rows, hidden, dtype) of an activation hop."""
+    kind = os.environ.get("DLLM_TRANSPORT", "")
+    on_gpu = str(device).startswith("cuda")
+    if kind == "ipc" and on_gpu:
+        from .ipc_transport import IpcTransport
+        rows, hidden, dtype = hop
+        return IpcTransport(ranks, stage, ctrl_group, device, rows, hidden, dtype, ring_group=ring_group)
+    if kind == "rccl" and data_group is None and on_gpu:
         from .rccl_transport import RcclTransport
         return RcclTransport(ranks, stage, ctrl_group, device)
     return DistTransport(ranks, stage, ctrl_group=ctrl_group, data_group=data_group, ring_group=ring_group)
@@ -182,8 +190,9 @@ class RankRole:
             self.engine = LLMEngine(ecfg1, stage)
         else:
             self.runner = StageRunner(stage, ecfg, num_blocks=nb)
+            hop = (max(ecfg.max_prefill_tokens, ecfg.max_batch), mcfg.hidden_size, stage.dtype)
             self.transport = make_transport(ctx.pipeline_ranks, ctx.stage, ctx.ctrl_group, ctx.data_group,
-                                            ctx.device, ctx.ring_group)
+                                            ctx.device, ctx.ring_group, hop=hop)
             if ctx.stage == 0 and ctx.tp_rank == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.runner, self.transport, ecfg, bm)

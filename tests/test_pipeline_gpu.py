@@ -28,21 +28,29 @@ def test_loopback_pipeline_gpu(cuda, stages):
     assert drv.num_steps > 0
 
 
-def _gpu_rank_main(rank, world, port, prompts, out_q):
+def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1):
     import os
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), DLLM_SHARE_GPU="1", DLLM_DATA_BACKEND="gloo")
+                      LOCAL_RANK=str(rank), DLLM_SHARE_GPU="1", DLLM_DATA_BACKEND="gloo", DLLM_TRANSPORT=transport)
     import torch.distributed as dist
     from distributed_llms_amd.parallel.dist_engine import RankRole, init_distributed
     ctx = init_distributed(pp=world)
     assert ctx.device == "cuda:0" and ctx.host_staged
     role = RankRole(ctx, _mp_ecfg(world))
+    if transport == "ipc":
+        from distributed_llms_amd.parallel.ipc_transport import IpcTransport
+        assert isinstance(role.transport, IpcTransport)
     p = SamplingParams(max_new_tokens=12, ignore_eos=True)
-    seqs = [role.add_request(q, p) for q in prompts] if role.is_driver else []
-    role.run_round()
+    outs = []
+    for _ in range(rounds):        # several rounds: the IPC sequence numbers carry across them
+        seqs = [role.add_request(q, p) for q in prompts] if role.is_driver else []
+        role.run_round()
+        outs.append([s.output for s in seqs])
     role.shutdown()
+    if transport == "ipc":
+        role.transport.close()
     dist.barrier(group=ctx.ctrl_group)
-    out_q.put((rank, [s.output for s in seqs]))
+    out_q.put((rank, outs))
     dist.destroy_process_group()
 
 
@@ -56,21 +64,40 @@ def _mp_ecfg(world):
 def test_multiprocess_gpu_pipeline_host_staged(cuda, world):
     """torch.distributed ranks (one process per stage, all on the one GPU, activations host-staged
     over gloo) reproduce the single-process engine -- the RCCL path minus the transport."""
-    import socket
-    import torch.multiprocessing as mp
     prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
     ref = LLMEngine(_mp_ecfg(1)).generate(prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
+    res = _run_ranks(world, prompts, "", rounds=1)
+    assert res[0] == [ref]
+
+
+def _run_ranks(world, prompts, transport, rounds):
+    import socket
+    import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
-    procs = [ctxm.Process(target=_gpu_rank_main, args=(r, world, port, prompts, q)) for r in range(world)]
+    # daemonic: a rank stuck in a stream wait dies with the test process instead of outliving it
+    procs = [ctxm.Process(target=_gpu_rank_main, args=(r, world, port, prompts, q, transport, rounds), daemon=True)
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0] == ref
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multiprocess_gpu_pipeline_ipc(cuda, world):
+    """The HIP-IPC data plane (parallel/ipc_transport.py): stage processes sharing the one
+    GPU hand activations over device to device through mapped peer slots + stream-ordered flags and
+    credits (RCCL refuses two ranks on one device, IPC does not); three rounds of ten requests
+    (ring reuse across rounds) reproduce the single-process engine token for token."""
+    prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
+    ref = LLMEngine(_mp_ecfg(1)).generate(prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
+    res = _run_ranks(world, prompts, "ipc", rounds=3)
+    assert res[0] == [ref, ref, ref]
