@@ -19,7 +19,7 @@ from ..config import EngineConfig
 from ..engine.llm_engine import LLMEngine, build_stage, make_block_manager
 from ..engine.runner import StageRunner, plan_kv_blocks
 from .comm import DistTransport
-from .pipeline import PipelineDriver, stage_worker_loop
+from .pipeline import PipelineDriver, inflight_window, stage_worker_loop
 from .planner import plan_units
 
 log = logging.getLogger("dllm.dist")
@@ -136,13 +136,14 @@ def make_transport(ranks, stage: int, ctrl_group, data_group, device: str, ring_
     """Activation transport for one pipeline stage: torch.distributed's RCCL process group by
     default; ``DLLM_TRANSPORT=rccl`` selects the native RCCL p2p module (own comm streams),
     ``DLLM_TRANSPORT=ipc`` the HIP-IPC peer-write data plane (parallel/ipc_transport.py; also
-    between processes sharing one GPU).  ``hop`` = (max rows, hidden, dtype) of an activation hop."""
+    between processes sharing one GPU).  ``hop`` = (max rows, hidden, dtype, in-flight window) of an activation hop."""
     kind = os.environ.get("DLLM_TRANSPORT", "")
     on_gpu = str(device).startswith("cuda")
     if kind == "ipc" and on_gpu:
         from .ipc_transport import IpcTransport
-        rows, hidden, dtype = hop
-        return IpcTransport(ranks, stage, ctrl_group, device, rows, hidden, dtype, ring_group=ring_group)
+        rows, hidden, dtype, window = hop
+        return IpcTransport(ranks, stage, ctrl_group, device, rows, hidden, dtype, ring_group=ring_group,
+                            window=window)
     if kind == "rccl" and data_group is None and on_gpu:
         from .rccl_transport import RcclTransport
         return RcclTransport(ranks, stage, ctrl_group, device)
@@ -190,7 +191,8 @@ class RankRole:
             self.engine = LLMEngine(ecfg1, stage)
         else:
             self.runner = StageRunner(stage, ecfg, num_blocks=nb)
-            hop = (max(ecfg.max_prefill_tokens, ecfg.max_batch), mcfg.hidden_size, stage.dtype)
+            hop = (max(ecfg.max_prefill_tokens, ecfg.max_batch), mcfg.hidden_size, stage.dtype,
+                   inflight_window(ecfg, ctx.pp))
             self.transport = make_transport(ctx.pipeline_ranks, ctx.stage, ctx.ctrl_group, ctx.data_group,
                                             ctx.device, ctx.ring_group, hop=hop)
             if ctx.stage == 0 and ctx.tp_rank == 0:

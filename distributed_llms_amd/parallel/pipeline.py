@@ -92,6 +92,19 @@ class _Issued:
         self.step, self.sid, self.ids = step, sid, ids
 
 
+def pipeline_slots(ecfg: EngineConfig, pp: int) -> int:
+    """Microbatch slots of a pp-stage pipeline: one per stage keeps every stage busy only if the
+    ring closure were free; one spare slot covers the hops."""
+    return ecfg.microbatches if ecfg.microbatches > 0 else pp + 1
+
+
+def inflight_window(ecfg: EngineConfig, pp: int) -> int:
+    """Most microbatches the driver ever has in flight: two per slot (a step and its lookahead
+    successor).  Microbatch n is issued only after n - window completed at stage 0, i.e. after
+    every stage finished it -- transports with slot rings deeper than this never need credits."""
+    return 2 * pipeline_slots(ecfg, pp)
+
+
 class PipelineDriver:
     """Stage 0: scheduler + block manager owner; issues microbatches into the pipeline."""
 
@@ -102,9 +115,7 @@ class PipelineDriver:
         self.t = transport
         self.ecfg = ecfg
         self.bm = block_manager
-        # one microbatch per stage keeps every stage busy only if the ring closure were free;
-        # one spare slot covers the hops
-        self.num_slots = num_slots or (ecfg.microbatches if ecfg.microbatches > 0 else transport.num_stages + 1)
+        self.num_slots = num_slots or pipeline_slots(ecfg, transport.num_stages)
         self.scheduler = Scheduler(block_manager, self.num_slots, ecfg.max_batch, ecfg.max_prefill_tokens,
                                    ecfg.max_seq_len)
         self.mcfg = runner.stage.cfg
@@ -127,6 +138,7 @@ class PipelineDriver:
         return seq
 
     def _issue(self, step: Step, ids_dev: Optional[torch.Tensor] = None):
+        assert len(self.inflight) < 2 * self.num_slots, "in-flight window exceeded (see inflight_window)"
         hb = build_host_batch(step, self.bm, self.ecfg.kv_block_size,
                               None if step.is_prefill else self.runner.max_blocks, self.step_id)
         if self.tp is not None:

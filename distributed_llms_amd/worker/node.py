@@ -443,10 +443,11 @@ class WorkerNode:
         else:
             self.stage_runner = StageRunner(stage, ecfg, num_blocks=nb)
             from ..parallel.dist_engine import make_transport
+            from ..parallel.pipeline import inflight_window
             transport = make_transport(list(range(world)), stage_idx, ctx.ctrl_group, ctx.data_group, self.device,
                                        ctx.ring_group,
                                        hop=(max(ecfg.max_prefill_tokens, ecfg.max_batch), stage.cfg.hidden_size,
-                                            stage.dtype))
+                                            stage.dtype, inflight_window(ecfg, world)))
             if stage_idx == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.stage_runner, transport, ecfg, bm)

@@ -94,9 +94,9 @@ def _run_ranks(world, prompts, transport, rounds):
 @pytest.mark.parametrize("world", [2, 3])
 def test_multiprocess_gpu_pipeline_ipc(cuda, world):
     """The HIP-IPC data plane (parallel/ipc_transport.py): stage processes sharing the one
-    GPU hand activations over device to device through mapped peer slots + stream-ordered flags and
-    credits (RCCL refuses two ranks on one device, IPC does not); three rounds of ten requests
-    (ring reuse across rounds) reproduce the single-process engine token for token."""
+    GPU hand activations over device to device through mapped peer slots + stream-ordered flags
+    (RCCL refuses two ranks on one device, IPC does not); three rounds of ten requests (slot reuse
+    across rounds) reproduce the single-process engine token for token."""
     prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
     ref = LLMEngine(_mp_ecfg(1)).generate(prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
     res = _run_ranks(world, prompts, "ipc", rounds=3)
