@@ -7,7 +7,8 @@ dependency; every request thread only submits to the master's request futures):
 
   GET  /health                 {"state": "ready" | "degraded" | "idle", "workers": n}
   GET  /status                 the master's STATUS fan-out (workers, KV occupancy, metrics)
-  GET  /metrics                Prometheus text exposition of the request metrics
+  GET  /metrics                Prometheus text: request metrics + per-worker gauges (HBM, KV blocks,
+                               running / waiting sequences, microbatches executed)
   POST /generate               {"prompt": str | "prompt_ids": [int], "max_new_tokens", "temperature",
                                 "top_k", "top_p", "ignore_eos"} -> {"tokens", "text", "latency_s", ...}
   POST /v1/completions         OpenAI-style: {"prompt": str | [int] | [str...], "max_tokens", ...}
@@ -24,7 +25,7 @@ import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional, Tuple
 
-from ..utils.metrics import prometheus_text
+from ..utils.metrics import cluster_prometheus_text
 
 log = logging.getLogger("dllm.http")
 
@@ -75,7 +76,7 @@ class _Handler(BaseHTTPRequestHandler):
             elif self.path == "/status":
                 self._send(200, m.status())
             elif self.path == "/metrics":
-                self._send(200, prometheus_text(m.metrics.summary()), "text/plain; version=0.0.4")
+                self._send(200, cluster_prometheus_text(m.status()), "text/plain; version=0.0.4")
             else:
                 self._send(404, {"error": f"no route {self.path}"})
         except Exception as e:  # noqa: BLE001 - reported to the client

@@ -446,4 +446,5 @@ class MasterNode:
             except Exception as e:
                 reg[wid]["remote"] = {"error": repr(e)}
         return {"state": self.state, "model": self.model_spec, "num_shards": self.num_shards,
-                "stage_workers": self.stage_workers, "workers": reg, "metrics": self.metrics.summary()}
+                "stage_workers": self.stage_workers, "workers": reg, "metrics": self.metrics.summary(),
+                "pending_requests": len(self._tasks)}

@@ -70,3 +70,34 @@ def prometheus_text(summary: Dict[str, Optional[float]], prefix: str = "dllm") -
         lines.append(f"# TYPE {prefix}_{k} gauge")
         lines.append(f"{prefix}_{k} {float(v):.6g}")
     return "\n".join(lines) + "\n"
+
+
+# per-worker gauges of the master's STATUS fan-out (HBM used, KV blocks, queue depth)
+_WORKER_GAUGES = ("hbm_used_bytes", "hbm_total_bytes", "kv_free_blocks", "running", "waiting", "steps")
+
+
+def _label(v) -> str:
+    return str(v).replace("\\", "\\\\").replace('"', '\\"').replace("\n", " ")
+
+
+def cluster_prometheus_text(status: Dict, prefix: str = "dllm") -> str:
+    """Render ``MasterNode.status()`` as Prometheus gauges: the request metrics, the master's
+    pending requests, and one labelled series per worker for every numeric gauge it reported."""
+    out = [prometheus_text(status.get("metrics") or {}, prefix).rstrip("\n")]
+    if "pending_requests" in status:
+        out += [f"# TYPE {prefix}_pending_requests gauge", f"{prefix}_pending_requests {int(status['pending_requests'])}"]
+    out += [f"# TYPE {prefix}_workers gauge", f"{prefix}_workers {len(status.get('workers') or {})}"]
+    stage_of = {w: i for i, w in enumerate(status.get("stage_workers") or [])}
+    rows = {g: [] for g in _WORKER_GAUGES}
+    for wid, w in sorted((status.get("workers") or {}).items()):
+        remote = w.get("remote") or {}
+        labels = f'worker="{_label(wid)}",stage="{stage_of.get(wid, -1)}",role="{_label(remote.get("role", ""))}"'
+        for g in _WORKER_GAUGES:
+            v = remote.get(g)
+            if isinstance(v, (int, float)) and not isinstance(v, bool):
+                rows[g].append(f"{prefix}_worker_{g}{{{labels}}} {float(v):.6g}")
+    for g, lines in rows.items():
+        if lines:
+            out.append(f"# TYPE {prefix}_worker_{g} gauge")
+            out += lines
+    return "\n".join(x for x in out if x) + "\n"

@@ -155,7 +155,10 @@ def test_http_api_generate_completions_status_metrics(cluster):
         with urllib.request.urlopen(base + "/health", timeout=30) as r:
             assert json.loads(r.read())["state"] == "ready"
         with urllib.request.urlopen(base + "/metrics", timeout=30) as r:
-            assert b"dllm_requests" in r.read()
+            text = r.read().decode()
+        assert "dllm_requests" in text and "dllm_workers 2" in text and "dllm_pending_requests 0" in text
+        assert 'dllm_worker_kv_free_blocks{worker="' in text and 'stage="0"' in text and 'stage="1"' in text
+        assert "dllm_worker_steps{" in text
         with urllib.request.urlopen(base + "/status", timeout=60) as r:
             assert json.loads(r.read())["state"] == "ready"
         bad = urllib.request.Request(base + "/generate", data=b'{"prompt_ids": []}')
