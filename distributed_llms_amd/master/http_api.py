@@ -13,6 +13,9 @@ dependency; every request thread only submits to the master's request futures):
                                 "top_k", "top_p", "ignore_eos"} -> {"tokens", "text", "latency_s", ...}
   POST /v1/completions         OpenAI-style: {"prompt": str | [int] | [str...], "max_tokens", ...}
                                -> {"object": "text_completion", "choices": [...], "usage": {...}}
+  "stream": true               (either POST, one prompt) server-sent events: one ``data: {...}`` event
+                               per pipeline step that produced tokens (TOKENS messages from stage 0),
+                               then ``data: [DONE]``
 
 Batches of prompts submitted together are scheduled together (continuous batching on stage 0).
 """
@@ -85,6 +88,8 @@ class _Handler(BaseHTTPRequestHandler):
     def do_POST(self):
         try:
             body = self._body()
+            if body.get("stream") and self.path in ("/generate", "/v1/completions"):
+                return self._stream(body)
             if self.path == "/generate":
                 self._send(200, self._generate(body))
             elif self.path == "/v1/completions":
@@ -95,6 +100,44 @@ class _Handler(BaseHTTPRequestHandler):
             self._send(400, {"error": repr(e)})
         except Exception as e:  # noqa: BLE001 - worker failures, timeouts
             self._send(503, {"error": repr(e)})
+
+    def _stream(self, body: Dict[str, Any]):
+        """Server-sent events: token chunks as stage 0 produces them, then [DONE]."""
+        completions = self.path == "/v1/completions"
+        prompt = body["prompt_ids"] if "prompt_ids" in body else body.get("prompt", "")
+        ids = self._ids(prompt)
+        if not ids:
+            raise ValueError("empty prompt")
+        params = _sampling(body, default_max=16 if completions else 64,
+                           max_key="max_tokens" if completions else "max_new_tokens")
+        gen = self.master.stream(ids, timeout=self.timeout_s, **params)
+        first = next(gen, None)                       # errors before the first byte -> HTTP status
+        self.send_response(200)
+        self.send_header("Content-Type", "text/event-stream")
+        self.send_header("Cache-Control", "no-cache")
+        self.send_header("Connection", "close")
+        self.end_headers()
+        tok = self.master.tokenizer
+
+        def event(chunk):
+            if completions:
+                obj = {"object": "text_completion", "model": self.master.model_spec,
+                       "choices": [{"index": 0, "text": tok.decode(chunk), "tokens": chunk, "finish_reason": None}]}
+            else:
+                obj = {"tokens": chunk, "text": tok.decode(chunk)}
+            self.wfile.write(b"data: " + json.dumps(obj).encode() + b"\n\n")
+            self.wfile.flush()
+
+        try:
+            if first is not None:
+                event(first)
+            for chunk in gen:
+                event(chunk)
+            self.wfile.write(b"data: [DONE]\n\n")
+        except Exception as e:  # noqa: BLE001 - mid-stream failure: report in-band
+            self.wfile.write(b"data: " + json.dumps({"error": repr(e)}).encode() + b"\n\n")
+        self.wfile.flush()
+        self.close_connection = True
 
     def _ids(self, prompt) -> List[int]:
         if isinstance(prompt, str):

@@ -26,6 +26,7 @@ import itertools
 import json
 import logging
 import os
+import queue
 import socket
 import threading
 import time
@@ -75,6 +76,7 @@ class MasterNode:
         self._lock = threading.RLock()
         self._ids = itertools.count()
         self._tasks: Dict[str, cf.Future] = {}
+        self._streams: Dict[str, "queue.Queue"] = {}     # task_id -> (offset, new ids) chunks, None = done
         self._acks: Dict[str, cf.Future] = {}
         self._status_futs: Dict[str, cf.Future] = {}
         self._threads: List[threading.Thread] = []
@@ -173,10 +175,17 @@ class MasterNode:
                     self.workers[worker_id]["status"] = "loaded"
             if fut and not fut.done():
                 fut.set_result(header)
+        elif command == "TOKENS":
+            q = self._streams.get(header.get("task_id"))
+            if q is not None:
+                q.put((int(header.get("offset", 0)), unpack_ids(payload)))
         elif command == "RESULT":
             fut = self._tasks.pop(header.get("task_id"), None)
             if fut and not fut.done():
                 fut.set_result((header, unpack_ids(payload)))
+            q = self._streams.get(header.get("task_id"))
+            if q is not None:
+                q.put(None)                         # the stream's end: the full ids are in the future
         elif command == "STATUS_REPLY":
             fut = self._status_futs.pop(header.get("req"), None)
             if fut and not fut.done():
@@ -224,6 +233,8 @@ class MasterNode:
             if not fut.done():
                 fut.set_exception(exc)
         self._tasks.clear()
+        for q in list(self._streams.values()):
+            q.put(None)                               # streams end; their futures carry the error
 
     def _monitor(self):
         """Heartbeat-timeout eviction (the reference records last_heartbeat and never reads it, D15)."""
@@ -392,7 +403,8 @@ class MasterNode:
             time.sleep(1.0)
 
     # ---------------------------------------------------------------- inference
-    def submit(self, prompt_ids: Sequence[int], params: Optional[Dict[str, Any]] = None) -> cf.Future:
+    def submit(self, prompt_ids: Sequence[int], params: Optional[Dict[str, Any]] = None, _stream_queue=None,
+               _task_out=None) -> cf.Future:
         if self.state != "ready":
             raise WorkerFailure(f"pipeline not ready (state={self.state})")
         task_id = f"task_{next(self._ids)}_{int(time.time() * 1000)}"
@@ -400,6 +412,9 @@ class MasterNode:
         fut.t_submit = time.perf_counter()
         fut.task_id = task_id
         self._tasks[task_id] = fut
+        if _stream_queue is not None:
+            self._streams[task_id] = _stream_queue
+            _task_out["task_id"] = task_id
         with self._lock:
             w0 = self.workers.get(self.stage_workers[0])
         if w0 is None:
@@ -411,6 +426,35 @@ class MasterNode:
             self._tasks.pop(task_id, None)
             raise WorkerFailure("cannot send request to stage 0")
         return fut
+
+    def stream(self, prompt_ids: Sequence[int], timeout: float = 600, **params):
+        """Generate with token streaming: yields lists of new token ids as stage 0 produces them
+        (TOKENS messages, one per pipeline step that advanced the request); the last chunk is what
+        the final RESULT adds.  The chunks concatenate to exactly what :meth:`submit` returns."""
+        q: "queue.Queue" = queue.Queue()
+        # register the queue before the request can produce anything
+        task_hint = {}
+        fut = self.submit(prompt_ids, dict(params, stream=True), _stream_queue=q, _task_out=task_hint)
+        sent = 0
+        deadline = time.time() + timeout
+        try:
+            while True:
+                try:
+                    item = q.get(timeout=max(0.01, deadline - time.time()))
+                except queue.Empty:
+                    raise TimeoutError("stream timed out") from None
+                if item is None:
+                    break
+                off, ids = item
+                if off + len(ids) > sent:
+                    new = ids[sent - off:]
+                    sent += len(new)
+                    yield new
+            r = self._finish(fut, max(0.01, deadline - time.time()))
+            if len(r["tokens"]) > sent:
+                yield r["tokens"][sent:]
+        finally:
+            self._streams.pop(task_hint.get("task_id"), None)
 
     def _finish(self, fut: cf.Future, timeout: float):
         header, ids = fut.result(timeout=timeout)

@@ -500,8 +500,9 @@ class WorkerNode:
         from ..engine.sequence import SamplingParams
         ids = unpack_ids(payload) if payload else list(header.get("input_ids", []))
         params = SamplingParams.from_dict(header.get("params"))
+        stream = bool((header.get("params") or {}).get("stream"))
         with self._req_cv:
-            self._pending.append((sock, header.get("task_id"), ids, params))
+            self._pending.append((sock, header.get("task_id"), ids, params, stream))
             self._req_cv.notify()
 
     def _abort(self, task_id):
@@ -514,9 +515,11 @@ class WorkerNode:
                 sch.abort(s.seq_id)
 
     def _serve_loop(self):
-        """Stage 0: admit requests, step the pipeline, return finished sequences as RESULT."""
+        """Stage 0: admit requests, step the pipeline, return finished sequences as RESULT; requests
+        submitted with ``stream`` also get their new tokens as TOKENS messages after every step."""
         target = self.driver or self.engine
         owners: Dict[str, Any] = {}
+        streams: Dict[str, list] = {}          # task_id -> [sequence, tokens already sent]
         last_activity = time.time()
         keepalive_s = 60.0     # idle pipelines ping their followers so gloo/RCCL receives never time out
         while self.running and target is (self.driver or self.engine):
@@ -528,14 +531,25 @@ class WorkerNode:
                         last_activity = time.time()
                 batch, self._pending = self._pending, []
             last_activity = time.time()
-            for sock, task_id, ids, params in batch:
+            for sock, task_id, ids, params, stream in batch:
                 seq = target.add_request(ids, params, request_id=task_id)
                 owners[task_id] = sock
+                if stream:
+                    streams[task_id] = [seq, 0]
             if not target.has_work():
                 continue
             done = target.poll() if self.driver is not None else target.step()
+            for task_id, st in list(streams.items()):
+                seq, sent = st
+                # finished sequences' last tokens go out with their RESULT
+                out = seq.output if seq.finished else target.scheduler.sync_output(seq)
+                if not seq.finished and len(out) > sent and task_id in owners:
+                    self.proto.send_message(owners[task_id], "TOKENS", payload=pack_ids(out[sent:]),
+                                            metadata={"task_id": task_id, "offset": sent})
+                    st[1] = len(out)
             for s in done:
                 sock = owners.pop(s.request_id, None)
+                st = streams.pop(s.request_id, None)
                 if sock is None:
                     continue
                 meta = {"task_id": s.request_id, "finish_reason": s.finish_reason, "num_tokens": len(s.output),

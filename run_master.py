@@ -96,7 +96,7 @@ def main(argv=None):
                                   "p50_latency_ms": round(1000 * lat[len(lat) // 2], 2)}), flush=True)
             return 0
         while True:
-            cmd = input("\nEnter command (assign/distribute/inference/generate/status/metrics/exit): ").strip()
+            cmd = input("\nEnter command (assign/distribute/inference/stream/generate/status/metrics/exit): ").strip()
             if cmd == "assign":
                 print("Shard assignments:", master.assign_shards())
             elif cmd == "distribute":
@@ -106,6 +106,13 @@ def main(argv=None):
                 text = input("Enter text for inference: ")
                 res = master.run_inference(text, max_new_tokens=32)
                 print("Inference result:", json.dumps({k: res[k] for k in ("tokens", "text", "latency_s")}))
+            elif cmd == "stream":
+                # tokens printed as the pipeline produces them (TOKENS messages from stage 0)
+                text = input("Enter text for inference: ")
+                ids = master.tokenizer.encode(text)
+                for chunk in master.stream(ids, max_new_tokens=32):
+                    print(master.tokenizer.decode(chunk), end="", flush=True)
+                print()
             elif cmd.startswith("generate"):
                 n = int(cmd.split()[1]) if len(cmd.split()) > 1 else 8
                 res = master.generate([[5, 6, 7, 8]] * n, max_new_tokens=16)

@@ -67,8 +67,11 @@ def test_two_worker_pipeline_matches_single_process(cluster, model):
     assert [r["tokens"] for r in res] == ref
     text = m.run_inference("hello", max_new_tokens=4, timeout=60, ignore_eos=True)
     assert len(text["tokens"]) == 4 and isinstance(text["text"], str)
+    # token streaming (TOKENS messages from the stage-0 driver): several chunks, same tokens
+    chunks = list(m.stream(PROMPTS[2], max_new_tokens=6, ignore_eos=True, timeout=120))
+    assert sum(chunks, []) == ref[2] and len(chunks) >= 2
     st = m.status()
-    assert st["state"] == "ready" and st["metrics"]["requests"] == 4
+    assert st["state"] == "ready" and st["metrics"]["requests"] == 5
     assert {w["remote"]["role"] for w in st["workers"].values()} == {"driver", "follower"}
 
 
@@ -80,6 +83,8 @@ def test_single_worker_engine(cluster):
     res = m.generate(PROMPTS, max_new_tokens=5, ignore_eos=True, timeout=120)
     ref = LLMEngine(_cfg("synthetic:tiny-llama")).generate(PROMPTS, SamplingParams(max_new_tokens=5, ignore_eos=True))
     assert [r["tokens"] for r in res] == ref
+    chunks = list(m.stream(PROMPTS[1], max_new_tokens=5, ignore_eos=True, timeout=120))
+    assert sum(chunks, []) == ref[1] and len(chunks) >= 2
 
 
 def test_worker_failure_eviction_and_recovery(cluster):
@@ -161,6 +166,16 @@ def test_http_api_generate_completions_status_metrics(cluster):
         assert "dllm_worker_steps{" in text
         with urllib.request.urlopen(base + "/status", timeout=60) as r:
             assert json.loads(r.read())["state"] == "ready"
+        # server-sent events: chunks concatenate to the same greedy tokens
+        req = urllib.request.Request(base + "/v1/completions",
+                                     data=json.dumps({"prompt": PROMPTS[0], "max_tokens": 5, "ignore_eos": True,
+                                                      "stream": True}).encode())
+        with urllib.request.urlopen(req, timeout=120) as r:
+            assert r.headers["Content-Type"] == "text/event-stream"
+            events = [ln[len(b"data: "):] for ln in r.read().split(b"\n\n") if ln.startswith(b"data: ")]
+        assert events[-1] == b"[DONE]" and len(events) >= 2
+        streamed = [t for e in events[:-1] for t in json.loads(e)["choices"][0]["tokens"]]
+        assert streamed == expect
         bad = urllib.request.Request(base + "/generate", data=b'{"prompt_ids": []}')
         with pytest.raises(urllib.error.HTTPError) as ei:
             urllib.request.urlopen(bad, timeout=30)
