@@ -49,6 +49,9 @@ def parse(argv=None):
     ap.add_argument("--tp", type=int, default=0,
                     help="tensor-parallel group size (--parallelism tp: default all ranks; with pp: "
                          "every pipeline stage is a TP group of this size, dp x pp x tp)")
+    ap.add_argument("--moe", choices=["tp", "ep"], default="tp",
+                    help="MoE models under TP: slice every expert along I (tp) or give each rank whole "
+                         "experts (ep, expert parallelism)")
     ap.add_argument("--pp", type=int, default=0,
                     help="pipeline depth for --parallelism pp (default: all ranks); world/pp pipelines run as "
                          "data-parallel replicas, e.g. --gpus 8 --pp 4 = 2 pipelines of 4 stages")
@@ -75,7 +78,9 @@ def _par_name(args, world):
     else:
         pp = 1
     dp = world // (pp * tp)
-    parts = [f"dp{dp}" if dp > 1 else "", f"pp{pp}" if pp > 1 else "", f"tp{tp}" if tp > 1 else ""]
+    ep = tp > 1 and getattr(args, "moe", "tp") == "ep" and "mixtral" in args.model
+    parts = [f"dp{dp}" if dp > 1 else "", f"pp{pp}" if pp > 1 else "",
+             (f"ep{tp}" if ep else f"tp{tp}") if tp > 1 else ""]
     name = "x".join(p for p in parts if p)
     return name or f"dp{world}"
 

@@ -87,7 +87,7 @@ class ModelStage:
         holds its column / row / vocab shard of every layer (parallel/tensor_parallel.py)."""
         from ..parallel.tensor_parallel import TPGroup, check_divisible
         self.tp = tp if tp is not None else TPGroup(0, 1)
-        check_divisible(cfg, self.tp.size)
+        check_divisible(cfg, self.tp.size, self.tp.moe)
         # heads this rank computes (all of them without TP)
         self.hq = cfg.num_heads // self.tp.size
         self.hkv = cfg.num_kv_heads // self.tp.size
@@ -138,7 +138,7 @@ class ModelStage:
             return
         from ..parallel.tensor_parallel import shard_block, shard_vocab
         r, n = self.tp.rank, self.tp.size
-        self.layers = [shard_block(self.cfg, lw, r, n) for lw in self.layers]
+        self.layers = [shard_block(self.cfg, lw, r, n, self.tp.moe) for lw in self.layers]
         if self.is_last:
             self.head["lm_head_tp"] = shard_vocab(self.lm_head_weight(full=True), r, n)
             self.head.pop("lm_head", None)
@@ -152,7 +152,7 @@ class ModelStage:
             lw = {n: W.synth_tensor(seed, l, n, s, self.dtype, self.device) for n, s in shapes.items()}
             if self.tp.enabled:
                 from ..parallel.tensor_parallel import shard_block
-                lw = shard_block(cfg, lw, self.tp.rank, self.tp.size)     # one full layer at a time
+                lw = shard_block(cfg, lw, self.tp.rank, self.tp.size, self.tp.moe)   # one full layer at a time
             self.layers.append(lw)
         if self.needs_embed():
             self.embed = W.synth_embed(cfg, seed, self.dtype, self.device)
@@ -237,7 +237,7 @@ class ModelStage:
     def _mlp(self, h: torch.Tensor, lw: Dict[str, torch.Tensor]) -> torch.Tensor:
         if self.cfg.is_moe:
             out = ops.moe_forward(h, lw["router"], lw["experts_gate_up"], lw["experts_down"],
-                                  self.cfg.experts_per_token)
+                                  self.cfg.experts_per_token, self.tp.expert_offset(self.cfg.num_experts))
             return self.tp.all_reduce_(out) if self.tp.enabled else out
         # defer: the down projection's split-K reduce is fused into the next residual-add + RMSNorm
         # (under TP the partial [T, H] is all-reduced first, so it is materialised)

@@ -344,7 +344,8 @@ def moe_mlp(x, w_gate_up, w_down, topk_w, topk_ids):
     return moe.mlp(x, w_gate_up, w_down, topk_w, topk_ids)
 
 
-def moe_forward(x, w_router, w_gate_up, w_down, top_k: int):
-    """Full Mixtral sparse MLP: route + expert SwiGLU MLPs + weighted combine."""
+def moe_forward(x, w_router, w_gate_up, w_down, top_k: int, expert_offset: int = 0):
+    """Full Mixtral sparse MLP: route + expert SwiGLU MLPs + weighted combine (``expert_offset``:
+    the weights hold experts [offset, offset + E_local) -- expert parallelism, ops/moe.py)."""
     from . import moe
-    return moe.forward(x, w_router, w_gate_up, w_down, top_k)
+    return moe.forward(x, w_router, w_gate_up, w_down, top_k, expert_offset)

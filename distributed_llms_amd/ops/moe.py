@@ -40,15 +40,24 @@ def mlp(x, w_gate_up, w_down, topk_w, topk_ids):
 
 
 def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor,
-            top_k: int) -> torch.Tensor:
+            top_k: int, expert_offset: int = 0) -> torch.Tensor:
+    """``w_gate_up`` / ``w_down`` may hold a contiguous range of the experts (expert parallelism):
+    experts ``[expert_offset, expert_offset + w_gate_up.shape[0])`` of the router's E.  Routing is
+    always over all E; tokens routed elsewhere contribute zero here, so the expert-parallel
+    group's sum (an all-reduce) is the full MoE output."""
+    e_all = w_router.shape[0]
+    if not (0 <= expert_offset and expert_offset + w_gate_up.shape[0] <= e_all):
+        raise ValueError(f"experts [{expert_offset}, {expert_offset + w_gate_up.shape[0]}) outside the router's {e_all}")
     if not x.is_cuda:
         tw, tid = ref.moe_route(ref.linear(x, w_router), top_k)
-        return ref.moe_mlp(x, w_gate_up, w_down, tw, tid)
+        return ref.moe_mlp(x, w_gate_up, w_down, tw, tid - expert_offset)
     from . import linear, silu_mul
     k = _ext.kernels()
     st = torch.cuda.current_stream().cuda_stream
     t, h = x.shape
-    e, two_i, _ = w_gate_up.shape
+    e_loc, two_i, _ = w_gate_up.shape
+    e = e_all
+    ep = e_loc != e_all
     inter = two_i // 2
     if not (x.is_contiguous() and w_gate_up.is_contiguous() and w_down.is_contiguous()):
         raise ValueError("moe: operands must be contiguous")
@@ -68,28 +77,30 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
         logits = linear(x, w_router)
         k.moe_route(logits.data_ptr(), t, e, top_k, topk_w.data_ptr(), topk_ids.data_ptr(), counts.data_ptr(),
                     offsets.data_ptr(), sorted_tok.data_ptr(), inv.data_ptr(), st)
-    ys = torch.empty(t * top_k, h, dtype=x.dtype, device=dev)
+    # expert parallel: only this rank's experts fill their slot rows; the others stay zero
+    ys = (torch.zeros if ep else torch.empty)(t * top_k, h, dtype=x.dtype, device=dev)
+    # the local experts' counts / offsets are a contiguous slice of the routing arrays
+    cnt_p, off_p = counts.data_ptr() + 4 * expert_offset, offsets.data_ptr() + 4 * expert_offset
     if t <= GROUPED_MAX_TOKENS:
         act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
         rows = -(-t * top_k // e)        # expected rows per expert picks the kernel's row tile
         if 0 < WIDE_MIN_PAIRS <= t * top_k and x.dtype == torch.bfloat16 and two_i % 128 == 0 and h % 128 == 0 \
                 and h % 64 == 0 and inter % 64 == 0:
             k.moe_wide_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
-                            counts.data_ptr(), offsets.data_ptr(), e, two_i, h, 1, st)
-            k.moe_wide_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), counts.data_ptr(),
-                            offsets.data_ptr(), e, h, inter, 0, st)
+                            cnt_p, off_p, e_loc, two_i, h, 1, st)
+            k.moe_wide_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, 0, st)
         else:
             k.moe_grouped_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
-                               counts.data_ptr(), offsets.data_ptr(), e, two_i, h, 1, rows, GROUPED_VARIANT, st)
-            k.moe_grouped_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), counts.data_ptr(),
-                               offsets.data_ptr(), e, h, inter, 0, rows, GROUPED_VARIANT, st)
+                               cnt_p, off_p, e_loc, two_i, h, 1, rows, GROUPED_VARIANT, st)
+            k.moe_grouped_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, 0,
+                               rows, GROUPED_VARIANT, st)
     else:
         xs = x.index_select(0, sorted_tok.long())
         off = offsets.cpu().tolist()          # prefill only: eager, host sync is fine here
-        for ex in range(e):
-            a, b = off[ex], off[ex + 1]
+        for j in range(e_loc):
+            a, b = off[expert_offset + j], off[expert_offset + j + 1]
             if b > a:
-                ys[a:b] = F.linear(silu_mul(F.linear(xs[a:b], w_gate_up[ex])), w_down[ex])
+                ys[a:b] = F.linear(silu_mul(F.linear(xs[a:b], w_gate_up[j])), w_down[j])
     out = torch.empty_like(x)
     k.moe_combine(out.data_ptr(), ys.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), t, h, top_k, st)
     return out

@@ -21,7 +21,7 @@ def _sync(ctx):
 def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=None):
     pp = (getattr(args, "pp", 0) or None) if args.parallelism == "pp" else 1
     tp = getattr(args, "tp", 0) or (int(os.environ.get("WORLD_SIZE", "1")) if args.parallelism == "tp" else 1)
-    ctx = init_distributed(pp=pp, tp=tp)
+    ctx = init_distributed(pp=pp, tp=tp, moe=getattr(args, "moe", "tp"))
     world = ctx.world
     # pipeline: prefill in ~8K-token microbatches (M large enough for full-rate GEMMs) so the
     # fill/drain bubble of the prefill phase is (pp-1) x ~8K-token stage times, not (pp-1) x a

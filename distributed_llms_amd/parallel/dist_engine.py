@@ -76,8 +76,9 @@ class DistContext:
 
 
 def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
-                     timeout_s: float = 1800, tp: int = 1) -> DistContext:
+                     timeout_s: float = 1800, tp: int = 1, moe: str = "tp") -> DistContext:
     """dp x pp x tp over the launched world (dp = world / (pp * tp); pp None = world / tp).
+    ``moe``: how a TP group splits MoE experts ("tp": along I, "ep": whole experts per rank).
 
     Environment knobs (tests / rehearsal only):
       DLLM_SHARE_GPU=1       ranks share the visible GPUs round-robin (local_rank % device_count)
@@ -121,7 +122,7 @@ def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
                 g = dist.new_group(ranks=ranks, backend=p2p_backend, timeout=tmo)
                 c = dist.new_group(ranks=ranks, backend="gloo", timeout=tmo)
                 if rank in ranks:
-                    tpg = TPGroup(rank - ranks[0], tp, g, c, ranks[0])
+                    tpg = TPGroup(rank - ranks[0], tp, g, c, ranks[0], moe=moe)
     # one {first, last} group per lane for the sampled-ids ring closure
     rings = ()
     if pp > 1:

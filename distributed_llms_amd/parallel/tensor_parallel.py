@@ -7,6 +7,10 @@ each) shares every layer of its stage:
   column-parallel   wqkv      rows of this rank's q heads | kv heads (GQA groups stay whole)
                     w_gate_up rows of this rank's slice of I, gate and up halves kept aligned
                     experts   (MoE) each expert's I sliced the same way; the router replicated
+  expert-parallel   experts   (MoE, ``moe="ep"``) whole experts [r E/size, (r+1) E/size) per rank
+                              instead: routing stays global (replicated router), a rank runs
+                              only its experts' tokens, and the same all-reduce sums the group's
+                              partial MoE outputs -- every expert GEMM at full I, ~T k / E rows
   row-parallel      wo        the matching q-head columns   -> partial [T, H] -> all-reduce
                     w_down    the matching I columns        -> partial [T, H] -> all-reduce
   vocab-parallel    lm_head   rows [r V/size, (r+1) V/size)  -> greedy: distributed argmax
@@ -43,10 +47,15 @@ class TPGroup:
     group: object = None      # data collectives (RCCL on GPU, gloo on CPU)
     ctrl: object = None       # gloo: step metadata broadcast
     leader: int = 0           # global rank of the group's rank 0
+    moe: str = "tp"           # MoE experts: "tp" = every expert's I sliced, "ep" = whole experts per rank
 
     @property
     def enabled(self) -> bool:
         return self.size > 1
+
+    def expert_offset(self, num_experts: int) -> int:
+        """First global expert this rank holds (expert parallel), else 0."""
+        return self.rank * (num_experts // self.size) if self.moe == "ep" and self.size > 1 else 0
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
@@ -74,20 +83,24 @@ class TPGroup:
 
 
 # ------------------------------------------------------------------ weight sharding
-def check_divisible(cfg, size: int):
+def check_divisible(cfg, size: int, moe: str = "tp"):
     if size <= 1:
         return
-    bad = [n for n, v in (("num_heads", cfg.num_heads), ("num_kv_heads", cfg.num_kv_heads),
-                          ("intermediate_size", cfg.intermediate_size), ("vocab_size", cfg.vocab_size))
-           if v % size]
+    if moe not in ("tp", "ep"):
+        raise ValueError(f"moe parallel mode {moe!r}: 'tp' or 'ep'")
+    dims = [("num_heads", cfg.num_heads), ("num_kv_heads", cfg.num_kv_heads), ("vocab_size", cfg.vocab_size)]
+    dims.append(("num_experts", cfg.num_experts) if cfg.is_moe and moe == "ep"
+                else ("intermediate_size", cfg.intermediate_size))
+    bad = [n for n, v in dims if v % size]
     if bad:
         raise ValueError(f"tensor parallel size {size} must divide {', '.join(bad)} of {cfg.name}")
     if cfg.arch == "gpt2":
         raise ValueError("tensor parallelism is implemented for the llama / mixtral families")
 
 
-def shard_block(cfg, w: Dict[str, torch.Tensor], rank: int, size: int) -> Dict[str, torch.Tensor]:
-    """Full runtime block tensors -> this rank's shard (new contiguous tensors)."""
+def shard_block(cfg, w: Dict[str, torch.Tensor], rank: int, size: int, moe: str = "tp") -> Dict[str, torch.Tensor]:
+    """Full runtime block tensors -> this rank's shard (new contiguous tensors).  ``moe="ep"``:
+    the MoE experts are split whole (expert parallelism) instead of sliced along I."""
     if size <= 1:
         return w
     d = cfg.head_dim
@@ -101,7 +114,11 @@ def shard_block(cfg, w: Dict[str, torch.Tensor], rank: int, size: int) -> Dict[s
     out["wqkv"] = torch.cat([qkv[q0:q0 + hq * d], qkv[k0:k0 + hkv * d], qkv[v0:v0 + hkv * d]], 0).contiguous()
     out["wo"] = w["wo"][:, q0:q0 + hq * d].contiguous()
     i, a = cfg.intermediate_size, rank * i_l
-    if cfg.is_moe:
+    if cfg.is_moe and moe == "ep":
+        e_l = cfg.num_experts // size
+        out["experts_gate_up"] = w["experts_gate_up"][rank * e_l:(rank + 1) * e_l].contiguous()
+        out["experts_down"] = w["experts_down"][rank * e_l:(rank + 1) * e_l].contiguous()
+    elif cfg.is_moe:
         gu = w["experts_gate_up"]
         out["experts_gate_up"] = torch.cat([gu[:, a:a + i_l], gu[:, i + a:i + a + i_l]], 1).contiguous()
         out["experts_down"] = w["experts_down"][:, :, a:a + i_l].contiguous()

@@ -57,6 +57,25 @@ def test_row_and_column_shards_sum_to_the_full_projection(name, size):
         torch.testing.assert_close(part, ref_mlp, rtol=1e-4, atol=1e-4)
 
 
+def test_expert_parallel_shards_sum_to_the_full_moe():
+    """moe="ep": each rank holds whole experts; with routing over all experts and the other ranks'
+    tokens contributing zero, the group's partial MoE outputs sum to the full sparse MLP."""
+    cfg = get_model_config("tiny-mixtral")
+    w = W.synth_block(cfg, 0, 5, torch.float32, "cpu")
+    x = torch.randn(7, cfg.hidden_size)
+    from distributed_llms_amd import ops
+    full = ops.moe_forward(x, w["router"], w["experts_gate_up"], w["experts_down"], cfg.experts_per_token)
+    for size in (2, 4):
+        shards = [T.shard_block(cfg, w, r, size, moe="ep") for r in range(size)]
+        assert shards[0]["experts_gate_up"].shape[0] == cfg.num_experts // size
+        parts = [ops.moe_forward(x, s["router"], s["experts_gate_up"], s["experts_down"], cfg.experts_per_token,
+                                 T.TPGroup(r, size, moe="ep").expert_offset(cfg.num_experts))
+                 for r, s in enumerate(shards)]
+        torch.testing.assert_close(sum(parts), full, rtol=1e-5, atol=1e-5)
+    with pytest.raises(ValueError):
+        T.check_divisible(cfg, 8, moe="ep")                  # 4 experts
+
+
 def test_divisibility_is_checked():
     with pytest.raises(ValueError):
         T.check_divisible(get_model_config("tiny-llama"), 4)          # 2 kv heads
@@ -80,14 +99,14 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, tp, model, port, out_q, pp=1):
+def _rank_main(rank, world, tp, model, port, out_q, pp=1, moe="tp"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     import torch.distributed as dist
     from distributed_llms_amd.parallel.dist_engine import RankRole, init_distributed
     try:
-        ctx = init_distributed(pp=pp, backend="gloo", tp=tp)
+        ctx = init_distributed(pp=pp, backend="gloo", tp=tp, moe=moe)
         role = RankRole(ctx, _ecfg(model, num_workers=pp))
         res = []
         for rnd in range(2):       # followers return on ROUND_END and serve the next round
@@ -104,13 +123,17 @@ def _rank_main(rank, world, tp, model, port, out_q, pp=1):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("model,world,tp", [("tiny-llama", 2, 2), ("tiny-mixtral", 2, 2), ("tiny-llama", 4, 2)])
-def test_multiprocess_tensor_parallel_matches_single(model, world, tp):
+@pytest.mark.parametrize("model,world,tp,moe", [("tiny-llama", 2, 2, "tp"), ("tiny-mixtral", 2, 2, "tp"),
+                                                ("tiny-llama", 4, 2, "tp"), ("tiny-mixtral", 2, 2, "ep"),
+                                                ("tiny-mixtral", 4, 2, "ep")])
+def test_multiprocess_tensor_parallel_matches_single(model, world, tp, moe):
+    """dp x tp groups (and, for Mixtral, expert parallelism inside the group: moe="ep") generate the
+    single-process engine's greedy tokens."""
     expected = LLMEngine(_ecfg(model)).generate(PROMPTS, PARAMS)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, tp, model, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, tp, model, port, q, 1, moe)) for r in range(world)]
     for p in procs:
         p.start()
     results = {}

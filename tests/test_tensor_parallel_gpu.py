@@ -1,7 +1,8 @@
 """Tensor parallelism on ONE GPU: two torch.distributed ranks share cuda:0 (collectives over gloo,
 RCCL refuses two ranks on one device) and run the TP forward on the HIP kernels -- local head
-counts in the fused decode attention, sharded GEMM shapes, vocab-parallel argmax -- against
-the single-process engine."""
+counts in the fused decode attention, sharded GEMM shapes, vocab-parallel argmax, and for
+Mixtral expert parallelism (whole experts per rank through the grouped MoE kernels' expert
+slices) -- against the single-process engine."""
 import pytest
 import torch
 
@@ -15,22 +16,22 @@ PROMPTS = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
 PARAMS = SamplingParams(max_new_tokens=8, ignore_eos=True)
 
 
-def _ecfg():
-    # tiny-llama: 4 q heads / 2 kv heads, so tp=2 keeps a whole GQA group per rank
-    return EngineConfig(model="tiny-llama", dtype="bfloat16", device="cuda", max_batch=4, max_seq_len=256,
+def _ecfg(model="tiny-llama"):
+    # tiny-llama / tiny-mixtral: 4 q heads / 2 kv heads, so tp=2 keeps a whole GQA group per rank
+    return EngineConfig(model=model, dtype="bfloat16", device="cuda", max_batch=4, max_seq_len=256,
                         num_kv_blocks=128, graph_batch_sizes=(1, 2, 4), seed=3)
 
 
-def _rank(rank, world, port, out_q):
+def _rank(rank, world, port, out_q, model="tiny-llama", moe="tp"):
     import os
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), DLLM_SHARE_GPU="1", DLLM_DATA_BACKEND="gloo")
     import torch.distributed as dist
     from distributed_llms_amd.parallel.dist_engine import RankRole, init_distributed
     try:
-        ctx = init_distributed(pp=1, tp=world)
+        ctx = init_distributed(pp=1, tp=world, moe=moe)
         assert ctx.device == "cuda:0" and ctx.tpg.size == world
-        role = RankRole(ctx, _ecfg())
+        role = RankRole(ctx, _ecfg(model))
         seqs = [role.add_request(q, PARAMS) for q in PROMPTS] if role.is_driver else []
         role.run_round()
         role.shutdown()
@@ -43,17 +44,18 @@ def _rank(rank, world, port, out_q):
 
 
 @pytest.mark.slow
-def test_tensor_parallel_two_ranks_on_one_gpu(cuda):
+@pytest.mark.parametrize("model,moe", [("tiny-llama", "tp"), ("tiny-mixtral", "ep")])
+def test_tensor_parallel_two_ranks_on_one_gpu(cuda, model, moe):
     import socket
     import torch.multiprocessing as mp
-    ref = LLMEngine(_ecfg()).generate(PROMPTS, PARAMS)
+    ref = LLMEngine(_ecfg(model)).generate(PROMPTS, PARAMS)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
-    procs = [ctxm.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctxm.Process(target=_rank, args=(r, 2, port, q, model, moe)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
