@@ -98,7 +98,7 @@ def wide(a, flush):
             # one HIP graph per implementation: `copies` back-to-back calls, each on its own weight
             # copy (launch overhead out of the measurement, like the engine's captured decode step)
             impls = {
-                "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=1),
+                "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=gemm.WIDE_VARIANT),
                 **{f"v{v}": (lambda w, v=v: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=v))
                    for v in a.variants},
                 **({"sq": lambda w: gemm.linear_sq(x, w, swiglu=sw, variant=4),
