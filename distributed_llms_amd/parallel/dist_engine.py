@@ -262,3 +262,5 @@ class RankRole:
             self.driver.shutdown()
         elif self.runner is not None:
             stage_worker_loop(self.runner, self.transport, stop_on_round_end=False)
+        if hasattr(getattr(self, "transport", None), "close"):
+            self.transport.close()          # IPC: unmap the peers' exports once this rank has drained

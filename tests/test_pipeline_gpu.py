@@ -46,9 +46,7 @@ def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1):
         seqs = [role.add_request(q, p) for q in prompts] if role.is_driver else []
         role.run_round()
         outs.append([s.output for s in seqs])
-    role.shutdown()
-    if transport == "ipc":
-        role.transport.close()
+    role.shutdown()                # (IPC: also unmaps the peer slots)
     dist.barrier(group=ctx.ctrl_group)
     out_q.put((rank, outs))
     dist.destroy_process_group()
