@@ -31,8 +31,6 @@ def load_tokenizer(model_path: str):
 
 def load_model(model_id: str, device_map: str = "auto", dtype: Optional[str] = None) -> Tuple[object, object]:
     """Load a checkpoint dir (HF layout or ``shards/``) or a ``synthetic:<preset>`` into one stage."""
-    import torch
-
     from ..config import get_model_config, resolve_device, torch_dtype
     from ..models.stage import ModelStage
     from .shard_manager import iter_checkpoint

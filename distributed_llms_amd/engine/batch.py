@@ -7,7 +7,7 @@ uploads into its :class:`BatchMeta` device tensors.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Optional
 
 import numpy as np
 import torch

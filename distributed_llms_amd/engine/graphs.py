@@ -13,7 +13,6 @@ from typing import Dict, Optional, Tuple
 
 import torch
 
-from .. import ops
 from ..models.stage import BatchMeta, ModelStage
 from .batch import HostBatch, next_pow2
 

@@ -5,7 +5,7 @@ use softmax + top-k/top-p + multinomial in torch (fp32).
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence as Seq
+from typing import Optional, Sequence as Seq
 
 import torch
 

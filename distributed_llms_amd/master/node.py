@@ -23,7 +23,6 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import itertools
-import json
 import logging
 import os
 import queue

@@ -22,8 +22,7 @@ how the pipeline schedule is exercised on the single-GPU test box.
 from __future__ import annotations
 
 import queue
-import threading
-from typing import Dict, Optional, Tuple
+from typing import Optional
 
 import numpy as np
 import torch

@@ -8,7 +8,7 @@ the text REPL end to end with random-init models.
 """
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import List
 
 
 class ByteTokenizer:

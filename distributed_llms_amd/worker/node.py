@@ -26,12 +26,11 @@ import threading
 import time
 from typing import Any, Dict, List, Optional
 
-import numpy as np
 import torch
 
-from ..config import EngineConfig, ModelConfig, get_model_config, resolve_device, torch_dtype
+from ..config import EngineConfig, ModelConfig, get_model_config, resolve_device
 from ..models import weights as W
-from ..models.stage import BatchMeta, KVCache, ModelStage
+from ..models.stage import BatchMeta, ModelStage
 from ..network.protocol import MessageProtocol, pack_ids, pack_tensors, unpack_ids, unpack_tensors
 
 log = logging.getLogger("dllm.worker")
@@ -411,7 +410,6 @@ class WorkerNode:
         from ..checkpoint.shard_manager import load_shard_bytes, load_shard_file
         from ..engine.llm_engine import LLMEngine, build_stage, make_block_manager
         from ..engine.runner import StageRunner, plan_kv_blocks
-        from ..parallel.comm import DistTransport
         from ..parallel.pipeline import PipelineDriver, stage_worker_loop
 
         self._teardown_pipeline(send_stop=False)
