@@ -37,6 +37,13 @@ class _FakeSock:
         self.pos += k
         return k
 
+    def recv(self, n, flags=0):
+        # short reads even with MSG_WAITALL (what a signal or a peer close can cause): the
+        # receiver must loop
+        buf = bytearray(n)
+        k = self.recv_into(memoryview(buf), n)
+        return bytes(buf[:k])
+
 
 class TestMessageProtocol(unittest.TestCase):
     @patch("socket.socket")
