@@ -12,7 +12,7 @@ payload=None, metadata=None) -> bool``, ``receive_message(sock, timeout=60) ->
   length, header CRC-32 -- encoded/validated by the native codec in ``_C_runtime``), a
   JSON header, and the raw payload read by one ``MSG_WAITALL`` receive straight into the
   result (O(n), no zero-fill, no copy; short reads continue with ``recv_into``).  Nothing
-  received is ever unpickled (bench/protocol_bench.py: 16-300x the reference framing's
+  received is ever unpickled (bench/protocol_bench.py: ~20x (1 MiB) to ~150-300x (16 MiB) the reference framing's
   throughput from 1 to 16 MiB, profiles/protocol_vs_reference.md).
 
 ``send_message``/``receive_message`` are static, so both ``MessageProtocol.send_message(sock,
