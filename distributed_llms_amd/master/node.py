@@ -353,8 +353,13 @@ class MasterNode:
         master_addr = self.config.host if self.config.host not in ("0.0.0.0", "") else "127.0.0.1"
         dist = {"master_addr": os.environ.get("DLLM_DIST_ADDR", "127.0.0.1" if master_addr == "0.0.0.0" else master_addr),
                 "master_port": _free_port()}
+        # stage workers sharing a host: CPU workers split its cores instead of oversubscribing them
+        with self._lock:
+            hosts = [(self.workers.get(w) or {}).get("capabilities", {}).get("host") for w in self.stage_workers]
+        hosts += [None] * (n - len(hosts))
+        host_workers = [sum(1 for h in hosts if h is not None and h == hosts[i]) or 1 for i in range(n)]
         return [{"shard_id": i, "stage": i, "num_stages": n, "layer_range": list(ranges[i]),
-                 "unit_range": list(unit_ranges[i]),
+                 "unit_range": list(unit_ranges[i]), "host_workers": host_workers[i],
                  "shard_path": paths[i], "engine_config": ed, "dist": dist} for i in range(n)]
 
     def distribute_shards(self, timeout: float = 1800.0, ship_bytes: bool = False) -> Dict[str, Any]:
