@@ -97,8 +97,10 @@ def wide(a, flush):
             x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
             # one HIP graph per implementation: `copies` back-to-back calls, each on its own weight
             # copy (launch overhead out of the measurement, like the engine's captured decode step)
+            split = (a.splits or gemm.wide_splits(m, n, k, sw)) > 1
+            wv = gemm.WIDE_VARIANT_SPLIT if split else gemm.WIDE_VARIANT     # the engine's choice
             impls = {
-                "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=gemm.WIDE_VARIANT),
+                "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=wv),
                 **{f"v{v}": (lambda w, v=v: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=v))
                    for v in a.variants},
                 **({"sq": lambda w: gemm.linear_sq(x, w, swiglu=sw, variant=4),

@@ -224,7 +224,7 @@ class EngineConfig:
     device: str = "auto"               # "auto" -> cuda if available else cpu
     num_workers: int = 1               # pipeline stages (one process / GPU each)
     dp_replicas: int = 1               # data-parallel replica groups (dp x pp = world)
-    microbatches: int = 0              # 0 -> = number of stages
+    microbatches: int = 0              # 0 -> pipeline_slots(): stages + 1 on GPUs, stages on CPUs
     # single-GPU engine: microbatch slots interleaved on HIP streams.  1 by default: decode GEMMs
     # are weight-streaming, and two half-batches stream every weight twice (measured 16.2k vs
     # 21.0k tok/s at batch 256, profiles/dual_stream.txt)
@@ -292,6 +292,25 @@ class EngineConfig:
     def apply_overrides(self, **kw) -> "EngineConfig":
         kw = {k: v for k, v in kw.items() if v is not None}
         return dataclasses.replace(self, **kw)
+
+
+def pipeline_slots(ecfg: "EngineConfig", pp: int, device=None) -> int:
+    """Microbatch slots of a pp-stage pipeline (``ecfg.microbatches`` when set).
+
+    GPU stages: pp + 1 -- one per stage keeps every stage busy only if the ring closure (sampled
+    ids back to stage 0) were free; the spare slot covers the hops.  CPU stages: pp -- a CPU
+    stage at these batch sizes is bound by streaming its weights, which every extra microbatch
+    re-reads (GPT-2 small on two 4-core stages: 140 tok/s with 3 slots, 184 with 2), while its
+    hops are cheap next to a step.  ``device`` is the stages' device (``ecfg.device`` if None).
+    """
+    if ecfg.microbatches > 0:
+        return ecfg.microbatches
+    if pp <= 1:
+        return 1
+    dev = str(device if device is not None else ecfg.device)
+    if dev == "auto":
+        dev = resolve_device(dev)
+    return pp if dev.startswith("cpu") else pp + 1
 
 
 def resolve_device(spec: str = "auto") -> str:

@@ -9,7 +9,7 @@ from typing import Optional
 
 import torch
 
-from ..config import EngineConfig, ModelConfig
+from ..config import EngineConfig, ModelConfig, pipeline_slots
 from ..models.stage import KVCache, ModelStage
 from ..ops.tuning import enable_tuned_gemms
 from ..utils.tracing import get_tracer
@@ -27,8 +27,8 @@ def plan_kv_blocks(mcfg: ModelConfig, num_layers: int, ecfg: EngineConfig, devic
     if ecfg.num_kv_blocks > 0:
         return ecfg.num_kv_blocks
     per_seq = -(-ecfg.max_seq_len // bs)
-    # microbatch slots in flight: the pipeline driver runs pp + 1 (parallel/pipeline.py)
-    slots = ecfg.microbatches or (ecfg.num_workers + 1 if ecfg.num_workers > 1 else 1)
+    # microbatch slots in flight (the pipeline driver's, config.pipeline_slots)
+    slots = pipeline_slots(ecfg, ecfg.num_workers, device)
     want = ecfg.max_batch * slots * per_seq + 2
     per_block = max(1, KVCache.bytes_per_block(num_layers, num_kv_heads or mcfg.num_kv_heads, mcfg.head_dim, bs))
     dev = torch.device(device)

@@ -277,6 +277,13 @@ class MasterNode:
         self.shard_manager = ModelShardManager(self.model_path, num_shards, self.model_config)
         return self.shard_manager.shard_model()
 
+    def _plan_device(self) -> str:
+        """The cost model the stage planner uses: "cpu" when every (stage) worker is a CPU worker."""
+        with self._lock:
+            ws = [self.workers[w] for w in (self.stage_workers or list(self.workers)) if w in self.workers]
+        devs = [str(w.get("capabilities", {}).get("device", "cuda")) for w in ws]
+        return "cpu" if devs and all(d.startswith("cpu") for d in devs) else "cuda"
+
     def stage_weight_bytes(self) -> List[int]:
         """bf16/fp16 weight bytes each pipeline stage will hold (layers + embedding / LM head)."""
         from ..parallel.planner import plan_units
@@ -284,7 +291,8 @@ class MasterNode:
         n = self.num_shards
         if self.shard_manager is not None:
             return [os.path.getsize(p) for p in self.shard_manager.get_shard_paths()]
-        up = plan_units(cfg, n, batch=self.config.max_batch, ctx=max(32, self.config.max_seq_len // 2))
+        up = plan_units(cfg, n, batch=self.config.max_batch, ctx=max(32, self.config.max_seq_len // 2),
+                            device=self._plan_device())
         width = 4 if self.config.dtype == "float32" else 2
         per_layer = cfg.layer_param_count() * width
         out = []
@@ -342,7 +350,8 @@ class MasterNode:
             unit_ranges = [(2 * a, 2 * b) for a, b in ranges]
             paths = self.shard_manager.get_shard_paths()
         else:
-            up = plan_units(cfg, n, batch=self.config.max_batch, ctx=max(32, self.config.max_seq_len // 2))
+            up = plan_units(cfg, n, batch=self.config.max_batch, ctx=max(32, self.config.max_seq_len // 2),
+                            device=self._plan_device())
             ranges = list(up.ranges)
             unit_ranges = list(up.units)
             paths = [None] * n

@@ -87,8 +87,13 @@ def _use_tiled(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool
 WIDE = {t for t in os.environ.get("DLLM_WIDE", "auto").split(",") if t and t != "none"}
 # gemm_wide variant: 1 = LDS-DMA pieces interleaved with the MFMAs (weights nt where the grid has no
 # K split); | 32 = fragment reads in asm with one lgkmcnt wait per MFMA row instead of hipcc's
-# lgkmcnt(0) before a K-tile's first MFMA (+0.8 % tok/s on 8B, +0.5 % on 70B at B = 256; bit-exact)
+# lgkmcnt(0) before a K-tile's first MFMA (bit-exact).  In-engine (profiles/wide_gemm.md) bit 32
+# speeds up the unsplit SwiGLU gate|up grid (68.7 -> 66.9 us at B = 256) and slows the split-K
+# qkv / o / down grids (24.7 -> 26.3 us), so split grids keep variant 1: Llama-3-8B B = 256
+# 27,014 (all 1) / 26,896 (all 33) / 27,123 tok/s (this split), interleaved on one box.
 WIDE_VARIANT = int(os.environ.get("DLLM_WIDE_VARIANT", "33"))
+# variant for split-K grids (qkv / o / down at decode M)
+WIDE_VARIANT_SPLIT = int(os.environ.get("DLLM_WIDE_VARIANT_SPLIT", "1"))
 
 
 # smallest M the wide kernel serves (1: every decode batch; the 64-row tile at M <= 64 streams
@@ -277,7 +282,7 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     if s > 1 and s * m * n > ws.numel():
         s = max(1, ws.numel() // (m * n))
     stream = torch.cuda.current_stream().cuda_stream
-    v = WIDE_VARIANT if variant < 0 else variant
+    v = (WIDE_VARIANT_SPLIT if s > 1 else WIDE_VARIANT) if variant < 0 else variant
     bm = wide_row_tile(m, n, k, swiglu)
     if bm != wide_bm(m):
         v |= bm << 8

@@ -156,19 +156,32 @@ def _gather_kv(k_cache, v_cache, block_table, n):
 def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                            block_tables: torch.Tensor, seq_lens: torch.Tensor,
                            scale: float) -> torch.Tensor:
-    """q [B, Hq, D] (one new token per sequence, already in the cache) -> [B, Hq, D]."""
+    """q [B, Hq, D] (one new token per sequence, already in the cache) -> [B, Hq, D].
+
+    The whole batch in one gather: every sequence's first ceil(max_len / bs) blocks (table
+    padding is block 0, a valid index), keys past its own length masked to -inf.
+    """
     b, hq, d = q.shape
-    hkv = k_cache.shape[1]
-    out = torch.empty_like(q)
-    for i in range(b):
-        n = int(seq_lens[i])
-        k, v = _gather_kv(k_cache, v_cache, block_tables[i], n)
-        qi = q[i].float().view(hkv, hq // hkv, d)
-        s = torch.einsum("hgd,hnd->hgn", qi, k.float()) * scale
-        p = torch.softmax(s, dim=-1)
-        o = torch.einsum("hgn,hnd->hgd", p, v.float())
-        out[i] = o.reshape(hq, d).to(q.dtype)
-    return out
+    if b == 0:
+        return torch.empty_like(q)
+    hkv, bs = k_cache.shape[1], k_cache.shape[2]
+    lens = seq_lens[:b].long()
+    n = int(lens.max())
+    nb = (n + bs - 1) // bs
+    blocks = block_tables[:b, :nb].long().clamp_min(0)
+    kb, vb = k_cache[blocks], v_cache[blocks]               # [B, nb, Hkv, ...]
+    if bs == 32:
+        kb = kb[:, :, :, _KROW32.to(kb.device), :]         # physical rows back to key order
+        v = vb.reshape(b, nb, hkv, 4, d, 8).permute(0, 2, 1, 3, 5, 4).reshape(b, hkv, nb * bs, d)
+    else:
+        v = vb.permute(0, 2, 1, 4, 3).reshape(b, hkv, nb * bs, d)
+    k = kb.permute(0, 2, 1, 3, 4).reshape(b, hkv, nb * bs, d)
+    qf = q.float().view(b, hkv, hq // hkv, d)
+    s = torch.einsum("bhgd,bhnd->bhgn", qf, k.float()) * scale
+    pad = torch.arange(nb * bs, device=q.device).view(1, 1, 1, -1) >= lens.to(q.device).view(b, 1, 1, 1)
+    p = torch.softmax(s.masked_fill(pad, float("-inf")), dim=-1)
+    o = torch.einsum("bhgn,bhnd->bhgd", p, v.float())
+    return o.reshape(b, hq, d).to(q.dtype)
 
 
 def paged_attention_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,

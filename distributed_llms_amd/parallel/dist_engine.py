@@ -179,7 +179,8 @@ class RankRole:
         if ctx.tp > 1 and ctx.pp == 1:
             self._init_tp(ctx, ecfg, mcfg, hf_state)
             return
-        self.plan = plan_units(mcfg, ctx.pp, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2))
+        self.plan = plan_units(mcfg, ctx.pp, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2),
+                               device=str(ctx.device))
         a, b = self.plan.ranges[ctx.stage]
         stage = build_stage(ecfg, a, b, device=ctx.device, shard_state=hf_state,
                             units=self.plan.unit_range(ctx.stage), tp=ctx.tpg)
@@ -193,7 +194,7 @@ class RankRole:
         else:
             self.runner = StageRunner(stage, ecfg, num_blocks=nb)
             hop = (max(ecfg.max_prefill_tokens, ecfg.max_batch), mcfg.hidden_size, stage.dtype,
-                   inflight_window(ecfg, ctx.pp))
+                   inflight_window(ecfg, ctx.pp, stage.device))
             self.transport = make_transport(ctx.pipeline_ranks, ctx.stage, ctx.ctrl_group, ctx.data_group,
                                             ctx.device, ctx.ring_group, hop=hop)
             if ctx.stage == 0 and ctx.tp_rank == 0:

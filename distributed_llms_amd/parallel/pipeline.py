@@ -30,7 +30,7 @@ from typing import Deque, List, Optional
 import numpy as np
 import torch
 
-from ..config import EngineConfig
+from ..config import EngineConfig, pipeline_slots, resolve_device  # noqa: F401  (pipeline_slots re-exported)
 from ..engine.batch import HostBatch, build_host_batch
 from ..engine.runner import StageRunner
 from ..engine.sampler import sample
@@ -92,17 +92,11 @@ class _Issued:
         self.step, self.sid, self.ids = step, sid, ids
 
 
-def pipeline_slots(ecfg: EngineConfig, pp: int) -> int:
-    """Microbatch slots of a pp-stage pipeline: one per stage keeps every stage busy only if the
-    ring closure were free; one spare slot covers the hops."""
-    return ecfg.microbatches if ecfg.microbatches > 0 else pp + 1
-
-
-def inflight_window(ecfg: EngineConfig, pp: int) -> int:
+def inflight_window(ecfg: EngineConfig, pp: int, device=None) -> int:
     """Most microbatches the driver ever has in flight: two per slot (a step and its lookahead
     successor).  Microbatch n is issued only after n - window completed at stage 0, i.e. after
     every stage finished it -- transports with slot rings deeper than this never need credits."""
-    return 2 * pipeline_slots(ecfg, pp)
+    return 2 * pipeline_slots(ecfg, pp, device)
 
 
 class PipelineDriver:
@@ -115,7 +109,7 @@ class PipelineDriver:
         self.t = transport
         self.ecfg = ecfg
         self.bm = block_manager
-        self.num_slots = num_slots or pipeline_slots(ecfg, transport.num_stages)
+        self.num_slots = num_slots or pipeline_slots(ecfg, transport.num_stages, runner.stage.device)
         self.scheduler = Scheduler(block_manager, self.num_slots, ecfg.max_batch, ecfg.max_prefill_tokens,
                                    ecfg.max_seq_len)
         self.mcfg = runner.stage.cfg
@@ -289,7 +283,8 @@ def run_loopback_pipeline(ecfg: EngineConfig, num_stages: int, prompts, params: 
     from .planner import plan_units
 
     mcfg = ecfg.model_config()
-    plan = plan_units(mcfg, num_stages, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2))
+    plan = plan_units(mcfg, num_stages, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2),
+                      device=str(device or resolve_device(ecfg.device)))
     hub = LoopbackHub(num_stages)
     runners = []
     for s, (a, b) in enumerate(plan.ranges):

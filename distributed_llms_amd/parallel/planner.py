@@ -136,7 +136,7 @@ def unit_costs_us(cfg: ModelConfig, batch: int = 256, ctx: int = 192) -> Tuple[L
         mlp_p_read = cfg.num_experts * 3 * h * i           # every expert is read at decode batch sizes
         mlp_p_flop = cfg.experts_per_token * 3 * h * i
     else:
-        mlp_p_read = mlp_p_flop = 3 * h * i
+        mlp_p_read = mlp_p_flop = (2 if cfg.arch == "gpt2" else 3) * h * i
     kv_b = batch * ctx * 2 * cfg.kv_size * 2
     attn = max(2 * attn_p / HBM_B_PER_US, 2 * batch * attn_p / ATTN_GEMM_FLOP_PER_US) + kv_b / KV_B_PER_US \
         + ATTN_FIXED_US
@@ -146,9 +146,30 @@ def unit_costs_us(cfg: ModelConfig, batch: int = 256, ctx: int = 192) -> Tuple[L
     return [attn, mlp] * cfg.num_layers, head
 
 
-def plan_units(cfg: ModelConfig, num_stages: int, batch: int = 256, ctx: int = 192) -> StagePlan:
-    """Half-layer plan for runtime pipelines (see module doc)."""
-    costs, head = unit_costs_us(cfg, batch, ctx)
+def unit_costs_cpu(cfg: ModelConfig, ctx: int = 192) -> Tuple[List[float], float]:
+    """Per half-layer costs of a CPU stage, in multiply-adds per decoded token.
+
+    A CPU stage has no fixed per-kernel floor worth modelling: its GEMMs stream their weights
+    (small batches) or are FLOP bound (large ones), and both scale with the parameter count, so
+    the LM head weighs what its parameters weigh -- GPT-2 small's (50257 x 768) is worth ~5.5
+    layers, which the GPU model above prices at ~1.  Attention adds its q.k and p.v work over
+    ``ctx`` cached tokens."""
+    h, i = cfg.hidden_size, cfg.intermediate_size
+    attn = h * cfg.qkv_size + cfg.q_size * h + 2 * ctx * cfg.q_size
+    mlp = (cfg.num_experts if cfg.is_moe else 1) * 3 * h * i
+    if cfg.arch == "gpt2":
+        mlp = 2 * h * i                                      # fc + proj, no gate
+    return [float(attn), float(mlp)] * cfg.num_layers, float(cfg.vocab_size * h)
+
+
+def plan_units(cfg: ModelConfig, num_stages: int, batch: int = 256, ctx: int = 192,
+               device: str = "cuda") -> StagePlan:
+    """Half-layer plan for runtime pipelines (see module doc); ``device`` picks the cost model
+    (GPU decode time model, or :func:`unit_costs_cpu` for CPU stages)."""
+    if str(device).startswith("cpu"):
+        costs, head = unit_costs_cpu(cfg, ctx)
+    else:
+        costs, head = unit_costs_us(cfg, batch, ctx)
     units = _partition(costs, num_stages, head)
     pre = [0.0]
     for c in costs:

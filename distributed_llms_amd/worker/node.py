@@ -446,7 +446,7 @@ class WorkerNode:
             transport = make_transport(list(range(world)), stage_idx, ctx.ctrl_group, ctx.data_group, self.device,
                                        ctx.ring_group,
                                        hop=(max(ecfg.max_prefill_tokens, ecfg.max_batch), stage.cfg.hidden_size,
-                                            stage.dtype, inflight_window(ecfg, world)))
+                                            stage.dtype, inflight_window(ecfg, world, stage.device)))
             if stage_idx == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.stage_runner, transport, ecfg, bm)

@@ -1,7 +1,7 @@
 # Full GPU check: pytest -m gpu, smoke(), default bench, short profile. Each GPU step has its own limit.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests/ -x -q -m gpu > gpurun_out/tests_gpu.log 2>&1 || { echo "GPU tests failed"; tail -60 gpurun_out/tests_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/ -x -v -m gpu --timeout 240 --timeout-method thread > gpurun_out/tests_gpu.log 2>&1 || { echo "GPU tests failed"; tail -60 gpurun_out/tests_gpu.log; exit 1; }
 tail -2 gpurun_out/tests_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log

@@ -42,9 +42,9 @@ def test_torchrun_bench_cpu(n, par, trace, tmp_path):
     rec = lines[0]
     assert KEYS <= set(rec)
     assert rec["n_gpus"] == n and rec["value"] > 0 and rec["config"]["parallelism"] == f"{par}{n}"
-    if par == "pp":
-        assert rec["microbatch_slots"] == n + 1
-        assert rec["config"]["global_batch"] == 3 * (n + 1)
+    if par == "pp":                 # CPU stages run one slot per stage (config.pipeline_slots)
+        assert rec["microbatch_slots"] == n
+        assert rec["config"]["global_batch"] == 3 * n
     if par == "tp":                 # one TP group: one engine's batch
         assert rec["config"]["global_batch"] == 3
     if trace:   # every rank wrote a timeline; every stage reports its busy fraction
@@ -76,4 +76,4 @@ def test_torchrun_bench_hybrid_dp_pp_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_lines(r.stdout)[0]
     assert rec["config"]["parallelism"] == "dp2xpp2" and rec["n_gpus"] == 4
-    assert rec["microbatch_slots"] == 3 and rec["config"]["global_batch"] == 2 * 3 * 3
+    assert rec["microbatch_slots"] == 2 and rec["config"]["global_batch"] == 2 * 3 * 2   # CPU: pp slots

@@ -47,8 +47,9 @@ def test_shallower_ring_would_be_overwritten(window):
 @pytest.mark.parametrize("pp", [2, 4, 8])
 def test_window_matches_driver_slots(pp):
     ecfg = EngineConfig(model="tiny-llama", num_workers=pp)
-    assert pl.pipeline_slots(ecfg, pp) == pp + 1
-    assert pl.inflight_window(ecfg, pp) == 2 * (pp + 1)
+    assert pl.pipeline_slots(ecfg, pp, "cuda:0") == pp + 1
+    assert pl.inflight_window(ecfg, pp, "cuda:0") == 2 * (pp + 1)
+    assert pl.inflight_window(ecfg, pp, "cpu") == 2 * pp
 
 
 @pytest.mark.parametrize("stages", [2, 3])

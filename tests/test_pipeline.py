@@ -143,16 +143,33 @@ def test_unit_planner_balances_better_than_layers():
         assert all(a[1] == b[0] for a, b in zip(u.units, u.units[1:]))
 
 
+def test_cpu_planner_prices_the_lm_head_by_its_weights():
+    """CPU stages stream their weights: GPT-2 small's LM head (50257 x 768, ~5.5 layers of
+    parameters) pushes the 2-stage cut to layer 9, where the GPU time model cuts at ~6."""
+    from distributed_llms_amd.parallel.planner import plan_units, unit_costs_cpu
+    cfg = get_model_config("gpt2-small")
+    c, head = unit_costs_cpu(cfg, ctx=64)
+    assert 5 < head / (c[0] + c[1]) < 6
+    cpu = plan_units(cfg, 2, 16, 64, device="cpu")
+    assert cpu.ranges == ((0, 9), (9, 12)) and cpu.imbalance() < 1.05
+    assert plan_units(cfg, 2, 16, 64, device="cuda:0").ranges[0][1] < 9
+
+
 def test_kv_plan_covers_all_pipeline_slots():
-    """A pp-stage pipeline keeps pp + 1 microbatch slots in flight; the KV pool must hold all of them."""
+    """The KV pool holds every microbatch slot the driver keeps in flight: pp + 1 on GPUs, pp on
+    CPUs (config.pipeline_slots)."""
+    from distributed_llms_amd.config import pipeline_slots
     from distributed_llms_amd.engine.runner import plan_kv_blocks
     cfg = get_model_config("tiny-llama")
     per_seq = -(-288 // 32)
-    for pp, slots in ((1, 1), (2, 3), (8, 9)):
+    for pp, slots in ((1, 1), (2, 2), (8, 8)):
         e = EngineConfig(model="tiny-llama", device="cpu", max_batch=16, max_seq_len=288, num_workers=pp)
         assert plan_kv_blocks(cfg, 1, e, "cpu") == 16 * slots * per_seq + 2
+    for pp, slots in ((1, 1), (2, 3), (8, 9)):
+        assert pipeline_slots(EngineConfig(num_workers=pp), pp, "cuda:0") == slots
     e = EngineConfig(model="tiny-llama", device="cpu", max_batch=16, max_seq_len=288, num_workers=8, microbatches=4)
     assert plan_kv_blocks(cfg, 1, e, "cpu") == 16 * 4 * per_seq + 2
+    assert pipeline_slots(e, 8, "cuda:0") == 4
 
 
 @pytest.mark.parametrize("stages", [2, 3])
