@@ -56,6 +56,8 @@ def parse(argv=None):
                     help="pipeline depth for --parallelism pp (default: all ranks); world/pp pipelines run as "
                          "data-parallel replicas, e.g. --gpus 8 --pp 4 = 2 pipelines of 4 stages")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--quant", choices=["none", "fp8"], default="none",
+                    help="fp8: W8A8 e4m3 dense projections (opt-in serving mode; the headline stays bf16)")
     ap.add_argument("--streams", type=int, default=1, help="1-GPU engine: microbatch slots on separate streams")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
@@ -95,7 +97,8 @@ def emit(args, world, elapsed, lat, extra, global_batch=None):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
         "higher_is_better": True, "scaling": "weak",
         "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
-        "dtype": "bf16", "data": "synthetic (random-init weights, random prompt ids)",
+        "dtype": "bf16" if args.quant == "none" else "fp8 (W8A8 projections, bf16 rest)",
+        "data": "synthetic (random-init weights, random prompt ids)",
         "p50_latency_ms": round(1000 * statistics.median(lat), 3) if lat else None,
         "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.prompt_len + args.gen_len,
                    "prompt_len": args.prompt_len, "gen_len": args.gen_len,
@@ -136,7 +139,7 @@ def run_single(args):
     ecfg = EngineConfig(model=f"synthetic:{args.model}", max_batch=args.batch,
                         max_prefill_tokens=max(16384, args.batch * args.prompt_len),
                         max_seq_len=args.prompt_len + args.gen_len + 32, use_graphs=not args.no_graphs,
-                        seed=args.seed, streams=args.streams)
+                        seed=args.seed, streams=args.streams, quant=args.quant)
     sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
     t0 = time.perf_counter()
     eng = LLMEngine(ecfg)

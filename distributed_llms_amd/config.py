@@ -236,6 +236,7 @@ class EngineConfig:
     kv_cache_fraction: float = 0.80    # of free HBM after weights
     num_kv_blocks: int = 0             # 0 -> derive from kv_cache_fraction
     use_graphs: bool = True            # HIP-graph capture of the decode step
+    quant: str = "none"                # "fp8": W8A8 e4m3 dense projections (ops/quant.py)
     graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
     host: str = "0.0.0.0"
     port: int = 65432
@@ -254,6 +255,8 @@ class EngineConfig:
             raise ValueError("num_workers and dp_replicas must be >= 1")
         if self.kv_block_size not in (16, 32, 64):
             raise ValueError("kv_block_size must be 16, 32 or 64")
+        if self.quant not in ("none", "fp8"):
+            raise ValueError(f"quant {self.quant!r} (none, fp8)")
         if self.max_batch < 1 or self.max_seq_len < 2:
             raise ValueError("max_batch/max_seq_len")
         cfg = get_model_config(self.model if self.shard_dir is None else self.shard_dir)

@@ -59,6 +59,67 @@ __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x))
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 
+// Block-wide max for blockDim.x <= 1024; `red` must hold >= 16 floats.
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_max(v);
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = red[0];
+  for (int i = 1; i < nw; ++i) t = fmaxf(t, red[i]);
+  __syncthreads();
+  return t;
+}
+
+// ---- per-token FP8 (OCP e4m3) quantization shared by quant.hip and the fused norm epilogues:
+// scale = amax / 448 (1 for an all-zero row), q = RNE(clamp(v / scale)), packed 4 per dword.
+constexpr float kFp8Max = 448.f;
+__device__ __forceinline__ float fp8_row_scale(float amax) { return amax > 0.f ? amax / kFp8Max : 1.f; }
+__device__ __forceinline__ float fp8_in(float v, float s) { return fminf(fmaxf(v / s, -kFp8Max), kFp8Max); }
+__device__ __forceinline__ int pack4_fp8(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+// 8 values (already bf16-rounded, in f32) -> 8 e4m3 bytes at q
+__device__ __forceinline__ void store8_fp8(uint8_t* q, const float (&v)[8], float s) {
+  int2 o;
+  o.x = pack4_fp8(fp8_in(v[0], s), fp8_in(v[1], s), fp8_in(v[2], s), fp8_in(v[3], s));
+  o.y = pack4_fp8(fp8_in(v[4], s), fp8_in(v[5], s), fp8_in(v[6], s), fp8_in(v[7], s));
+  *reinterpret_cast<int2*>(q) = o;
+}
+
+// Norm epilogue with an FP8 consumer: y = bf16(v * inv * g) per element (written when y != null),
+// then the row's e4m3 quantization of those bf16 values (q8 row, scale at *qs).  v [MAXV][8]: the
+// thread's row values, vector idx = threadIdx.x + i * NTH.
+template <int MAXV, int NTH>
+__device__ __forceinline__ void norm_out_fp8(float (&v)[MAXV][8], float inv, const bf16x8* __restrict__ wv, int nvec,
+                                             bf16* __restrict__ y, uint8_t* __restrict__ q8, float* __restrict__ qs,
+                                             float* red) {
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int idx = threadIdx.x + i * NTH;
+    if (idx < nvec) {
+      const bf16x8 g = wv[idx];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = f2bf(v[i][j] * inv * bf2f(g[j]));
+        v[i][j] = bf2f(o[j]);
+        amax = fmaxf(amax, fabsf(v[i][j]));
+      }
+      if (y) reinterpret_cast<bf16x8*>(y)[idx] = o;
+    }
+  }
+  const float s = fp8_row_scale(block_max(amax, red));
+  if (threadIdx.x == 0) *qs = s;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int idx = threadIdx.x + i * NTH;
+    if (idx < nvec) store8_fp8(q8 + idx * 8, v[i], s);
+  }
+}
+
 // Paged KV layout of a 32-key block (one kv head), chosen so that the QK^T MFMA output hands
 // every lane group g the probabilities of keys 8g..8g+7 in natural order:
 //   K  [32 rows][D]        key j stored at row krow32(j): 8g+i -> row 4g+i, 8g+4+i -> row 16+4g+i

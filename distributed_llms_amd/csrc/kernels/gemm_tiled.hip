@@ -182,7 +182,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16* __restrict__ o
 template <int MAXV, int SC, int NTH = 256>
 __global__ void __launch_bounds__(NTH) splitk_add_rms_norm_kernel(bf16* __restrict__ y, bf16* __restrict__ residual,
                                                                   const float* __restrict__ P, int S_, int M, int N,
-                                                                  const bf16* __restrict__ w, float eps) {
+                                                                  const bf16* __restrict__ w, float eps,
+                                                                  uint8_t* __restrict__ q8, float* __restrict__ qs) {
   // SC > 0: the slab count is a compile-time constant, so all of a vector's 2*SC slab loads are
   // issued before the first add (the runtime-S loop waited on each slab in turn)
   const int S = SC > 0 ? SC : S_;
@@ -235,6 +236,11 @@ __global__ void __launch_bounds__(NTH) splitk_add_rms_norm_kernel(bf16* __restri
   ss = block_sum(ss, red);
   const float inv = rsqrtf(ss / (float)N + eps);
   const bf16x8* wv = reinterpret_cast<const bf16x8*>(w);
+  if (q8) {   // FP8 consumer: per-token e4m3 of the normalised row (rms_norm_kernel's epilogue)
+    norm_out_fp8<MAXV, NTH>(v, inv, wv, nvec, y ? y + (size_t)row * N : nullptr, q8 + (size_t)row * N, qs + row,
+                            red);
+    return;
+  }
   bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)row * N);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
@@ -251,7 +257,14 @@ __global__ void __launch_bounds__(NTH) splitk_add_rms_norm_kernel(bf16* __restri
 
 void splitk_add_rms_norm(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, int M, int N, uintptr_t w, float eps,
                          uintptr_t stream) {
+  splitk_add_rms_norm_q8(y, residual, ws, S, M, N, w, eps, 0, 0, stream);
+}
+
+void splitk_add_rms_norm_q8(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, int M, int N, uintptr_t w,
+                            float eps, uintptr_t q8, uintptr_t qs, uintptr_t stream) {
   DLLM_HOST_CHECK(N % 8 == 0 && N <= 8 * 256 * 8, "hidden must be a multiple of 8 and <= 16384");
+  DLLM_HOST_CHECK(y != 0 || q8 != 0, "splitk_add_rms_norm needs an output");
+  DLLM_HOST_CHECK((q8 == 0) == (qs == 0), "q8 and its scales go together");
   DLLM_HOST_CHECK(S >= 1 && M >= 0, "S >= 1");
   if (M == 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -269,7 +282,7 @@ void splitk_add_rms_norm(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, i
   const int bth = (nth == 512 && nvec > 256 && nvec <= 512 && S == 8) ? 512 : 256;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(M), dim3(bth), 0, s, (bf16*)y, (bf16*)residual, (const float*)ws, S, M, N,
-                       (const bf16*)w, eps);
+                       (const bf16*)w, eps, (uint8_t*)q8, (float*)qs);
   };
   if (bth == 512) {
     go(splitk_add_rms_norm_kernel<1, 8, 512>);

@@ -42,6 +42,8 @@
 
 namespace dllm {
 
+typedef int i32x4w __attribute__((ext_vector_type(4)));
+typedef int i32x8w __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_vptr_w;
 typedef __attribute__((address_space(1))) void* glb_vptr_w;
 
@@ -112,32 +114,54 @@ __device__ __forceinline__ int wide_b_row(int r, int n_t, int half) {
 
 // epilogue shared by both wide kernels: acc[rt][ct] lane holds tile column (lane & 15), rows
 // 4 * (lane >> 4) + i of each 16 x 16 fragment
-template <int BM, bool SPLIT, bool SWIGLU>
+// SCALED (fp8 operands): the accumulator is in quantized units; output = acc * sa[m] * sb[n]
+// (per-token activation scale x per-output-channel weight scale), applied before the SwiGLU and
+// before a split-K slab store (the cross-slice sum is linear in it).
+template <int BM, bool SPLIT, bool SWIGLU, bool SCALED = false>
 __device__ __forceinline__ void wide_epilogue(const f32x4 (&acc)[BM / 64][4], bf16* __restrict__ C,
                                               float* __restrict__ P, int M, int N, int m0, int n_t, int split, int wm,
-                                              int wn, int lane) {
+                                              int wn, int lane, const float* __restrict__ sa = nullptr,
+                                              const float* __restrict__ sb = nullptr) {
   constexpr int RT = BM / 64;
   const int fr = lane & 15, fq = lane >> 4;
+  float sbn[4];
+  if constexpr (SCALED) {
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      int n;
+      if (SWIGLU && !SPLIT) n = n_t * 64 + (wn * 2 + (ct >> 1)) * 16 + fr + ((ct & 1) ? N / 2 : 0);
+      else n = wide_b_row<SWIGLU>(wn * 64 + ct * 16 + fr, n_t, N / 2);
+      sbn[ct] = sb[n];
+    }
+  }
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wm * (BM / 4) + rt * 16 + 4 * fq + i;
       if (m >= M) continue;
+      float v[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) v[ct] = acc[rt][ct][i];
+      if constexpr (SCALED) {
+        const float s = sa[m];
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) v[ct] *= s * sbn[ct];
+      }
       if (SWIGLU && !SPLIT) {
         const int half = N / 2;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           const int c = n_t * 64 + (wn * 2 + p) * 16 + fr;
-          const float g = acc[rt][2 * p][i], u = acc[rt][2 * p + 1][i];
+          const float g = v[2 * p], u = v[2 * p + 1];
           C[(size_t)m * half + c] = f2bf(silu_f(g) * u);
         }
       } else {
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
           const int n = wide_b_row<SWIGLU>(wn * 64 + ct * 16 + fr, n_t, N / 2);
-          if (SPLIT) part_store(P, ((size_t)split * M + m) * N + n, acc[rt][ct][i]);
-          else C[(size_t)m * N + n] = f2bf(acc[rt][ct][i]);
+          if (SPLIT) part_store(P, ((size_t)split * M + m) * N + n, v[ct]);
+          else C[(size_t)m * N + n] = f2bf(v[ct]);
         }
       }
     }
@@ -147,7 +171,7 @@ __device__ __forceinline__ void wide_epilogue(const f32x4 (&acc)[BM / 64][4], bf
 // The K loop shared by the dense and the grouped (MoE) wide kernels: stages A/B tiles through
 // NBUF LDS buffers (LDS-DMA, counted vmcnt, raw barrier) and accumulates acc = A_tile B_tile^T
 // over `nt` 64-deep K-tiles.  srcA/srcB: this lane's staging source for K-tile 0.
-template <int BM, int NBUF, int VAR>
+template <int BM, int NBUF, int VAR, bool FP8 = false>
 __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&srcA)[BM / 64],
                                               const bf16* const (&srcB)[2], int nt, f32x4 (&acc)[BM / 64][4],
                                               int wv, int lane) {
@@ -288,7 +312,53 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
     if constexpr (RT > 2) { lgkm_wait1<RT - 3>(fa[1][2]); __builtin_amdgcn_sched_barrier(0); row(1, 2); }
     if constexpr (RT > 3) { lgkm_wait1<RT - 4>(fa[1][3]); __builtin_amdgcn_sched_barrier(0); row(1, 3); }
   };
-  constexpr bool SPLITRD = (VAR & 32) != 0 && RT <= 4;
+  // FP8: the same 128-byte LDS rows hold 128 e4m3 values of K; lane group fq's fragment is chunks
+  // 2fq and 2fq + 1 (k = 32 fq .. 32 fq + 31, the same k map for A and B), one block-scaled
+  // v_mfma_scale_f32_16x16x128_f8f6f4 per (row, column) fragment pair and K-tile (unit E8M0 scales:
+  // the real per-token / per-channel scales are applied in the epilogue).  Same cycles per K-tile
+  // as the bf16 loop at twice the K: half the K-tiles, half the staging instructions per FLOP.
+  auto ktile8 = [&](int cur, bf16* dst, int ko, auto stg) {
+    constexpr bool STG = decltype(stg)::value;
+    const bf16* sa = smem + cur * BUF;
+    const bf16* sb = sa + AEL;
+    i32x8w fa[RT], fb[4];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int row = wm * (BM / 4) + rt * 16 + fr;
+      const i32x4w lo = *reinterpret_cast<const i32x4w*>(sa + row * WBK + wswz(row, 2 * fq) * 8);
+      const i32x4w hi = *reinterpret_cast<const i32x4w*>(sa + row * WBK + wswz(row, 2 * fq + 1) * 8);
+      fa[rt] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int row = wn * 64 + ct * 16 + fr;
+      const i32x4w lo = *reinterpret_cast<const i32x4w*>(sb + row * WBK + wswz(row, 2 * fq) * 8);
+      const i32x4w hi = *reinterpret_cast<const i32x4w*>(sb + row * WBK + wswz(row, 2 * fq + 1) * 8);
+      fb[ct] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    constexpr int NMF = RT * 4;
+    constexpr int EVERY = NMF / (G + 1) > 0 ? NMF / (G + 1) : 1;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        acc[rt][ct] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[rt], fb[ct], acc[rt][ct], 0, 0, 0, 127, 0, 127);
+        if constexpr (STG) {
+          const int i = rt * 4 + ct + 1;
+          if (i % EVERY == 0 && i / EVERY <= G) piece(dst, ko, i / EVERY - 1);
+        }
+      }
+    if constexpr (STG) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (RT + 4), 0);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, EVERY, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF - G * EVERY, 0);
+    }
+  };
+  constexpr bool SPLITRD = (VAR & 32) != 0 && RT <= 4 && !FP8;
 
   if (nt > 0) {
 #pragma unroll
@@ -304,7 +374,9 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       // buffer (t-1) % NBUF was last read in iteration t-1, which every wave finished before
       // this barrier: refill it with tile t + NBUF - 1
       const int nb = cur == 0 ? NBUF - 1 : cur - 1;
-      if constexpr (SPLITRD) {
+      if constexpr (FP8) {
+        ktile8(cur, smem + nb * BUF, (t + NBUF - 1) * WBK, std::true_type{});
+      } else if constexpr (SPLITRD) {
         ktile_sr(cur, smem + nb * BUF, (t + NBUF - 1) * WBK, std::true_type{});
       } else if constexpr ((VAR & 7) == 0) {
         stage(nb, t + NBUF - 1);
@@ -319,7 +391,8 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       wait_tiles<G>(nt - 1 - t);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if constexpr (SPLITRD) ktile_sr(cur, smem, 0, std::false_type{});
+      if constexpr (FP8) ktile8(cur, smem, 0, std::false_type{});
+      else if constexpr (SPLITRD) ktile_sr(cur, smem, 0, std::false_type{});
       else ktile(cur, smem, 0, std::false_type{});
       cur = cur == NBUF - 1 ? 0 : cur + 1;
     }
@@ -378,6 +451,54 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
   wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, nt, acc, wv, lane);
   if ((VAR & 8) && nsplit >= 0) return;
   wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
+}
+
+// FP8 (W8A8) variant: A [M, K] and B [N, K] OCP e4m3 bytes, per-row scales sa [M] (dynamic,
+// per token: ops/quant) and sb [N] (per output channel, at load time).  Staging is the bf16 kernel's
+// byte for byte: a 128 x 128-byte K-tile is 128 K of fp8, addressed as 64 bf16-sized units.
+template <int BM, bool SPLIT, bool SWIGLU, int NBUF, int VAR>
+__global__ void __launch_bounds__(512, 1) gemm_wide_fp8_kernel(const uint8_t* __restrict__ A8,
+                                                               const uint8_t* __restrict__ B8, const float* __restrict__ sa,
+                                                               const float* __restrict__ sb, bf16* __restrict__ C,
+                                                               float* __restrict__ P, int M, int N, int K,
+                                                               int kt_per_split, int nsplit) {
+  constexpr int AEL = BM * WBK, BEL = WBN * WBK, BUF = AEL + BEL;   // 2-byte units
+  constexpr int AI = BM / 64, BI = 2, RT = BM / 64;
+  static_assert(NBUF >= 3 && NBUF * BUF * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BUF];
+  const bf16* A = reinterpret_cast<const bf16*>(A8);
+  const bf16* B = reinterpret_cast<const bf16*>(B8);
+  const int KU = K / 2;                       // row length in 2-byte units
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int mtiles = (M + BM - 1) / BM;
+  const int total = gridDim.x;
+  int b = blockIdx.x;
+  {
+    const int q = total >> 3, r = total & 7, x = b & 7;
+    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  }
+  const int m_t = b % mtiles, rest = b / mtiles;
+  const int split = rest % nsplit, n_t = rest / nsplit;
+  const int m0 = m_t * BM;
+  const int kt0 = split * kt_per_split;
+  const int nt = max(0, min(KU / WBK, kt0 + kt_per_split) - kt0);
+  const bf16* srcA[AI];
+  const bf16* srcB[BI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int r = 8 * (wv * AI + j) + (lane >> 3);
+    srcA[j] = A + (size_t)min(m0 + r, M - 1) * KU + (size_t)kt0 * WBK + wswz(r, lane & 7) * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int r = 8 * (wv * BI + j) + (lane >> 3);
+    srcB[j] = B + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * KU + (size_t)kt0 * WBK + wswz(r, lane & 7) * 8;
+  }
+  f32x4 acc[RT][4];
+  wide_mainloop<BM, NBUF, VAR, true>(smem, srcA, srcB, nt, acc, wv, lane);
+  wide_epilogue<BM, SPLIT, SWIGLU, true>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane, sa, sb);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -537,6 +658,61 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   else { if (swiglu) DLLM_WIDE_GO(256, true, true); else DLLM_WIDE_GO(256, true, false); }
 #undef DLLM_WIDE_GO
 #undef DLLM_WIDE_GO3
+  DLLM_HIP_CHECK(hipGetLastError());
+  if (mode == 2) return S;
+  splitk_reduce_ex(c, ws, 0, S, M, N, swiglu ? 1 : 0, stream);
+  return S;
+}
+
+// FP8 W8A8 wide GEMM: modes as gemm_wide; K in elements (= bytes), multiple of 128.
+int gemm_wide_fp8(uintptr_t c, uintptr_t a, uintptr_t a_scale, uintptr_t b, uintptr_t b_scale, uintptr_t ws,
+                  long ws_floats, int M, int N, int K, int splits, int mode, int variant, uintptr_t stream) {
+  DLLM_HOST_CHECK(M >= 1, "M >= 1");
+  DLLM_HOST_CHECK(K % 128 == 0, "fp8 K must be a multiple of 128");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");
+  DLLM_HOST_CHECK(a_scale != 0 && b_scale != 0, "fp8 GEMM needs both scale vectors");
+  const bool swiglu = mode == 1;
+  DLLM_HOST_CHECK(N % 128 == 0, "N must be a multiple of 128");
+  DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
+  const int bm_force = variant >> 8;
+  variant &= 0xff;
+  DLLM_HOST_CHECK(bm_force == 0 || bm_force == 64 || bm_force == 128 || bm_force == 192 || bm_force == 256,
+                  "row tile override must be 64, 128, 192 or 256");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int ktiles = K / 128;
+  const int kts = (ktiles + splits - 1) / splits;
+  const int S = (ktiles + kts - 1) / kts;
+  DLLM_HOST_CHECK(mode != 2 || S > 1, "mode 2 needs a K split");
+  const int BM = bm_force ? bm_force : wide_bm(M);
+  const int mtiles = (M + BM - 1) / BM;
+  const int ntiles = swiglu ? (N / 2) / 64 : N / WBN;
+  const long grid = (long)ntiles * mtiles * S;
+  DLLM_HOST_CHECK(grid >= 1 && grid < (1L << 31), "grid");
+  if (S > 1) DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
+  // weights nt where the grid has no K split (as the bf16 kernel's variant 1)
+  const bool nt = (variant & 7) != 4 && S == 1;
+#define DLLM_F8_GO3(BM_, SPLIT_, SW_, V_)                                                                   \
+  hipLaunchKernelGGL((gemm_wide_fp8_kernel<BM_, SPLIT_, SW_, 3, V_>), dim3((unsigned)grid), dim3(512), 0, s,  \
+                     (const uint8_t*)a, (const uint8_t*)b, (const float*)a_scale, (const float*)b_scale,      \
+                     (bf16*)c, (float*)ws, M, N, K, kts, S)
+#define DLLM_F8_GO(BM_, SPLIT_, SW_)                                   \
+  do {                                                                \
+    if (nt) DLLM_F8_GO3(BM_, SPLIT_, SW_, 2); else DLLM_F8_GO3(BM_, SPLIT_, SW_, 1); \
+  } while (0)
+  if (S == 1) {
+    if (BM == 64) { if (swiglu) DLLM_F8_GO(64, false, true); else DLLM_F8_GO(64, false, false); }
+    else if (BM == 128) { if (swiglu) DLLM_F8_GO(128, false, true); else DLLM_F8_GO(128, false, false); }
+    else if (BM == 192) { if (swiglu) DLLM_F8_GO(192, false, true); else DLLM_F8_GO(192, false, false); }
+    else { if (swiglu) DLLM_F8_GO(256, false, true); else DLLM_F8_GO(256, false, false); }
+    DLLM_HIP_CHECK(hipGetLastError());
+    return 1;
+  }
+  if (BM == 64) { if (swiglu) DLLM_F8_GO(64, true, true); else DLLM_F8_GO(64, true, false); }
+  else if (BM == 128) { if (swiglu) DLLM_F8_GO(128, true, true); else DLLM_F8_GO(128, true, false); }
+  else if (BM == 192) { if (swiglu) DLLM_F8_GO(192, true, true); else DLLM_F8_GO(192, true, false); }
+  else { if (swiglu) DLLM_F8_GO(256, true, true); else DLLM_F8_GO(256, true, false); }
+#undef DLLM_F8_GO
+#undef DLLM_F8_GO3
   DLLM_HIP_CHECK(hipGetLastError());
   if (mode == 2) return S;
   splitk_reduce_ex(c, ws, 0, S, M, N, swiglu ? 1 : 0, stream);

@@ -9,6 +9,10 @@ namespace dllm {
 
 void rms_norm(uintptr_t y, uintptr_t x, uintptr_t residual, uintptr_t w, int rows, int hidden, float eps,
               uintptr_t stream);
+void rms_norm_q8(uintptr_t y, uintptr_t x, uintptr_t residual, uintptr_t w, int rows, int hidden, float eps,
+                 uintptr_t q8, uintptr_t qs, uintptr_t stream);
+void splitk_add_rms_norm_q8(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, int M, int N, uintptr_t w,
+                            float eps, uintptr_t q8, uintptr_t qs, uintptr_t stream);
 void embedding(uintptr_t out, uintptr_t ids, uintptr_t table, int tokens, int hidden, int vocab,
                uintptr_t stream);
 void rope_cache_append(uintptr_t q_out, uintptr_t qkv, uintptr_t positions, uintptr_t cos_sin,
@@ -30,6 +34,9 @@ void splitk_reduce_ex(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M,
                       uintptr_t stream);
 int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
               int mode, int variant, uintptr_t stream);
+int gemm_wide_fp8(uintptr_t c, uintptr_t a, uintptr_t a_scale, uintptr_t b, uintptr_t b_scale, uintptr_t ws,
+                  long ws_floats, int M, int N, int K, int splits, int mode, int variant, uintptr_t stream);
+void quant_fp8_rows(uintptr_t q, uintptr_t scale, uintptr_t x, int M, int K, uintptr_t stream);
 int gemm_sq(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream);
 

@@ -19,7 +19,7 @@ template <int MAXV>
 __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ y, const bf16* __restrict__ x,
                                                        bf16* __restrict__ residual,
                                                        const bf16* __restrict__ w, int hidden,
-                                                       float eps) {
+                                                       float eps, uint8_t* __restrict__ q8, float* __restrict__ qs) {
   __shared__ float red[16];
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
@@ -50,6 +50,11 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ y, con
   ss = block_sum(ss, red);
   const float inv = rsqrtf(ss / (float)hidden + eps);
   const bf16x8* wv = reinterpret_cast<const bf16x8*>(w);
+  if (q8) {   // FP8 consumer (W8A8 GEMM): per-token e4m3 of the bf16-rounded output, y optional
+    norm_out_fp8<MAXV, 256>(v, inv, wv, nvec, y ? y + (size_t)row * hidden : nullptr, q8 + (size_t)row * hidden,
+                            qs + row, red);
+    return;
+  }
   bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)row * hidden);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
@@ -66,14 +71,22 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ y, con
 
 void rms_norm(uintptr_t y, uintptr_t x, uintptr_t residual, uintptr_t w, int rows, int hidden,
               float eps, uintptr_t stream) {
+  rms_norm_q8(y, x, residual, w, rows, hidden, eps, 0, 0, stream);
+}
+
+// q8 != 0: also (y == 0: only) the per-token e4m3 quantization of the output, scales in qs
+void rms_norm_q8(uintptr_t y, uintptr_t x, uintptr_t residual, uintptr_t w, int rows, int hidden, float eps,
+                 uintptr_t q8, uintptr_t qs, uintptr_t stream) {
   DLLM_HOST_CHECK(hidden % 8 == 0 && hidden <= 8 * 256 * 8, "hidden must be a multiple of 8 and <= 16384");
   DLLM_HOST_CHECK(rows >= 0, "rows >= 0");
+  DLLM_HOST_CHECK(y != 0 || q8 != 0, "rms_norm needs an output");
+  DLLM_HOST_CHECK((q8 == 0) == (qs == 0), "q8 and its scales go together");
   if (rows == 0) return;
   const int nvec = hidden / 8;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(rows), dim3(256), 0, s, (bf16*)y, (const bf16*)x, (bf16*)residual,
-                       (const bf16*)w, hidden, eps);
+                       (const bf16*)w, hidden, eps, (uint8_t*)q8, (float*)qs);
   };
   if (nvec <= 256) args(rms_norm_kernel<1>);
   else if (nvec <= 512) args(rms_norm_kernel<2>);

@@ -48,7 +48,7 @@ def build_stage(ecfg: EngineConfig, layer_start: int = 0, layer_end: Optional[in
         stage.load_hf_state(shard_state)
     else:
         stage.init_synthetic(ecfg.seed)
-    return stage
+    return stage.quantize(ecfg.quant)
 
 
 class LLMEngine:

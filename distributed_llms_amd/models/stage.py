@@ -182,8 +182,23 @@ class ModelStage:
         self._shard()
         return self
 
+    def quantize(self, mode: str) -> "ModelStage":
+        """``"fp8"``: the dense projections (qkv, o, gate|up, down) become W8A8 e4m3 weights
+        (ops/quant.py); embeddings, norms, LM head, MoE experts and the KV cache stay in ``dtype``."""
+        if mode in ("", "none", None):
+            return self
+        if mode != "fp8":
+            raise ValueError(f"unknown quantization {mode!r} (none, fp8)")
+        from ..ops import quant
+        quant.quantize_layers(self.layers)
+        return self
+
+    @staticmethod
+    def _nbytes(t) -> int:
+        return t.nbytes() if hasattr(t, "scale") else t.numel() * t.element_size()
+
     def weight_bytes(self) -> int:
-        n = sum(t.numel() * t.element_size() for d in self.layers for t in d.values())
+        n = sum(self._nbytes(t) for d in self.layers for t in d.values())
         n += sum(t.numel() * t.element_size() for t in self.embed.values())
         n += sum(t.numel() * t.element_size() for t in self.head.values())
         return n
@@ -256,10 +271,12 @@ class ModelStage:
         h = None   # output of the previous half, not yet added to the residual stream
         for is_attn, l, lw in self._units():
             norm_w = lw["attn_norm"] if is_attn else lw["mlp_norm"]
+            # W8A8 projection next (quant="fp8"): the norm kernel emits the per-token e4m3 input
+            q8 = isinstance(lw.get("wqkv" if is_attn else "w_gate_up"), ops.quant.Fp8Weight)
             if h is None:
-                x = ops.rms_norm(residual, norm_w, eps)
+                x = ops.rms_norm(residual, norm_w, eps, quant_out=q8)
             else:
-                x, residual = ops.fused_add_rms_norm(h, residual, norm_w, eps)
+                x, residual = ops.fused_add_rms_norm(h, residual, norm_w, eps, quant_out=q8)
             if is_attn:
                 a = self._attention(ops.linear(x, lw["wqkv"], defer=DEFER_QKV), self.kv_index[l], meta)
                 # defer: a split-K o-projection's reduce is fused into the MLP half's add + RMSNorm

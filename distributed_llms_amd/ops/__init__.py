@@ -18,7 +18,7 @@ import os
 import torch
 
 from .. import _ext
-from . import gemm
+from . import gemm, quant
 from . import reference as ref
 
 __all__ = [
@@ -56,40 +56,67 @@ def embedding(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
 
 
 # --------------------------------------------------------------------- K2
-def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+def _q8_out(x_like: torch.Tensor):
+    h = x_like.shape[-1]
+    m = x_like.numel() // h
+    return (torch.empty(m, h, dtype=quant.FP8, device=x_like.device),
+            torch.empty(m, dtype=torch.float32, device=x_like.device))
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, quant_out: bool = False):
+    """``quant_out``: return the output as a per-token e4m3 :class:`quant.Fp8Act` for a W8A8 GEMM
+    (quantized in the norm kernel's epilogue on the GPU)."""
     if not _gpu(x):
-        return ref.rms_norm(x, w, eps)
+        y = ref.rms_norm(x, w, eps)
+        return quant.Fp8Act(*quant.quantize_rows_ref(y), y.shape, y.dtype) if quant_out else y
     _ck(x, "rms_norm.x")
     _ck(w, "rms_norm.w")
     h = x.shape[-1]
+    if quant_out:
+        q, s = _q8_out(x)
+        _ext.kernels().rms_norm_q8(0, x.data_ptr(), 0, w.data_ptr(), x.numel() // h, h, float(eps), q.data_ptr(),
+                                   s.data_ptr(), _stream())
+        return quant.Fp8Act(q, s, x.shape, x.dtype)
     y = torch.empty_like(x)
     _ext.kernels().rms_norm(y.data_ptr(), x.data_ptr(), 0, w.data_ptr(), x.numel() // h, h, float(eps), _stream())
     return y
 
 
 def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
-                       eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+                       eps: float, quant_out: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """residual <- x + residual (in place); returns (rms_norm(residual) * w, residual).
 
     ``x`` may be a :class:`gemm.SplitKPartial` (split-K GEMM output not yet reduced): the
-    reduction then happens inside the same kernel (splitk_add_rms_norm)."""
+    reduction then happens inside the same kernel (splitk_add_rms_norm).  ``quant_out``: the
+    normalised output comes back as a :class:`quant.Fp8Act` (see :func:`rms_norm`)."""
     if isinstance(x, gemm.SplitKPartial):
         _ck(residual, "fused_add_rms_norm.residual")
         _ck(w, "fused_add_rms_norm.w")
         if tuple(x.shape) != tuple(residual.shape):
             raise ValueError("x/residual shape mismatch")
+        if quant_out:
+            q, s = _q8_out(residual)
+            _ext.kernels().splitk_add_rms_norm_q8(0, residual.data_ptr(), x.ws.data_ptr(), x.splits, x.m, x.n,
+                                                  w.data_ptr(), float(eps), q.data_ptr(), s.data_ptr(), _stream())
+            return quant.Fp8Act(q, s, residual.shape, residual.dtype), residual
         y = torch.empty_like(residual)
         _ext.kernels().splitk_add_rms_norm(y.data_ptr(), residual.data_ptr(), x.ws.data_ptr(), x.splits, x.m, x.n,
                                            w.data_ptr(), float(eps), _stream())
         return y, residual
     if not _gpu(x):
-        return ref.fused_add_rms_norm(x, residual, w, eps)
+        y, residual = ref.fused_add_rms_norm(x, residual, w, eps)
+        return (quant.Fp8Act(*quant.quantize_rows_ref(y), y.shape, y.dtype) if quant_out else y), residual
     _ck(x, "fused_add_rms_norm.x")
     _ck(residual, "fused_add_rms_norm.residual")
     _ck(w, "fused_add_rms_norm.w")
     if x.shape != residual.shape:
         raise ValueError("x/residual shape mismatch")
     h = x.shape[-1]
+    if quant_out:
+        q, s = _q8_out(x)
+        _ext.kernels().rms_norm_q8(0, x.data_ptr(), residual.data_ptr(), w.data_ptr(), x.numel() // h, h,
+                                   float(eps), q.data_ptr(), s.data_ptr(), _stream())
+        return quant.Fp8Act(q, s, x.shape, x.dtype), residual
     y = torch.empty_like(x)
     _ext.kernels().rms_norm(y.data_ptr(), x.data_ptr(), residual.data_ptr(), w.data_ptr(), x.numel() // h, h,
                             float(eps), _stream())
@@ -108,7 +135,12 @@ def gelu_tanh(x):
 # --------------------------------------------------------------- GEMM
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, defer: bool = False):
     """y = x @ w^T (+bias). w is [N, K].  ``defer`` (GPU): the result may come back as a
-    :class:`gemm.SplitKPartial` for ``fused_add_rms_norm`` to reduce (or ``materialize()``)."""
+    :class:`gemm.SplitKPartial` for ``fused_add_rms_norm`` to reduce (or ``materialize()``).
+    ``w`` may be a :class:`quant.Fp8Weight` (W8A8 e4m3 GEMM, no bias)."""
+    if isinstance(w, quant.Fp8Weight):
+        if bias is not None:
+            raise ValueError("linear: fp8 weights take no bias")
+        return quant.linear_fp8(x, w, defer=defer)
     if not _gpu(x):
         return ref.linear(x, w, bias)
     return gemm.linear(x, w, bias, defer=defer)
@@ -116,6 +148,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     """silu(x @ Wg^T) * (x @ Wu^T), W = [Wg; Wu]; fused into the GEMM epilogue on the GPU (decode)."""
+    if isinstance(w_gate_up, quant.Fp8Weight):
+        return quant.linear_fp8(x, w_gate_up, swiglu=True)
     if _gpu(x):
         from . import gemm
         y = gemm.linear_swiglu(x, w_gate_up)

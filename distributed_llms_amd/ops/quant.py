@@ -1,0 +1,217 @@
+"""FP8 (OCP e4m3) W8A8 decode GEMMs -- the quantization capability the reference only documents
+(``plan.md:109-112,438-456``, ``snippets.md:684-833`` sketch bitsandbytes int8/int4
+with an absmax fallback; the reference code never quantizes anything).
+
+MI355X-native form: CDNA4's block-scaled MFMA (``v_mfma_scale_f32_16x16x128_f8f6f4``) runs e4m3 at
+twice the bf16 rate, and an e4m3 weight is half the bytes, so the decode projections -- which sit on
+the bf16 ridge at batch 256 -- get both halves of their bound cut:
+
+* weights: per-output-channel absmax scales, quantized once at load (:func:`quantize_weight`);
+* activations: per-token absmax scales, quantized on the fly by ``quant_fp8_rows``
+  (csrc/kernels/quant.hip);
+* GEMM: ``gemm_wide_fp8`` (csrc/kernels/gemm_wide.hip) -- the wide kernel's LDS-DMA pipeline with
+  fp8 K-tiles of 128, scales applied in the epilogue (also before SwiGLU and before split-K slabs,
+  so the bf16 path's deferred reductions are reused unchanged).
+
+Opt-in (``EngineConfig.quant = "fp8"``, ``bench.py --quant fp8``): the LM head, embeddings, norms,
+attention and the KV cache stay bf16, and so do MoE experts.  CPU tensors take the PyTorch
+reference below (same quantization, f32 math), which is also the numerics oracle of the GPU tests.
+"""
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+import torch
+
+from .. import _ext
+
+FP8 = torch.float8_e4m3fn
+FP8_MAX = 448.0
+QUANT_KEYS = ("wqkv", "wo", "w_gate_up", "w_down")
+
+
+class Fp8Weight:
+    """An [N, K] weight as e4m3 values ``q`` and per-row (output channel) f32 ``scale``:
+    w ~= q * scale[:, None]."""
+
+    __slots__ = ("q", "scale")
+
+    def __init__(self, q: torch.Tensor, scale: torch.Tensor):
+        if q.dtype != FP8 or q.dim() != 2 or scale.shape != (q.shape[0],) or scale.dtype != torch.float32:
+            raise ValueError("Fp8Weight: q [N, K] float8_e4m3fn and scale [N] float32")
+        self.q, self.scale = q.contiguous(), scale.contiguous()
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    @property
+    def device(self):
+        return self.q.device
+
+    @property
+    def dtype(self):
+        return FP8
+
+    def numel(self) -> int:
+        return self.q.numel()
+
+    def nbytes(self) -> int:
+        return self.q.numel() + 4 * self.scale.numel()
+
+    def dequantize(self, dtype=torch.float32) -> torch.Tensor:
+        return (self.q.float() * self.scale[:, None]).to(dtype)
+
+    def __repr__(self):
+        return f"Fp8Weight(shape={tuple(self.q.shape)}, device={self.q.device})"
+
+
+class Fp8Act:
+    """A per-token quantized activation [..., K]: e4m3 ``q`` [M, K], f32 ``scale`` [M].  Produced by
+    the norm kernels when the next GEMM takes fp8 (``ops.rms_norm(..., quant=True)``), consumed by
+    :func:`linear_fp8` without a separate quantization launch."""
+
+    __slots__ = ("q", "scale", "shape", "dtype")
+
+    def __init__(self, q, scale, shape, dtype):
+        self.q, self.scale, self.shape, self.dtype = q, scale, tuple(shape), dtype
+
+    @property
+    def device(self):
+        return self.q.device
+
+    @property
+    def is_cuda(self):
+        return self.q.is_cuda
+
+    def dequantize(self) -> torch.Tensor:
+        return (self.q.float() * self.scale[:, None]).to(self.dtype).reshape(self.shape)
+
+
+def _absmax_scale(amax: torch.Tensor) -> torch.Tensor:
+    # a tensor divisor: torch divides a GPU tensor by a Python scalar as a multiply by its
+    # (inexact) reciprocal; the kernel, and the CPU, divide correctly rounded
+    return torch.where(amax > 0, amax / torch.full_like(amax, FP8_MAX), torch.ones_like(amax))
+
+
+def quantize_weight(w: torch.Tensor) -> Fp8Weight:
+    """Per-output-channel absmax quantization of an [N, K] weight (any float dtype, any device)."""
+    wf = w.float()
+    s = _absmax_scale(wf.abs().amax(dim=1))
+    q = (wf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    return Fp8Weight(q, s)
+
+
+def quantize_rows_ref(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-row (per-token) absmax quantization, PyTorch reference: (q [M, K] e4m3, scale [M] f32)."""
+    xf = x.reshape(-1, x.shape[-1]).float()
+    s = _absmax_scale(xf.abs().amax(dim=1))
+    return (xf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8), s
+
+
+def quantize_rows(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-token quantization of a bf16 activation [..., K] -> (q [M, K] e4m3, scale [M] f32); the
+    HIP kernel on the GPU (bit-identical to :func:`quantize_rows_ref`)."""
+    if not x.is_cuda:
+        return quantize_rows_ref(x)
+    if x.dtype != torch.bfloat16 or not x.is_contiguous():
+        raise ValueError("quantize_rows: bf16 contiguous activations")
+    k = x.shape[-1]
+    m = x.numel() // k
+    if k % 8:
+        raise ValueError("quantize_rows: K % 8")
+    q = torch.empty(m, k, dtype=FP8, device=x.device)
+    s = torch.empty(m, dtype=torch.float32, device=x.device)
+    _ext.kernels().quant_fp8_rows(q.data_ptr(), s.data_ptr(), x.data_ptr(), m, k,
+                                  torch.cuda.current_stream().cuda_stream)
+    return q, s
+
+
+def linear_ref(x, w: Fp8Weight, swiglu: bool = False) -> torch.Tensor:
+    """The W8A8 product in f32 from the quantized operands (CPU path and GPU-test oracle);
+    ``x``: a float tensor (quantized here) or an :class:`Fp8Act`."""
+    q, s = (x.q, x.scale) if isinstance(x, Fp8Act) else quantize_rows_ref(x)
+    y = (q.float() * s[:, None]) @ w.dequantize(torch.float32).t().to(q.device)
+    if swiglu:
+        g, u = y.chunk(2, dim=-1)
+        y = torch.nn.functional.silu(g) * u
+    return y.to(x.dtype).reshape(*x.shape[:-1], y.shape[-1])
+
+
+# 128 < M <= 256 split-K grids (qkv / o / down): two 128-row tiles with half the K slices instead of
+# one 256-row tile -- a third fewer staged bytes per workgroup per K-tile (the loop is bound by its
+# LDS-DMA staging): o_8b 21.4 -> 18.1 us, qkv 20.3 -> 19.6 us, down equal (bench/fp8_bench.py --sweep)
+FP8_BM128 = os.environ.get("DLLM_FP8_BM128", "1") != "0"
+
+
+def fp8_plan(m: int, n: int, k: int, swiglu: bool = False) -> Tuple[int, int]:
+    """(K slices, row-tile override or 0) of gemm_wide_fp8 for this shape.  Default: the bf16
+    kernel's rule on the 128-K tiles (a K-tile of fp8 holds the bytes of a 64-K bf16 tile)."""
+    from .gemm import wide_splits
+    s = wide_splits(m, n, k // 2, swiglu)
+    if FP8_BM128 and not swiglu and s > 1 and 128 < m <= 256:
+        tiles = (n // 128) * 2
+        return max(1, min(round(256 / tiles), (k // 128) // 4, 16)), 128
+    return s, 0
+
+
+def fp8_splits(m: int, n: int, k: int, swiglu: bool = False) -> int:
+    return fp8_plan(m, n, k, swiglu)[0]
+
+
+def linear_fp8(x: torch.Tensor, w: Fp8Weight, swiglu: bool = False, defer: bool = False, splits: int = 0):
+    """y = x w^T (``swiglu``: silu(x Wg^T) * (x Wu^T), w = [Wg; Wu]) with W8A8 e4m3 operands.
+    ``defer``: may return a :class:`~distributed_llms_amd.ops.gemm.SplitKPartial` (no SwiGLU)."""
+    if not x.is_cuda:
+        return linear_ref(x, w, swiglu)
+    from .gemm import SplitKPartial, _workspace
+    pre = isinstance(x, Fp8Act)
+    k = x.shape[-1]
+    n, kw = w.shape
+    if kw != k:
+        raise ValueError(f"linear_fp8: x[..., {k}] vs w {tuple(w.shape)}")
+    if n % 128 or k % 128:
+        raise ValueError("linear_fp8: N % 128 and K % 128")
+    if x.dtype != torch.bfloat16:
+        raise TypeError("linear_fp8: bf16 activations")
+    if pre:
+        xq, xs = x.q, x.scale
+        m = xq.shape[0]
+    else:
+        x = x.contiguous()
+        m = x.numel() // k
+        xq, xs = quantize_rows(x)
+    s, bm = fp8_plan(m, n, k, swiglu)
+    if splits:
+        s, bm = splits, 0
+    ws = _workspace(x.device)
+    if s > 1 and s * m * n > ws.numel():
+        s = max(1, ws.numel() // (m * n))
+    # weights streamed non-temporal only where one row tile covers M (each weight byte read once)
+    variant = (1 if m <= 256 else 4) | (bm << 8)
+    stream = torch.cuda.current_stream().cuda_stream
+    kern = _ext.kernels()
+    if defer and not swiglu and s > 1:
+        se = kern.gemm_wide_fp8(0, xq.data_ptr(), xs.data_ptr(), w.q.data_ptr(), w.scale.data_ptr(), ws.data_ptr(),
+                                ws.numel(), m, n, k, s, 2, variant, stream)
+        return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
+    y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
+    kern.gemm_wide_fp8(y.data_ptr(), xq.data_ptr(), xs.data_ptr(), w.q.data_ptr(), w.scale.data_ptr(), ws.data_ptr(),
+                       ws.numel(), m, n, k, s, 1 if swiglu else 0, variant, stream)
+    return y
+
+
+def quantize_layers(layers, keys=QUANT_KEYS) -> int:
+    """Replace the dense projections of every layer dict by :class:`Fp8Weight` (in place); returns
+    how many were converted.  MoE expert stacks, norms and biases are left as they are."""
+    n = 0
+    for lw in layers:
+        for name in keys:
+            t = lw.get(name)
+            # the GPU kernel tiles N and K by 128 (CPU reference: any shape)
+            if isinstance(t, torch.Tensor) and t.dim() == 2 and (not t.is_cuda or (t.shape[0] % 128 == 0
+                                                                                 and t.shape[1] % 128 == 0)):
+                lw[name] = quantize_weight(t)
+                n += 1
+    return n
