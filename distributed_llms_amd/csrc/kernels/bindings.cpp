@@ -28,6 +28,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("gemm_wide_fp8", &dllm::gemm_wide_fp8);
   m.def("quant_fp8_rows", &dllm::quant_fp8_rows);
   m.def("rms_norm_q8", &dllm::rms_norm_q8);
+  m.def("moe_wide_gemm_fp8", &dllm::moe_wide_gemm_fp8);
   m.def("splitk_add_rms_norm_q8", &dllm::splitk_add_rms_norm_q8);
   m.def("gemm_sq", &dllm::gemm_sq);
   m.def("moe_combine", &dllm::moe_combine);

@@ -510,11 +510,16 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_fp8_kernel(const uint8_t* __
 // the decode regime of Mixtral at B >= 128 (32-128 rows per expert), where the weight-streaming
 // grouped kernel (moe.hip) runs its MFMAs at a fraction of the rate.
 // ---------------------------------------------------------------------------------------------
-template <int BM, bool SWIGLU, int VAR>
+template <int BM, bool SWIGLU, int VAR, bool FP8 = false>
 __device__ __forceinline__ void moe_wide_rows(bf16* smem, bf16* __restrict__ Y, const bf16* __restrict__ X,
                                               const int* __restrict__ gather, const bf16* __restrict__ We, int cnt,
-                                              int off, int N, int K, int n_t, int wv, int lane) {
+                                              int off, int N, int K, int n_t, int wv, int lane,
+                                              const float* __restrict__ sa = nullptr,
+                                              const float* __restrict__ sb = nullptr) {
+  // FP8: X / We hold e4m3 bytes addressed in 2-byte units (K / 2 per row); sa: per-slot activation
+  // scales (slot order), sb: this expert's per-channel weight scales
   constexpr int AI = BM / 64, BI = 2, RT = BM / 64;
+  const int KU = FP8 ? K / 2 : K;
   const int wm = wv >> 1, wn = wv & 1;
   const int ldy = SWIGLU ? N / 2 : N;
   for (int r0 = 0; r0 < cnt; r0 += BM) {
@@ -526,41 +531,45 @@ __device__ __forceinline__ void moe_wide_rows(bf16* smem, bf16* __restrict__ Y, 
       const int r = 8 * (wv * AI + j) + (lane >> 3);
       const int slot = off + r0 + min(r, rows - 1);
       const int src = gather ? gather[slot] : slot;
-      srcA[j] = X + (size_t)src * K + wswz(r, lane & 7) * 8;
+      srcA[j] = X + (size_t)src * KU + wswz(r, lane & 7) * 8;
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
       const int r = 8 * (wv * BI + j) + (lane >> 3);
-      srcB[j] = We + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + wswz(r, lane & 7) * 8;
+      srcB[j] = We + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * KU + wswz(r, lane & 7) * 8;
     }
     f32x4 acc[RT][4];
-    wide_mainloop<BM, 3, VAR>(smem, srcA, srcB, K / WBK, acc, wv, lane);
-    wide_epilogue<BM, false, SWIGLU>(acc, Y + (size_t)(off + r0) * ldy, nullptr, rows, N, 0, n_t, 0, wm, wn, lane);
+    wide_mainloop<BM, 3, VAR, FP8>(smem, srcA, srcB, KU / WBK, acc, wv, lane);
+    wide_epilogue<BM, false, SWIGLU, FP8>(acc, Y + (size_t)(off + r0) * ldy, nullptr, rows, N, 0, n_t, 0, wm, wn,
+                                          lane, FP8 ? sa + off + r0 : nullptr, sb);
     __syncthreads();   // the next chunk's prologue refills buffers other waves may still read
   }
 }
 
-template <bool SWIGLU>
+template <bool SWIGLU, bool FP8 = false>
 __global__ void __launch_bounds__(512, 1) moe_wide_kernel(bf16* __restrict__ Y, const bf16* __restrict__ X,
                                                           const int* __restrict__ gather, const bf16* __restrict__ W,
                                                           const int* __restrict__ counts,
-                                                          const int* __restrict__ offsets, int N, int K, int nt) {
+                                                          const int* __restrict__ offsets, int N, int K, int nt,
+                                                          const float* __restrict__ sa = nullptr,
+                                                          const float* __restrict__ wscale = nullptr) {
   __shared__ __attribute__((aligned(16))) bf16 smem[3 * (128 + WBN) * WBK];
   const int e = blockIdx.y;
   const int cnt = counts[e];
   if (cnt == 0) return;                       // uniform across the workgroup
   const int off = offsets[e];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const bf16* We = W + (size_t)e * N * K;
+  const bf16* We = W + (size_t)e * N * (FP8 ? K / 2 : K);
+  const float* sb = FP8 ? wscale + (size_t)e * N : nullptr;
   // an expert's weight tile is read once when its rows fit one row tile: stream it nt (variant 2);
   // with several row chunks the re-reads should hit the caches (default policy)
   if (cnt <= 64) {
-    if (nt) moe_wide_rows<64, SWIGLU, 2>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
-    else moe_wide_rows<64, SWIGLU, 1>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+    if (nt) moe_wide_rows<64, SWIGLU, 2, FP8>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
+    else moe_wide_rows<64, SWIGLU, 1, FP8>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
   } else if (cnt <= 128 && nt) {
-    moe_wide_rows<128, SWIGLU, 2>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+    moe_wide_rows<128, SWIGLU, 2, FP8>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
   } else {
-    moe_wide_rows<128, SWIGLU, 1>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane);
+    moe_wide_rows<128, SWIGLU, 1, FP8>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
   }
 }
 
@@ -575,11 +584,36 @@ void moe_wide_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uint
   const int ntiles = mode == 1 ? (N / 2) / 64 : N / WBN;
   static const int nt = [] { const char* e = getenv("DLLM_MOE_WIDE_NT"); return e ? atoi(e) : 1; }();
   if (mode == 1)
-    hipLaunchKernelGGL(moe_wide_kernel<true>, dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
-                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt);
+    hipLaunchKernelGGL((moe_wide_kernel<true, false>), dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
+                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt,
+                       (const float*)nullptr, (const float*)nullptr);
   else
-    hipLaunchKernelGGL(moe_wide_kernel<false>, dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
-                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt);
+    hipLaunchKernelGGL((moe_wide_kernel<false, false>), dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
+                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt,
+                       (const float*)nullptr, (const float*)nullptr);
+  DLLM_HIP_CHECK(hipGetLastError());
+}
+
+// FP8 experts: X e4m3 [tokens or slots, K] (+ gather), W e4m3 [E, N, K] with per-channel scales
+// wscale [E, N], sa: per-slot activation scales in slot order.  K % 128 == 0.
+void moe_wide_gemm_fp8(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets,
+                       int E, int N, int K, int mode, uintptr_t sa, uintptr_t wscale, uintptr_t stream) {
+  DLLM_HOST_CHECK(E >= 1, "experts >= 1");
+  DLLM_HOST_CHECK(K % 128 == 0, "fp8 K must be a multiple of 128");
+  DLLM_HOST_CHECK(N % 128 == 0, "N must be a multiple of 128");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode");
+  DLLM_HOST_CHECK(sa != 0 && wscale != 0, "fp8 grouped GEMM needs both scale vectors");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int ntiles = mode == 1 ? (N / 2) / 64 : N / WBN;
+  static const int nt = [] { const char* e = getenv("DLLM_MOE_WIDE_NT"); return e ? atoi(e) : 1; }();
+  if (mode == 1)
+    hipLaunchKernelGGL((moe_wide_kernel<true, true>), dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
+                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt,
+                       (const float*)sa, (const float*)wscale);
+  else
+    hipLaunchKernelGGL((moe_wide_kernel<false, true>), dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
+                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt,
+                       (const float*)sa, (const float*)wscale);
   DLLM_HIP_CHECK(hipGetLastError());
 }
 

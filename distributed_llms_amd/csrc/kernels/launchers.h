@@ -48,6 +48,8 @@ void moe_router_route(uintptr_t x, uintptr_t w, int T, int H, int E, int k, uint
                       uintptr_t counts, uintptr_t offsets, uintptr_t sorted_tok, uintptr_t inv, uintptr_t stream);
 void moe_wide_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets,
                    int E, int N, int K, int mode, uintptr_t stream);
+void moe_wide_gemm_fp8(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets,
+                       int E, int N, int K, int mode, uintptr_t sa, uintptr_t wscale, uintptr_t stream);
 void moe_combine(uintptr_t out, uintptr_t ysorted, uintptr_t topk_w, uintptr_t inv, int T, int H, int k,
                  uintptr_t stream);
 

@@ -183,8 +183,9 @@ class ModelStage:
         return self
 
     def quantize(self, mode: str) -> "ModelStage":
-        """``"fp8"``: the dense projections (qkv, o, gate|up, down) become W8A8 e4m3 weights
-        (ops/quant.py); embeddings, norms, LM head, MoE experts and the KV cache stay in ``dtype``."""
+        """``"fp8"``: the dense projections (qkv, o, gate|up, down) and MoE expert stacks become
+        W8A8 e4m3 weights (ops/quant.py); embeddings, norms, router, LM head and the KV cache stay
+        in ``dtype``."""
         if mode in ("", "none", None):
             return self
         if mode != "fp8":

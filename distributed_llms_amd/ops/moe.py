@@ -48,8 +48,14 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     e_all = w_router.shape[0]
     if not (0 <= expert_offset and expert_offset + w_gate_up.shape[0] <= e_all):
         raise ValueError(f"experts [{expert_offset}, {expert_offset + w_gate_up.shape[0]}) outside the router's {e_all}")
+    from . import quant
+    fp8 = isinstance(w_gate_up, quant.Fp8Experts)
+    if fp8 != isinstance(w_down, quant.Fp8Experts):
+        raise TypeError("moe: gate|up and down experts must both be fp8 or both not")
     if not x.is_cuda:
         tw, tid = ref.moe_route(ref.linear(x, w_router), top_k)
+        if fp8:
+            return quant.moe_mlp_ref(x, w_gate_up, w_down, tw, tid - expert_offset)
         return ref.moe_mlp(x, w_gate_up, w_down, tw, tid - expert_offset)
     from . import linear, silu_mul
     k = _ext.kernels()
@@ -81,7 +87,28 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     ys = (torch.zeros if ep else torch.empty)(t * top_k, h, dtype=x.dtype, device=dev)
     # the local experts' counts / offsets are a contiguous slice of the routing arrays
     cnt_p, off_p = counts.data_ptr() + 4 * expert_offset, offsets.data_ptr() + 4 * expert_offset
-    if t <= GROUPED_MAX_TOKENS:
+    if fp8:
+        # W8A8 experts (ops/quant.py): per-token e4m3 x gathered by the grouped kernel (its scales in
+        # slot order), SwiGLU output re-quantized per slot row for the down projection
+        if x.dtype != torch.bfloat16 or two_i % 128 or h % 128 or inter % 128:
+            raise ValueError("moe fp8: bf16 activations, expert dims multiples of 128")
+        if t <= GROUPED_MAX_TOKENS:
+            xq, xsc = quant.quantize_rows(x)
+            sa = xsc.index_select(0, sorted_tok.long())
+            act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
+            k.moe_wide_gemm_fp8(act.data_ptr(), xq.data_ptr(), sorted_tok.data_ptr(), w_gate_up.q.data_ptr(), cnt_p,
+                                off_p, e_loc, two_i, h, 1, sa.data_ptr(), w_gate_up.scale.data_ptr(), st)
+            aq, asc = quant.quantize_rows(act)
+            k.moe_wide_gemm_fp8(ys.data_ptr(), aq.data_ptr(), 0, w_down.q.data_ptr(), cnt_p, off_p, e_loc, h, inter,
+                                0, asc.data_ptr(), w_down.scale.data_ptr(), st)
+        else:
+            xs = x.index_select(0, sorted_tok.long())
+            off = offsets.cpu().tolist()      # prefill only: eager, host sync is fine here
+            for j in range(e_loc):
+                a, b = off[expert_offset + j], off[expert_offset + j + 1]
+                if b > a:
+                    ys[a:b] = quant.linear_fp8(quant.linear_fp8(xs[a:b], w_gate_up[j], swiglu=True), w_down[j])
+    elif t <= GROUPED_MAX_TOKENS:
         act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
         rows = -(-t * top_k // e)        # expected rows per expert picks the kernel's row tile
         if 0 < WIDE_MIN_PAIRS <= t * top_k and x.dtype == torch.bfloat16 and two_i % 128 == 0 and h % 128 == 0 \

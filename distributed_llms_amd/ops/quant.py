@@ -13,9 +13,12 @@ the bf16 ridge at batch 256 -- get both halves of their bound cut:
   fp8 K-tiles of 128, scales applied in the epilogue (also before SwiGLU and before split-K slabs,
   so the bf16 path's deferred reductions are reused unchanged).
 
+Mixtral experts take the same scheme through the grouped kernel (``moe_wide_gemm_fp8``: fp8 token
+rows gathered by the expert-sorted slot list, per-(expert, channel) weight scales).
+
 Opt-in (``EngineConfig.quant = "fp8"``, ``bench.py --quant fp8``): the LM head, embeddings, norms,
-attention and the KV cache stay bf16, and so do MoE experts.  CPU tensors take the PyTorch
-reference below (same quantization, f32 math), which is also the numerics oracle of the GPU tests.
+router, attention and the KV cache stay bf16.  CPU tensors take the PyTorch reference below (same
+quantization, f32 math), which is also the numerics oracle of the GPU tests.
 """
 from __future__ import annotations
 
@@ -29,6 +32,7 @@ from .. import _ext
 FP8 = torch.float8_e4m3fn
 FP8_MAX = 448.0
 QUANT_KEYS = ("wqkv", "wo", "w_gate_up", "w_down")
+EXPERT_KEYS = ("experts_gate_up", "experts_down")
 
 
 class Fp8Weight:
@@ -67,6 +71,45 @@ class Fp8Weight:
         return f"Fp8Weight(shape={tuple(self.q.shape)}, device={self.q.device})"
 
 
+class Fp8Experts:
+    """A stack of expert weights [E, N, K] as e4m3 ``q`` with per-(expert, channel) f32 ``scale``
+    [E, N]; ``experts[j]`` is expert j's :class:`Fp8Weight`."""
+
+    __slots__ = ("q", "scale")
+
+    def __init__(self, q: torch.Tensor, scale: torch.Tensor):
+        if q.dtype != FP8 or q.dim() != 3 or scale.shape != q.shape[:2] or scale.dtype != torch.float32:
+            raise ValueError("Fp8Experts: q [E, N, K] float8_e4m3fn and scale [E, N] float32")
+        self.q, self.scale = q.contiguous(), scale.contiguous()
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    @property
+    def device(self):
+        return self.q.device
+
+    @property
+    def dtype(self):
+        return FP8
+
+    def is_contiguous(self) -> bool:
+        return True
+
+    def numel(self) -> int:
+        return self.q.numel()
+
+    def nbytes(self) -> int:
+        return self.q.numel() + 4 * self.scale.numel()
+
+    def __getitem__(self, j: int) -> Fp8Weight:
+        return Fp8Weight(self.q[j], self.scale[j])
+
+    def __repr__(self):
+        return f"Fp8Experts(shape={tuple(self.q.shape)}, device={self.q.device})"
+
+
 class Fp8Act:
     """A per-token quantized activation [..., K]: e4m3 ``q`` [M, K], f32 ``scale`` [M].  Produced by
     the norm kernels when the next GEMM takes fp8 (``ops.rms_norm(..., quant=True)``), consumed by
@@ -101,6 +144,14 @@ def quantize_weight(w: torch.Tensor) -> Fp8Weight:
     s = _absmax_scale(wf.abs().amax(dim=1))
     q = (wf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
     return Fp8Weight(q, s)
+
+
+def quantize_experts(w: torch.Tensor) -> Fp8Experts:
+    """Per-(expert, output channel) absmax quantization of an [E, N, K] expert stack."""
+    wf = w.float()
+    s = _absmax_scale(wf.abs().amax(dim=2))
+    q = (wf / s[..., None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    return Fp8Experts(q, s)
 
 
 def quantize_rows_ref(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -202,16 +253,37 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, swiglu: bool = False, defer: bool 
     return y
 
 
-def quantize_layers(layers, keys=QUANT_KEYS) -> int:
-    """Replace the dense projections of every layer dict by :class:`Fp8Weight` (in place); returns
-    how many were converted.  MoE expert stacks, norms and biases are left as they are."""
+def moe_mlp_ref(x: torch.Tensor, w_gate_up: Fp8Experts, w_down: Fp8Experts, topk_w: torch.Tensor,
+                topk_ids: torch.Tensor) -> torch.Tensor:
+    """Mixtral expert MLPs with W8A8 experts (reference): per-token e4m3 inputs, per-row e4m3
+    SwiGLU outputs, f32 products -- the numerics of the grouped fp8 kernels."""
+    t, h = x.shape
+    out = torch.zeros(t, h, dtype=torch.float32, device=x.device)
+    for e in range(w_gate_up.shape[0]):
+        tok, slot = (topk_ids == e).nonzero(as_tuple=True)
+        if tok.numel() == 0:
+            continue
+        y = linear_ref(linear_ref(x[tok], w_gate_up[e], swiglu=True), w_down[e])
+        out.index_add_(0, tok, y.float() * topk_w[tok, slot].unsqueeze(1).float())
+    return out.to(x.dtype)
+
+
+def quantize_layers(layers, keys=QUANT_KEYS, expert_keys=EXPERT_KEYS) -> int:
+    """Replace the dense projections (and MoE expert stacks) of every layer dict by
+    :class:`Fp8Weight` / :class:`Fp8Experts` (in place); returns how many were converted.  The
+    router, norms and biases stay as they are."""
+    def ok(t, dims):
+        # the GPU kernels tile N and K by 128 (CPU reference: any shape)
+        return isinstance(t, torch.Tensor) and t.dim() == dims and (
+            not t.is_cuda or (t.shape[-2] % 128 == 0 and t.shape[-1] % 128 == 0))
     n = 0
     for lw in layers:
         for name in keys:
-            t = lw.get(name)
-            # the GPU kernel tiles N and K by 128 (CPU reference: any shape)
-            if isinstance(t, torch.Tensor) and t.dim() == 2 and (not t.is_cuda or (t.shape[0] % 128 == 0
-                                                                                 and t.shape[1] % 128 == 0)):
-                lw[name] = quantize_weight(t)
+            if ok(lw.get(name), 2):
+                lw[name] = quantize_weight(lw[name])
+                n += 1
+        for name in expert_keys:
+            if ok(lw.get(name), 3):
+                lw[name] = quantize_experts(lw[name])
                 n += 1
     return n

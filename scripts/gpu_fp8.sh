@@ -9,3 +9,9 @@ for q in fp8 none; do
   timeout -k 10 400 python bench.py --steps 2 --warmup 1 --quant $q > gpurun_out/bench_$q.log 2>&1 || { echo "bench $q failed"; tail -30 gpurun_out/bench_$q.log; exit 1; }
   echo "$q: $(tail -1 gpurun_out/bench_$q.log | cut -c1-200)"
 done
+if [ -n "${FP8_MOE:-}" ]; then
+  for q in fp8 none; do
+    timeout -k 10 500 python bench.py --model mixtral-8x7b --steps 1 --warmup 1 --quant $q > gpurun_out/bench_moe_$q.log 2>&1 || { echo "moe bench $q failed"; tail -30 gpurun_out/bench_moe_$q.log; exit 1; }
+    echo "mixtral $q: $(tail -1 gpurun_out/bench_moe_$q.log | cut -c1-220)"
+  done
+fi

@@ -48,14 +48,29 @@ def test_linear_dispatches_fp8_weights(swiglu):
         ops.linear(x, fw, bias=torch.zeros(32))
 
 
-def test_stage_quantize_converts_only_dense_projections():
+def test_stage_quantize_converts_projections_and_experts():
     ecfg = EngineConfig(model="tiny-mixtral", dtype="float32", device="cpu", quant="fp8")
     s = build_stage(ecfg)
     lw = s.layers[0]
     assert isinstance(lw["wqkv"], quant.Fp8Weight) and isinstance(lw["wo"], quant.Fp8Weight)
-    assert all(isinstance(t, torch.Tensor) for k, t in lw.items() if k not in quant.QUANT_KEYS)
+    assert isinstance(lw["experts_gate_up"], quant.Fp8Experts) and isinstance(lw["experts_down"], quant.Fp8Experts)
+    skip = set(quant.QUANT_KEYS) | set(quant.EXPERT_KEYS)
+    assert all(isinstance(t, torch.Tensor) for k, t in lw.items() if k not in skip)     # router, norms
     with pytest.raises(ValueError):
         EngineConfig(model="tiny-llama", quant="int3").validate()
+
+
+def test_fp8_moe_tracks_the_bf16_moe():
+    from distributed_llms_amd.ops import moe
+    torch.manual_seed(1)
+    t, h, i, e = 12, 64, 96, 4
+    x = torch.randn(t, h)
+    wr, gu, dn = torch.randn(e, h), torch.randn(e, 2 * i, h) * 0.1, torch.randn(e, h, i) * 0.1
+    ref = moe.forward(x, wr, gu, dn, 2)
+    out = moe.forward(x, wr, quant.quantize_experts(gu), quant.quantize_experts(dn), 2)
+    assert ((out - ref).norm() / ref.norm()) < 0.08
+    with pytest.raises(TypeError):
+        moe.forward(x, wr, quant.quantize_experts(gu), dn, 2)
 
 
 def test_cpu_engine_runs_fp8():

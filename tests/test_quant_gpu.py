@@ -135,3 +135,22 @@ def test_fp8_act_input_skips_requantization():
     act = quant.Fp8Act(*quant.quantize_rows(x), x.shape, x.dtype)
     assert torch.equal(quant.linear_fp8(act, w), quant.linear_fp8(x, w))
     assert quant.fp8_plan(m, n, k) == (4, 128)                      # the two-row-tile split plan
+
+
+@pytest.mark.parametrize("t", [5, 64, 256, 300])
+def test_fp8_moe_matches_reference(t):
+    """Grouped fp8 expert GEMMs (decode, t <= 256) and the per-expert fp8 prefill path against
+    quant.moe_mlp_ref on the same quantized experts."""
+    from distributed_llms_amd.ops import moe, reference as R
+    torch.manual_seed(t)
+    h, i, e, k = 256, 384, 8, 2
+    x = (torch.randn(t, h) * 0.5).to(DEV, torch.bfloat16)
+    wr = (torch.randn(e, h) * 0.1).to(DEV, torch.bfloat16)
+    gu = quant.quantize_experts((torch.randn(e, 2 * i, h) * 0.05).to(DEV))
+    dn = quant.quantize_experts((torch.randn(e, h, i) * 0.05).to(DEV))
+    out = moe.forward(x, wr, gu, dn, k).float().cpu()
+    tw, tid = R.moe_route(R.linear(x.float().cpu(), wr.float().cpu()), k)
+    ref = quant.moe_mlp_ref(x.cpu(), quant.Fp8Experts(gu.q.cpu(), gu.scale.cpu()),
+                            quant.Fp8Experts(dn.q.cpu(), dn.scale.cpu()), tw, tid).float()
+    err = (out - ref).abs().max().item()
+    assert err <= 3e-2 * ref.abs().max().item() + 1e-3, err
