@@ -40,13 +40,13 @@ def timeit(fn, iters):
     return statistics.median(ts)
 
 
-def gemm_only(xq, xs, w, m, n, k, sw, y, splits=0, bm=0):
+def gemm_only(xq, xs, w, m, n, k, sw, y, splits=0, bm=0, grp=False):
     s, bm0 = quant.fp8_plan(m, n, k, sw)
     if splits:
         s, bm0 = splits, bm
     bm = bm0
     ws = gemm._workspace(xq.device)
-    v = (1 if m <= 256 else 4) | (bm << 8)
+    v = (1 if m <= 256 else (4 | (64 if grp else 0))) | (bm << 8)
     _ext.kernels().gemm_wide_fp8(y.data_ptr(), xq.data_ptr(), xs.data_ptr(), w.q.data_ptr(), w.scale.data_ptr(),
                                  ws.data_ptr(), ws.numel(), m, n, k, s, 1 if sw else 0, v,
                                  torch.cuda.current_stream().cuda_stream)
@@ -81,8 +81,10 @@ def main():
                 "fp8": lambda i: quant.linear_fp8(x, w8[i % len(w8)], swiglu=sw),
                 "gemm": lambda i: gemm_only(xq, xs, w8[i % len(w8)], m, n, k, sw, y),
                 "quant": lambda i: quant.quantize_rows(x),
+                **({"grp": lambda i: gemm_only(xq, xs, w8[i % len(w8)], m, n, k, sw, y, grp=True)} if m > 256 else {}),
                 **{f"s{c}": (lambda i, c=c: gemm_only(xq, xs, w8[i % len(w8)], m, n, k, sw, y,
-                                                      *map(int, c.split("x")))) for c in a.sweep},
+                                                      *map(int, c.split("x")))) for c in a.sweep
+                   if int(c.split("x")[0]) * m * n <= gemm._workspace(x.device).numel()},
             }
             reps = max(len(w8), 8)
             graphs = {}
@@ -109,7 +111,8 @@ def main():
             rows.append((name, m, t["bf16"], t["fp8"], t["gemm"]))
             print(f"{name:12s} {m:5d} {t['bf16']*1e6:8.1f} {t['fp8']*1e6:8.1f} {t['gemm']*1e6:8.1f} "
                   f"{t['bf16']/t['fp8']:8.2f} {tf:7.0f}  quant {t['quant']*1e6:5.1f} "
-                  + " ".join(f"{c} {t['s' + c]*1e6:6.1f}" for c in a.sweep), flush=True)
+                  + (f"grouped {t['grp']*1e6:7.1f} " if "grp" in t else "")
+                  + " ".join(f"{c} {t['s' + c]*1e6:6.1f}" for c in a.sweep if "s" + c in t), flush=True)
         del wb, w8
         torch.cuda.empty_cache()
     if a.out:

@@ -479,8 +479,18 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_fp8_kernel(const uint8_t* __
     const int q = total >> 3, r = total & 7, x = b & 7;
     b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
   }
-  const int m_t = b % mtiles, rest = b / mtiles;
-  const int split = rest % nsplit, n_t = rest / nsplit;
+  int m_t = b % mtiles, rest = b / mtiles;
+  int split = rest % nsplit, n_t = rest / nsplit;
+  if constexpr ((VAR & 64) != 0) {
+    // large M (prefill), no K split: groups of 8 row tiles walk the column tiles together, so the
+    // blocks resident on an XCD share their A row tiles and a band of B in its L2 instead of
+    // every block streaming its own A tile against one B tile
+    const int ntl = N / WBN;                 // column tiles (SwiGLU: (N / 2) / 64, the same count)
+    const int per = 8 * ntl, g = b / per, first = g * 8, gsz = min(mtiles - first, 8);
+    m_t = first + (b % per) % gsz;
+    n_t = (b % per) / gsz;
+    split = 0;
+  }
   const int m0 = m_t * BM;
   const int kt0 = split * kt_per_split;
   const int nt = max(0, min(KU / WBK, kt0 + kt_per_split) - kt0);
@@ -723,15 +733,19 @@ int gemm_wide_fp8(uintptr_t c, uintptr_t a, uintptr_t a_scale, uintptr_t b, uint
   const long grid = (long)ntiles * mtiles * S;
   DLLM_HOST_CHECK(grid >= 1 && grid < (1L << 31), "grid");
   if (S > 1) DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
-  // weights nt where the grid has no K split (as the bf16 kernel's variant 1)
+  // weights nt where the grid has no K split (as the bf16 kernel's variant 1); variant | 64: grouped
+  // row-tile order for large M (no K split)
   const bool nt = (variant & 7) != 4 && S == 1;
+  const bool grp = (variant & 64) != 0 && S == 1 && !nt;
 #define DLLM_F8_GO3(BM_, SPLIT_, SW_, V_)                                                                   \
   hipLaunchKernelGGL((gemm_wide_fp8_kernel<BM_, SPLIT_, SW_, 3, V_>), dim3((unsigned)grid), dim3(512), 0, s,  \
                      (const uint8_t*)a, (const uint8_t*)b, (const float*)a_scale, (const float*)b_scale,      \
                      (bf16*)c, (float*)ws, M, N, K, kts, S)
 #define DLLM_F8_GO(BM_, SPLIT_, SW_)                                   \
   do {                                                                \
-    if (nt) DLLM_F8_GO3(BM_, SPLIT_, SW_, 2); else DLLM_F8_GO3(BM_, SPLIT_, SW_, 1); \
+    if (nt) DLLM_F8_GO3(BM_, SPLIT_, SW_, 2);                          \
+    else if (grp && !SPLIT_) DLLM_F8_GO3(BM_, SPLIT_, SW_, 65);          \
+    else DLLM_F8_GO3(BM_, SPLIT_, SW_, 1);                              \
   } while (0)
   if (S == 1) {
     if (BM == 64) { if (swiglu) DLLM_F8_GO(64, false, true); else DLLM_F8_GO(64, false, false); }

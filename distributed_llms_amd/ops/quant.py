@@ -194,6 +194,8 @@ def linear_ref(x, w: Fp8Weight, swiglu: bool = False) -> torch.Tensor:
 # one 256-row tile -- a third fewer staged bytes per workgroup per K-tile (the loop is bound by its
 # LDS-DMA staging): o_8b 21.4 -> 18.1 us, qkv 20.3 -> 19.6 us, down equal (bench/fp8_bench.py --sweep)
 FP8_BM128 = os.environ.get("DLLM_FP8_BM128", "1") != "0"
+# prefill-sized M (> 256, no K split): grouped row-tile order (gemm_wide_fp8 variant bit 64)
+FP8_GROUP_M = os.environ.get("DLLM_FP8_GROUP_M", "0") == "1"
 
 
 def fp8_plan(m: int, n: int, k: int, swiglu: bool = False) -> Tuple[int, int]:
@@ -240,7 +242,7 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, swiglu: bool = False, defer: bool 
     if s > 1 and s * m * n > ws.numel():
         s = max(1, ws.numel() // (m * n))
     # weights streamed non-temporal only where one row tile covers M (each weight byte read once)
-    variant = (1 if m <= 256 else 4) | (bm << 8)
+    variant = (1 if m <= 256 else (4 | (64 if FP8_GROUP_M else 0))) | (bm << 8)
     stream = torch.cuda.current_stream().cuda_stream
     kern = _ext.kernels()
     if defer and not swiglu and s > 1:
