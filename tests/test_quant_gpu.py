@@ -41,6 +41,8 @@ def _oracle(x, w, swiglu=False):
     (256, 2048, 4096, True, 4),          # split-K SwiGLU (splitk_reduce_swiglu)
     (256, 4096, 14336, False, 0),        # down_8b
     (1000, 1024, 1024, False, 1),        # prefill-sized M, several row tiles
+    (5000, 1024, 512, True, 0),          # grouped row-tile order (M >= DLLM_FP8_GROUP_M), SwiGLU
+    (4500, 2048, 1024, False, 0),        # grouped, partial last row tile and group
 ])
 def test_gemm_wide_fp8_matches_reference(m, n, k, swiglu, splits):
     torch.manual_seed(m + n)
@@ -135,6 +137,7 @@ def test_fp8_act_input_skips_requantization():
     act = quant.Fp8Act(*quant.quantize_rows(x), x.shape, x.dtype)
     assert torch.equal(quant.linear_fp8(act, w), quant.linear_fp8(x, w))
     assert quant.fp8_plan(m, n, k) == (4, 128)                      # the two-row-tile split plan
+    assert quant.fp8_plan(256, 6144, 4096) == (2, 128)
 
 
 @pytest.mark.parametrize("t", [5, 64, 256, 300])
