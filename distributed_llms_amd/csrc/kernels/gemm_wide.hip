@@ -112,6 +112,15 @@ __device__ __forceinline__ int wide_b_row(int r, int n_t, int half) {
   return ((g & 1) ? half : 0) + n_t * 64 + (g >> 1) * 16 + (r & 15);
 }
 
+// Large-M (prefill) block order, no K split: groups of 8 row tiles walk the column tiles together,
+// so the blocks resident on an XCD share their A row tiles and a band of B in its L2 instead of
+// every block streaming its own A tile against one B tile.  b: the XCD-remapped block index.
+__device__ __forceinline__ void grouped_tile(int b, int mtiles, int ntiles, int& m_t, int& n_t) {
+  const int per = 8 * ntiles, g = b / per, first = g * 8, gsz = min(mtiles - first, 8);
+  m_t = first + (b % per) % gsz;
+  n_t = (b % per) / gsz;
+}
+
 // epilogue shared by both wide kernels: acc[rt][ct] lane holds tile column (lane & 15), rows
 // 4 * (lane >> 4) + i of each 16 x 16 fragment
 // SCALED (fp8 operands): the accumulator is in quantized units; output = acc * sa[m] * sb[n]
@@ -423,9 +432,12 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
     const int q = total >> 3, r = total & 7, x = b & 7;
     b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
   }
-  const int m_t = b % mtiles, rest = b / mtiles;
-  const int split = rest % nsplit, n_t = rest / nsplit;
-  (void)ntiles;
+  int m_t = b % mtiles, rest = b / mtiles;
+  int split = rest % nsplit, n_t = rest / nsplit;
+  if constexpr ((VAR & 64) != 0) {          // prefill M, no K split (grouped_tile)
+    grouped_tile(b, mtiles, ntiles, m_t, n_t);
+    split = 0;
+  }
   const int m0 = m_t * BM;
   const int kt0 = split * kt_per_split;
   // ablations (timing only, wrong results): VAR & 16 skips the K loop (launch + epilogue cost),
@@ -481,14 +493,8 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_fp8_kernel(const uint8_t* __
   }
   int m_t = b % mtiles, rest = b / mtiles;
   int split = rest % nsplit, n_t = rest / nsplit;
-  if constexpr ((VAR & 64) != 0) {
-    // large M (prefill), no K split: groups of 8 row tiles walk the column tiles together, so the
-    // blocks resident on an XCD share their A row tiles and a band of B in its L2 instead of
-    // every block streaming its own A tile against one B tile
-    const int ntl = N / WBN;                 // column tiles (SwiGLU: (N / 2) / 64, the same count)
-    const int per = 8 * ntl, g = b / per, first = g * 8, gsz = min(mtiles - first, 8);
-    m_t = first + (b % per) % gsz;
-    n_t = (b % per) / gsz;
+  if constexpr ((VAR & 64) != 0) {          // prefill M, no K split (column tiles: N / 128 both ways)
+    grouped_tile(b, mtiles, N / WBN, m_t, n_t);
     split = 0;
   }
   const int m0 = m_t * BM;
@@ -672,8 +678,9 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   // variant | 32: per-row fragment waits (SPLITRD in wide_mainloop; the engine default);
   // ablations (A/B timing only): variant | 8 = no epilogue stores, | 16 = no K loop
   const int abl = variant & 56;
+  const bool grp = (variant & 64) != 0 && S == 1;   // grouped row-tile order (large M)
   variant &= 7;
-  if (variant == 1 && S == 1) variant = 2;
+  if (variant == 1 && S == 1) variant = grp ? 1 : 2;
   else if (variant == 4) variant = 1;
 #define DLLM_WIDE_GO3(BM_, SPLIT_, SW_, V_)                                                                      \
   hipLaunchKernelGGL((gemm_wide_kernel<BM_, SPLIT_, SW_, 3, V_>), dim3((unsigned)grid), dim3(512), 0, s,          \
@@ -683,6 +690,7 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
     if (abl == 8) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 10); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 9); } \
     else if (abl == 16) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 18); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 17); } \
     else if (abl == 32) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 34); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 33); } \
+    else if (grp && !SPLIT_) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 65);                                              \
     else if (variant == 0) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 0);                                                 \
     else if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 2);                                                 \
     else if (variant == 3) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 3);                                                 \

@@ -153,6 +153,21 @@ def test_wide_split_fragment_waits_bit_exact(cuda, m, n, k, splits, swiglu):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("m,n,k,swiglu", [(4500, 1024, 512, False), (5000, 2048, 256, True), (2048, 256, 128, False)])
+def test_wide_grouped_tile_order_bit_exact(cuda, m, n, k, swiglu):
+    """Variant bit 64 (grouped row-tile order for prefill M) only reorders the workgroups: every
+    tile runs the same MFMAs, so outputs are bit-identical to the plain order."""
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    a = gemm.linear_wide(x, w, splits=1, swiglu=swiglu, variant=4)
+    b = gemm.linear_wide(x, w, splits=1, swiglu=swiglu, variant=4 | 64)
+    assert torch.equal(a, b)
+    ref = x.float() @ w.float().t()
+    if swiglu:
+        g, u = ref.chunk(2, -1)
+        ref = torch.nn.functional.silu(g) * u
+    torch.testing.assert_close(b.float(), ref, rtol=2e-2, atol=2e-2)
+
+
 def test_splitk_slabs_keep_output_precision(cuda):
     """Split-K slabs are stored as f16 x 2^-6 (csrc/kernels/common.h, DLLM_PART_TYPE 2): the split
     result must stay within one bf16 ulp of the exact product (plus half an ulp of the output's typical
