@@ -37,6 +37,8 @@ def parse(argv=None):
     ap.add_argument("--max-batch", type=int, default=None)
     ap.add_argument("--max-seq-len", type=int, default=None)
     ap.add_argument("--dtype", default=None)
+    ap.add_argument("--quant", choices=["none", "fp8"], default=None,
+                    help="fp8: workers run W8A8 e4m3 projections / experts (ops/quant.py)")
     ap.add_argument("--heartbeat-timeout", type=float, default=None)
     ap.add_argument("--auto", action="store_true", help="wait for workers, assign + distribute, no REPL prompt")
     ap.add_argument("--auto-recover", action="store_true", help="re-distribute after a worker failure")
@@ -59,7 +61,7 @@ def main(argv=None):
     cfg = EngineConfig.from_file(a.config) if a.config else EngineConfig()
     cfg = cfg.apply_overrides(host=a.host, port=a.port, model=a.model, num_workers=a.workers,
                               max_batch=a.max_batch, max_seq_len=a.max_seq_len, dtype=a.dtype,
-                              heartbeat_timeout=a.heartbeat_timeout)
+                              heartbeat_timeout=a.heartbeat_timeout, quant=a.quant)
     master = MasterNode(a.host, a.port, cfg, auto_recover=a.auto_recover).start()
     print(f"Initializing model {a.model} into {a.workers} shard(s)...", flush=True)
     path = master.initialize_model(a.model, num_shards=a.workers, cache_dir=a.cache_dir)
