@@ -44,7 +44,7 @@ class DecodeGraphRunner:
         self.seq_lens = self.dev_in[3 * mb:4 * mb]
         self.seq_lens.fill_(1)
         self.block_tables = self.dev_in[4 * mb:].view(mb, max_blocks)
-        self.hidden = None if stage.is_first else torch.zeros(mb, cfg.hidden_size, dtype=stage.dtype, device=dev)
+        self.hidden = None if stage.is_first else torch.zeros(mb, stage.in_width, dtype=stage.dtype, device=dev)
         max_splits = 64
         self.ws = (torch.empty(mb * cfg.num_heads * max_splits * cfg.head_dim, dtype=torch.float32, device=dev),
                    torch.empty(mb * cfg.num_heads * max_splits * 2, dtype=torch.float32, device=dev))

@@ -38,12 +38,15 @@ def make_block_manager(num_blocks: int, block_size: int):
 
 
 def build_stage(ecfg: EngineConfig, layer_start: int = 0, layer_end: Optional[int] = None,
-                device: Optional[str] = None, shard_state=None, units=None, tp=None) -> ModelStage:
+                device: Optional[str] = None, shard_state=None, units=None, tp=None,
+                unit_group: int = 2) -> ModelStage:
+    """``units`` / ``unit_group``: the stage's unit range (parallel/planner.py StagePlan)."""
     mcfg = ecfg.model_config()
     layer_end = mcfg.num_layers if layer_end is None else layer_end
     dev = resolve_device(device or ecfg.device)
     dtype = torch_dtype(ecfg.dtype)
-    stage = ModelStage(mcfg, layer_start, layer_end, device=dev, dtype=dtype, units=units, tp=tp)
+    stage = ModelStage(mcfg, layer_start, layer_end, device=dev, dtype=dtype, units=units, tp=tp,
+                       unit_group=unit_group)
     if shard_state is not None:
         stage.load_hf_state(shard_state)
     else:

@@ -7,9 +7,11 @@ embedding on the first stage and final norm + LM head on the last.
 
 Stage I/O:
   first stage  input: token ids [T] int32
-  other stages input: hidden [T, H] (the closed residual stream of the previous stage)
+  other stages input: hidden [T, H] (the closed residual stream of the previous stage), or
+                      [T, H + W] when the cut falls inside a half (sub-layer units): the residual
+                      stream and the pending W-wide qkv / attention output / partial MLP sum
   last stage  output: logits [n, V] for the rows in ``meta.logits_idx``
-  other stages output: hidden [T, H]
+  other stages output: hidden [T, H] or [T, H + W], as above
 """
 from __future__ import annotations
 
@@ -72,7 +74,23 @@ class KVCache:
         return 2 * num_layers * num_kv_heads * head_dim * block_size * dtype_bytes
 
 
-ATTN_KEYS = {"attn_norm", "wqkv", "wo", "ln1_w", "ln1_b", "bqkv", "bo"}
+# A layer is five ATOMS: 0 norm + qkv projection, 1 RoPE + KV append + attention, 2 o-projection,
+# 3 / 4 the MLP over the first / second half of the intermediate columns.  A stage's unit range is
+# counted in units of ``unit_group`` per layer: 2 (halves: unit 0 = atoms 0-2, unit 1 = atoms 3-4)
+# or 5 (one unit per atom; parallel/planner.py).
+QKV_KEYS = {"attn_norm", "wqkv", "ln1_w", "ln1_b", "bqkv"}
+O_KEYS = {"wo", "bo"}
+ATTN_KEYS = QKV_KEYS | O_KEYS
+NATOM = 5
+_HALF_ATOM = (0, 3)          # first atom of half-unit j
+
+
+def unit_to_atom(u: int, group: int) -> int:
+    if group == NATOM:
+        return u
+    if group != 2:
+        raise ValueError(f"unit group must be 2 or {NATOM}")
+    return NATOM * (u // 2) + _HALF_ATOM[u % 2]
 
 
 class ModelStage:
@@ -82,9 +100,10 @@ class ModelStage:
     stage hand-off is always the closed residual stream (one [T, H] tensor)."""
 
     def __init__(self, cfg: ModelConfig, layer_start: int, layer_end: int, device="cpu",
-                 dtype=torch.bfloat16, units: Optional[tuple] = None, tp=None):
+                 dtype=torch.bfloat16, units: Optional[tuple] = None, tp=None, unit_group: int = 2):
         """``tp``: a :class:`~distributed_llms_amd.parallel.tensor_parallel.TPGroup` -- this rank then
-        holds its column / row / vocab shard of every layer (parallel/tensor_parallel.py)."""
+        holds its column / row / vocab shard of every layer (parallel/tensor_parallel.py).
+        ``units``: [u0, u1) in units of ``unit_group`` per layer (2 halves or 5 sub-layer atoms)."""
         from ..parallel.tensor_parallel import TPGroup, check_divisible
         self.tp = tp if tp is not None else TPGroup(0, 1)
         check_divisible(cfg, self.tp.size, self.tp.moe)
@@ -92,18 +111,28 @@ class ModelStage:
         self.hq = cfg.num_heads // self.tp.size
         self.hkv = cfg.num_kv_heads // self.tp.size
         self.q_size_local = self.hq * cfg.head_dim
+        g = int(unit_group)
         if units is None:
-            units = (2 * layer_start, 2 * layer_end)
+            units = (g * layer_start, g * layer_end)
         u0, u1 = int(units[0]), int(units[1])
-        if not (0 <= u0 < u1 <= 2 * cfg.num_layers):
+        if not (0 <= u0 < u1 <= g * cfg.num_layers):
             raise ValueError(f"bad unit range [{u0}, {u1}) for {cfg.num_layers} layers")
         self.cfg = cfg
+        self.unit_group = g
         self.unit_start, self.unit_end = u0, u1
-        self.layer_start, self.layer_end = u0 // 2, (u1 + 1) // 2
-        self.is_first = u0 == 0
-        self.is_last = u1 == 2 * cfg.num_layers
-        # layers whose attention half (and therefore KV cache) lives on this stage
-        self.kv_layers = [l for l in range(self.layer_start, self.layer_end) if u0 <= 2 * l < u1]
+        # the same range in atoms (5 per layer)
+        self.atom_start, self.atom_end = unit_to_atom(u0, g), unit_to_atom(u1, g)
+        a0, a1 = self.atom_start, self.atom_end
+        if a0 % NATOM not in (0, 3) or a1 % NATOM not in (0, 3):
+            if cfg.arch == "gpt2" or cfg.is_moe:
+                raise ValueError("sub-layer cuts need a dense SwiGLU model")
+            if self.tp.enabled:
+                raise ValueError("sub-layer cuts are not combined with tensor parallelism")
+        self.layer_start, self.layer_end = a0 // NATOM, (a1 + NATOM - 1) // NATOM
+        self.is_first = a0 == 0
+        self.is_last = a1 == NATOM * cfg.num_layers
+        # layers whose attention core (and therefore KV cache) lives on this stage
+        self.kv_layers = [l for l in range(self.layer_start, self.layer_end) if self.has(l, 1)]
         self.kv_index = {l: i for i, l in enumerate(self.kv_layers)}
         self.device = torch.device(device)
         self.dtype = dtype
@@ -123,10 +152,49 @@ class ModelStage:
         """Layers with KV on this stage (what the paged KV pool is sized for)."""
         return len(self.kv_layers)
 
+    def has(self, layer: int, atom: int) -> bool:
+        """Does this stage run atom ``atom`` (0..4, see NATOM) of ``layer``?"""
+        return self.atom_start <= NATOM * layer + atom < self.atom_end
+
     def _keep(self, layer: int, name: str) -> bool:
-        has_attn = self.unit_start <= 2 * layer < self.unit_end
-        has_mlp = self.unit_start <= 2 * layer + 1 < self.unit_end
-        return has_attn if name in ATTN_KEYS else has_mlp
+        if name in QKV_KEYS:
+            return self.has(layer, 0)
+        if name in O_KEYS:
+            return self.has(layer, 2)
+        return self.has(layer, 3) or self.has(layer, 4)
+
+    def aux_width(self, atom: int) -> int:
+        """Width of the pending tensor a cut before global atom ``atom`` hands over (0: none)."""
+        j = atom % NATOM
+        if j == 1:
+            return (self.hq + 2 * self.hkv) * self.cfg.head_dim     # qkv projection output
+        if j == 2:
+            return self.q_size_local                                  # attention output
+        if j == 4:
+            return self.cfg.hidden_size                               # partial MLP sum
+        return 0
+
+    @property
+    def in_width(self) -> int:
+        """Columns of this stage's hidden input (non-first stages)."""
+        return self.cfg.hidden_size + self.aux_width(self.atom_start)
+
+    @property
+    def out_width(self) -> int:
+        return self.cfg.hidden_size + (0 if self.is_last else self.aux_width(self.atom_end))
+
+    def _slice_mlp_halves(self):
+        """A stage holding one MLP half of a layer keeps only that half's intermediate columns:
+        rows [c0, c1) of the gate and of the up block of w_gate_up, columns [c0, c1) of w_down."""
+        i = self.cfg.intermediate_size
+        for l, lw in zip(range(self.layer_start, self.layer_end), self.layers):
+            h0, h1 = self.has(l, 3), self.has(l, 4)
+            if h0 == h1 or "w_gate_up" not in lw:
+                continue
+            c0, c1 = (0, i // 2) if h0 else (i // 2, i)
+            gu = lw["w_gate_up"]
+            lw["w_gate_up"] = torch.cat([gu[c0:c1], gu[i + c0:i + c1]], 0).contiguous()
+            lw["w_down"] = lw["w_down"][:, c0:c1].contiguous()
 
     def needs_embed(self) -> bool:
         return self.is_first or (self.is_last and self.cfg.tie_embeddings)
@@ -154,6 +222,7 @@ class ModelStage:
                 from ..parallel.tensor_parallel import shard_block
                 lw = shard_block(cfg, lw, self.tp.rank, self.tp.size, self.tp.moe)   # one full layer at a time
             self.layers.append(lw)
+        self._slice_mlp_halves()
         if self.needs_embed():
             self.embed = W.synth_embed(cfg, seed, self.dtype, self.device)
             if not self.is_first:
@@ -172,6 +241,7 @@ class ModelStage:
         conv = lambda t: t.to(device=self.device, dtype=self.dtype).contiguous()
         self.layers = [{k: conv(v) for k, v in W.hf_to_block(cfg, l, sd).items() if self._keep(l, k)}
                        for l in range(self.layer_start, self.layer_end)]
+        self._slice_mlp_halves()
         if self.needs_embed():
             names = W.hf_embed_names(cfg)
             if not self.is_first:           # tied LM head on the last stage: token table only
@@ -261,35 +331,79 @@ class ModelStage:
         return self.tp.all_reduce_(out) if self.tp.enabled else out
 
     def _units(self):
-        for u in range(self.unit_start, self.unit_end):
-            l = u // 2
-            yield u % 2 == 0, l, self.layers[l - self.layer_start]
+        """(is_attention_half, layer, weights) for the halves this stage runs (whole halves only)."""
+        for l in range(self.layer_start, self.layer_end):
+            lw = self.layers[l - self.layer_start]
+            if self.has(l, 0):
+                yield True, l, lw
+            if self.has(l, 3):
+                yield False, l, lw
+
+    @staticmethod
+    def _dense(t):
+        return t.materialize() if isinstance(t, ops.gemm.SplitKPartial) else t
 
     def _forward_llama(self, inp: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
         cfg = self.cfg
         eps = cfg.norm_eps
-        residual = ops.embedding(inp, self.embed["embed"]) if self.is_first else inp.clone()
+        hs = cfg.hidden_size
+        carry = None   # pending qkv / attention output / partial MLP sum handed over by a sub-layer cut
+        if self.is_first:
+            residual = ops.embedding(inp, self.embed["embed"])
+        elif inp.shape[-1] > hs:
+            residual, carry = inp[:, :hs].contiguous(), inp[:, hs:].contiguous()
+        else:
+            residual = inp.clone()
         h = None   # output of the previous half, not yet added to the residual stream
-        for is_attn, l, lw in self._units():
-            norm_w = lw["attn_norm"] if is_attn else lw["mlp_norm"]
-            # W8A8 projection next (quant="fp8"): the norm kernel emits the per-token e4m3 input
-            q8 = isinstance(lw.get("wqkv" if is_attn else "w_gate_up"), ops.quant.Fp8Weight)
-            if h is None:
-                x = ops.rms_norm(residual, norm_w, eps, quant_out=q8)
-            else:
-                x, residual = ops.fused_add_rms_norm(h, residual, norm_w, eps, quant_out=q8)
-            if is_attn:
-                a = self._attention(ops.linear(x, lw["wqkv"], defer=DEFER_QKV), self.kv_index[l], meta)
-                # defer: a split-K o-projection's reduce is fused into the MLP half's add + RMSNorm
-                # (TP: row-parallel partial sums, all-reduced over the group)
-                if self.tp.enabled:
-                    h = self.tp.all_reduce_(ops.linear(a, lw["wo"]))
+        out_aux = None
+        for l in range(self.layer_start, self.layer_end):
+            lw = self.layers[l - self.layer_start]
+            # ---- attention half: atoms 0 (norm + qkv), 1 (attention), 2 (o-projection)
+            if self.has(l, 0) or self.has(l, 1) or self.has(l, 2):
+                a = qkv = None
+                if self.has(l, 0):
+                    # W8A8 projection next (quant="fp8"): the norm kernel emits the per-token e4m3 input
+                    q8 = isinstance(lw.get("wqkv"), ops.quant.Fp8Weight)
+                    if h is None:
+                        x = ops.rms_norm(residual, lw["attn_norm"], eps, quant_out=q8)
+                    else:
+                        x, residual = ops.fused_add_rms_norm(h, residual, lw["attn_norm"], eps, quant_out=q8)
+                    h = None
+                    qkv = ops.linear(x, lw["wqkv"], defer=DEFER_QKV and self.has(l, 1))
+                    if not self.has(l, 1):
+                        out_aux = self._dense(qkv)
+                        break
+                if self.has(l, 1):
+                    a = self._attention(qkv if qkv is not None else carry, self.kv_index[l], meta)
+                    if not self.has(l, 2):
+                        out_aux = a
+                        break
+                if self.has(l, 2):
+                    a = a if a is not None else carry
+                    # defer: a split-K o-projection's reduce is fused into the MLP half's add + RMSNorm
+                    # (TP: row-parallel partial sums, all-reduced over the group)
+                    if self.tp.enabled:
+                        h = self.tp.all_reduce_(ops.linear(a, lw["wo"]))
+                    else:
+                        h = ops.linear(a, lw["wo"], defer=DEFER_O)
+            # ---- MLP half: atoms 3 / 4 (first / second half of the intermediate columns)
+            if self.has(l, 3) or self.has(l, 4):
+                q8 = isinstance(lw.get("w_gate_up"), ops.quant.Fp8Weight)
+                if h is None:
+                    x = ops.rms_norm(residual, lw["mlp_norm"], eps, quant_out=q8)
                 else:
-                    h = ops.linear(a, lw["wo"], defer=DEFER_O)
-            else:
-                h = self._mlp(x, lw)
-        if isinstance(h, ops.gemm.SplitKPartial):
-            h = h.materialize()
+                    x, residual = ops.fused_add_rms_norm(h, residual, lw["mlp_norm"], eps, quant_out=q8)
+                if self.has(l, 3) and self.has(l, 4):
+                    h = self._mlp(x, lw)
+                elif self.has(l, 3):                  # cut between the MLP halves: hand over the partial sum
+                    out_aux = self._dense(self._mlp(x, lw))
+                    h = None
+                    break
+                else:                                 # second half: add the first half's partial sum
+                    h = ops.add_(self._dense(self._mlp(x, lw)), carry)
+        if out_aux is not None:
+            return torch.cat([residual, out_aux.view(out_aux.shape[0], -1)], dim=1)
+        h = self._dense(h)
         if not self.is_last:
             return ops.add_(residual, h)
         return self._logits(h, residual, meta)

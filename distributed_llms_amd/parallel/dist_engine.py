@@ -23,6 +23,8 @@ from .pipeline import PipelineDriver, inflight_window, stage_worker_loop
 from .planner import plan_units
 
 log = logging.getLogger("dllm.dist")
+# pipelines of dense models cut at sub-layer units (planner.py; DLLM_PP_FINE=0: half layers only)
+FINE_UNITS = os.environ.get("DLLM_PP_FINE", "1") != "0"
 
 
 @dataclass
@@ -180,10 +182,10 @@ class RankRole:
             self._init_tp(ctx, ecfg, mcfg, hf_state)
             return
         self.plan = plan_units(mcfg, ctx.pp, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2),
-                               device=str(ctx.device))
+                               device=str(ctx.device), fine=FINE_UNITS and ctx.tp == 1)
         a, b = self.plan.ranges[ctx.stage]
         stage = build_stage(ecfg, a, b, device=ctx.device, shard_state=hf_state,
-                            units=self.plan.unit_range(ctx.stage), tp=ctx.tpg)
+                            units=self.plan.unit_range(ctx.stage), tp=ctx.tpg, unit_group=self.plan.group)
         nb = plan_kv_blocks(mcfg, stage.num_layers, ecfg, stage.device, stage.hkv)
         nb = agree_min(ctx, nb)        # every stage of a pipeline must hold the same block ids
         if ctx.tp > 1:
@@ -193,7 +195,10 @@ class RankRole:
             self.engine = LLMEngine(ecfg1, stage)
         else:
             self.runner = StageRunner(stage, ecfg, num_blocks=nb)
-            hop = (max(ecfg.max_prefill_tokens, ecfg.max_batch), mcfg.hidden_size, stage.dtype,
+            # IPC slots fit the widest hop of the pipeline (a sub-layer cut adds the pending tensor)
+            width = mcfg.hidden_size + (max(mcfg.qkv_size, mcfg.q_size, mcfg.hidden_size)
+                                        if self.plan.group != 2 else 0)
+            hop = (max(ecfg.max_prefill_tokens, ecfg.max_batch), width, stage.dtype,
                    inflight_window(ecfg, ctx.pp, stage.device))
             self.transport = make_transport(ctx.pipeline_ranks, ctx.stage, ctx.ctrl_group, ctx.data_group,
                                             ctx.device, ctx.ring_group, hop=hop)

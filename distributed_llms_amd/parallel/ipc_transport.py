@@ -108,7 +108,7 @@ class IpcTransport(DistTransport):
         cs.wait_event(ready)
         s = cs.cuda_stream
         self.m.copy_async(self.peer_rx + slot * self.slot_bytes, buf.data_ptr(),
-                          rows * self.hidden * buf.element_size(), s)
+                          buf.numel() * buf.element_size(), s)
         self.m.write_value32(s, self.peer_flag + 4 * slot, use + 1)
         buf.record_stream(cs)
         done = torch.cuda.Event()
@@ -117,7 +117,7 @@ class IpcTransport(DistTransport):
         self._retire()
 
     def recv_hidden(self, rows, hidden, dtype, device):
-        if rows > self.max_rows or hidden != self.hidden or dtype != self.dtype:
+        if rows * hidden > self.slot_elems or dtype != self.dtype:
             raise ValueError(f"hop of ({rows}, {hidden}) {dtype} does not fit the IPC slot")
         n = self._rx_n
         self._rx_n += 1

@@ -53,7 +53,7 @@ def _marker(code: int) -> np.ndarray:
 def stage_worker_loop(runner: StageRunner, transport: Transport, stop_on_round_end: bool = True) -> str:
     """Run a non-first stage until STOP (returns "stop") or ROUND_END (returns "round")."""
     st = runner.stage
-    h = st.cfg.hidden_size
+    h = st.in_width
     last = transport.stage == transport.num_stages - 1
     tr = get_tracer()
     while True:
@@ -284,11 +284,13 @@ def run_loopback_pipeline(ecfg: EngineConfig, num_stages: int, prompts, params: 
 
     mcfg = ecfg.model_config()
     plan = plan_units(mcfg, num_stages, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2),
-                      device=str(device or resolve_device(ecfg.device)))
+                      device=str(device or resolve_device(ecfg.device)),
+                      fine=os.environ.get("DLLM_PP_FINE", "1") != "0")
     hub = LoopbackHub(num_stages)
     runners = []
     for s, (a, b) in enumerate(plan.ranges):
-        stage = build_stage(ecfg, a, b, device=device, shard_state=hf_state, units=plan.unit_range(s))
+        stage = build_stage(ecfg, a, b, device=device, shard_state=hf_state, units=plan.unit_range(s),
+                            unit_group=plan.group)
         runners.append(StageRunner(stage, ecfg, num_blocks=ecfg.num_kv_blocks or 512))
     errors = []
     # capture every stage's decode graphs up front, one at a time: concurrent captures from

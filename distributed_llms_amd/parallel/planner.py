@@ -9,13 +9,21 @@ minimise the most expensive stage.
 Two granularities:
 * whole layers (:func:`plan_stages`) -- checkpoint shards (``shards/shard_{i}.pt`` hold whole
   blocks), cost = weight bytes (+ the LM head on the last stage);
-* half layers (:func:`plan_units`) -- runtime pipelines: unit 2l = attention half of layer l
-  (norm, qkv, RoPE + KV append, attention, o-proj), unit 2l+1 = its MLP half.  Llama-3-8B on 8
-  stages at batch 256 is capped at ~80 % balance by whole-layer cuts (32 layers + an LM head
-  worth ~1.35 layers of time) and at ~93 % by half-layer cuts.  Costs come from a decode time
-  model calibrated on MI355X kernel profiles (profiles/llama3_8b_b256_kernels_current.md): each GEMM
-  takes max(weight bytes / HBM rate, FLOPs / achieved MFMA rate), attention reads the KV of
-  ``ctx`` tokens per sequence, plus fixed per-half elementwise/norm time.
+* half layers (:func:`plan_units`, ``group`` 2) -- runtime pipelines: unit 2l = attention half of
+  layer l (norm, qkv, RoPE + KV append, attention, o-proj), unit 2l+1 = its MLP half.  Llama-3-8B
+  on 8 stages at batch 256 is capped at ~80 % balance by whole-layer cuts (32 layers + an LM head
+  worth ~1.35 layers of time) and at ~93 % by half-layer cuts;
+* sub-layer units (``group`` 5, GPU pipelines of dense models) -- unit 5l + j of layer l is
+  j = 0 norm + qkv projection, 1 RoPE + KV append + attention, 2 o-projection, 3 / 4 the MLP over
+  the first / second half of the intermediate columns (models/stage.py).  The ~100 us attention
+  half is the grain that caps 8 stages at 93 %: a cut can now fall after the qkv projection, after
+  the attention core or between the MLP halves (the hop then carries the residual stream plus the
+  pending qkv / attention output / partial MLP sum), and the DP reaches ~98 % at 8 stages, ~99.4 %
+  at 4 (each cut inside a half prices the extra norm / slicing / wider hop on both sides).
+Costs come from a decode time model calibrated on MI355X kernel profiles
+(profiles/llama3_8b_b256_kernels_current.md): each GEMM takes max(weight bytes / HBM rate, FLOPs /
+achieved MFMA rate), attention reads the KV of ``ctx`` tokens per sequence, plus fixed per-half
+elementwise/norm time.
 """
 from __future__ import annotations
 
@@ -34,13 +42,19 @@ MLP_GEMM_FLOP_PER_US = 9.5e8  # gate_up (SwiGLU fused) + down (0.95 PF)
 HEAD_FLOP_PER_US = 9.85e8     # LM head + argmax (0.99 PF)
 ATTN_FIXED_US = 11.4          # qkv split-K reduce + residual/RMSNorm
 MLP_FIXED_US = 6.3            # residual/RMSNorm (SwiGLU is in the GEMM epilogue)
+# a stage cut inside a half (sub-layer units): the receiving side re-normalises the residual
+# stream, half-width MLP GEMMs fill fewer CUs, partial sums are materialised, the hop is wider
+CUT_US = {1: 4.0, 2: 4.0, 4: 12.0}   # by position j of the cut (after unit 5l + j - 1)
+
+HALF_GROUP, FINE_GROUP = 2, 5
 
 
 @dataclass(frozen=True)
 class StagePlan:
     ranges: Tuple[Tuple[int, int], ...]     # [start, end) layers touched per stage
     costs: Tuple[float, ...]
-    units: Optional[Tuple[Tuple[int, int], ...]] = None   # [start, end) half-layer units per stage
+    units: Optional[Tuple[Tuple[int, int], ...]] = None   # [start, end) units per stage
+    group: int = HALF_GROUP                 # units per layer (2: halves, 5: sub-layer units)
 
     @property
     def num_stages(self) -> int:
@@ -56,7 +70,7 @@ class StagePlan:
         if self.units is not None:
             return self.units[stage]
         a, b = self.ranges[stage]
-        return 2 * a, 2 * b
+        return self.group * a, self.group * b
 
     def imbalance(self) -> float:
         return max(self.costs) / (sum(self.costs) / len(self.costs))
@@ -65,6 +79,7 @@ class StagePlan:
         d = {"ranges": [list(r) for r in self.ranges], "costs": [round(c, 1) for c in self.costs]}
         if self.units is not None:
             d["units"] = [list(u) for u in self.units]
+            d["group"] = self.group
         return d
 
 
@@ -76,8 +91,10 @@ def head_cost(cfg: ModelConfig, dtype_bytes: int = 2) -> float:
     return cfg.head_param_count() * dtype_bytes
 
 
-def _partition(costs: Sequence[float], n: int, head: float, first_extra: float = 0.0) -> List[Tuple[int, int]]:
-    """Exact min-max contiguous partition of ``costs`` into ``n`` parts (head added to the last)."""
+def _partition(costs: Sequence[float], n: int, head: float, first_extra: float = 0.0,
+               cut: Optional[Sequence[float]] = None) -> List[Tuple[int, int]]:
+    """Exact min-max contiguous partition of ``costs`` into ``n`` parts (head added to the last).
+    ``cut[i]``: extra cost a cut before unit i puts on BOTH stages it separates."""
     L = len(costs)
     if not 1 <= n <= L:
         raise ValueError(f"cannot split {L} units into {n} stages")
@@ -87,6 +104,8 @@ def _partition(costs: Sequence[float], n: int, head: float, first_extra: float =
 
     def seg(a, b, s):
         c = pre[b] - pre[a]
+        if cut is not None:
+            c += (cut[a] if a > 0 else 0.0) + (cut[b] if b < L else 0.0)
         if s == 0:
             c += first_extra
         if s == n - 1:
@@ -162,18 +181,61 @@ def unit_costs_cpu(cfg: ModelConfig, ctx: int = 192) -> Tuple[List[float], float
     return [float(attn), float(mlp)] * cfg.num_layers, float(cfg.vocab_size * h)
 
 
+def unit_costs_fine_us(cfg: ModelConfig, batch: int = 256, ctx: int = 192) -> Tuple[List[float], float]:
+    """Per sub-layer unit decode time estimates (us): the half-layer model with the attention half
+    divided between qkv (its GEMM share + the split-K reduce and norm), the attention core (KV
+    read) and the o-projection (its GEMM share), and the MLP half in two equal column halves."""
+    halves, head = unit_costs_us(cfg, batch, ctx)
+    h = cfg.hidden_size
+    qkv_p, o_p = h * cfg.qkv_size, cfg.q_size * h
+    kv_b = batch * ctx * 2 * cfg.kv_size * 2
+    attn_core = kv_b / KV_B_PER_US
+    gemm = halves[0] - attn_core - ATTN_FIXED_US
+    qkv = gemm * qkv_p / (qkv_p + o_p) + ATTN_FIXED_US
+    o = gemm * o_p / (qkv_p + o_p)
+    mlp = halves[1]
+    return [qkv, attn_core, o, mlp / 2, mlp / 2] * cfg.num_layers, head
+
+
+def unit_costs_fine_cpu(cfg: ModelConfig, ctx: int = 192) -> Tuple[List[float], float]:
+    """:func:`unit_costs_cpu` per sub-layer unit (multiply-adds per decoded token)."""
+    h, i = cfg.hidden_size, cfg.intermediate_size
+    qkv, attn, o = h * cfg.qkv_size, 2 * ctx * cfg.q_size, cfg.q_size * h
+    mlp = 3 * h * i / 2
+    return [float(qkv), float(attn), float(o), mlp, mlp] * cfg.num_layers, float(cfg.vocab_size * h)
+
+
+def fine_units_ok(cfg: ModelConfig) -> bool:
+    """Sub-layer units need a dense SwiGLU MLP whose halves keep the GEMM shape rules."""
+    return cfg.arch != "gpt2" and not cfg.is_moe and cfg.intermediate_size % 256 == 0
+
+
 def plan_units(cfg: ModelConfig, num_stages: int, batch: int = 256, ctx: int = 192,
-               device: str = "cuda") -> StagePlan:
-    """Half-layer plan for runtime pipelines (see module doc); ``device`` picks the cost model
-    (GPU decode time model, or :func:`unit_costs_cpu` for CPU stages)."""
-    if str(device).startswith("cpu"):
+               device: str = "cuda", fine: bool = False) -> StagePlan:
+    """Runtime-pipeline plan (see module doc): half-layer units, or sub-layer units with ``fine``
+    (GPU stages of a dense model; ignored elsewhere).  ``device`` picks the cost model (GPU decode
+    time model, or :func:`unit_costs_cpu` for CPU stages)."""
+    cpu = str(device).startswith("cpu")
+    cut = None
+    group = HALF_GROUP
+    if fine and num_stages > 1 and fine_units_ok(cfg):
+        group = FINE_GROUP
+        if cpu:
+            costs, head = unit_costs_fine_cpu(cfg, ctx)
+        else:
+            costs, head = unit_costs_fine_us(cfg, batch, ctx)
+            cut = [CUT_US.get(i % group, 0.0) for i in range(len(costs) + 1)]
+    elif cpu:
         costs, head = unit_costs_cpu(cfg, ctx)
     else:
         costs, head = unit_costs_us(cfg, batch, ctx)
-    units = _partition(costs, num_stages, head)
+    units = _partition(costs, num_stages, head, cut=cut)
     pre = [0.0]
     for c in costs:
         pre.append(pre[-1] + c)
-    cs = [pre[b] - pre[a] + (head if k == num_stages - 1 else 0) for k, (a, b) in enumerate(units)]
-    ranges = tuple((a // 2, (b + 1) // 2) for a, b in units)
-    return StagePlan(ranges, tuple(cs), tuple(units))
+    L = len(costs)
+    cs = [pre[b] - pre[a] + (head if k == num_stages - 1 else 0)
+          + ((cut[a] if a > 0 else 0.0) + (cut[b] if b < L else 0.0) if cut is not None else 0.0)
+          for k, (a, b) in enumerate(units)]
+    ranges = tuple((a // group, (b + group - 1) // group) for a, b in units)
+    return StagePlan(ranges, tuple(cs), tuple(units), group)

@@ -131,6 +131,54 @@ def test_half_layer_stage_chain_matches_full():
         torch.testing.assert_close(x, ref)
 
 
+@pytest.mark.parametrize("cuts", [(1, 2, 4, 8), (3, 6, 7, 9), (2, 4, 11, 14), (4, 5, 6, 12)])
+def test_sub_layer_stage_chain_matches_full(cuts):
+    """Stages cut at sub-layer units (after qkv / after attention / between the MLP halves, a
+    stage inside one layer) hand over [T, H + W] and compose to the full model, prefill and decode."""
+    from distributed_llms_amd.engine.batch import build_host_batch, to_device_meta
+    from distributed_llms_amd.engine.llm_engine import make_block_manager
+    from distributed_llms_amd.engine.scheduler import Scheduler
+    from distributed_llms_amd.engine.sequence import Sequence
+    from distributed_llms_amd.models.stage import ModelStage
+    cfg = get_model_config("tiny-llama")
+    n = 5 * cfg.num_layers
+    full = ModelStage(cfg, 0, cfg.num_layers, "cpu", torch.float32).init_synthetic(5)
+    bounds = (0,) + tuple(cuts) + (n,)
+    parts = [ModelStage(cfg, 0, 0, "cpu", torch.float32, units=(a, b), unit_group=5).init_synthetic(5)
+             for a, b in zip(bounds, bounds[1:])]
+    assert sum(p.num_layers for p in parts) == cfg.num_layers          # each KV layer on one stage
+    for p in parts[1:]:
+        assert p.in_width == cfg.hidden_size + p.aux_width(p.atom_start)
+    for st in [full] + parts:
+        st.allocate_kv(16, 32)
+    bm = make_block_manager(16, 32)
+    sch = Scheduler(bm, 1, 4, 1024, 128)
+    seqs = [Sequence(p) for p in ([3, 4, 5, 6], [9, 9])]
+    for s in seqs:
+        sch.add(s)
+    for it in range(3):                                     # prefill, then two decode steps
+        step = sch.schedule(0)
+        ids, meta = to_device_meta(build_host_batch(step, bm, 32), "cpu")
+        ref = full.forward(ids, meta)
+        x = ids
+        for st in parts:
+            x = st.forward(x, meta)
+            if not st.is_last:
+                assert x.shape[1] == st.out_width
+        torch.testing.assert_close(x, ref, rtol=2e-4, atol=2e-4)
+        sch.complete(step, ref.argmax(-1).to(torch.int32).numpy(), 0.0)
+
+
+def test_fine_unit_plan_balances_8_stages():
+    from distributed_llms_amd.parallel.planner import plan_units
+    cfg = get_model_config("llama3-8b")
+    half = plan_units(cfg, 8, 256, 144)
+    fine = plan_units(cfg, 8, 256, 144, fine=True)
+    assert fine.group == 5 and fine.units[-1][1] == 5 * cfg.num_layers
+    assert fine.imbalance() < 1.04 < half.imbalance()
+    assert plan_units(get_model_config("tiny-mixtral"), 2, 16, 64, fine=True).group == 2   # MoE: halves
+
+
 def test_unit_planner_balances_better_than_layers():
     from distributed_llms_amd.parallel.planner import plan_stages, plan_units, unit_costs_us
     cfg = get_model_config("llama3-8b")
