@@ -74,8 +74,10 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
         busy = [None] * world
         dist.all_gather_object(busy, finish_trace(args, tr, elapsed, ctx.rank), group=ctx.ctrl_group)
     if ctx.rank == 0:
-        extra = {"load_s": round(load_s, 1), "stage_ranges": role.plan.to_json()["ranges"],
-                 "backend": dist.get_backend()}
+        pj = role.plan.to_json()
+        extra = {"load_s": round(load_s, 1), "stage_ranges": pj["ranges"], "backend": dist.get_backend()}
+        if "units" in pj:
+            extra["stage_units"] = {"group": pj["group"], "ranges": pj["units"]}
         if role.driver is not None:
             extra["driver_stall_s"] = round(role.driver.stall_s, 3)
         extra["microbatch_slots"] = slots
