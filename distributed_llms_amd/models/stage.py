@@ -351,7 +351,11 @@ class ModelStage:
         if self.is_first:
             residual = ops.embedding(inp, self.embed["embed"])
         elif inp.shape[-1] > hs:
-            residual, carry = inp[:, :hs].contiguous(), inp[:, hs:].contiguous()
+            # clone, not .contiguous(): a one-row column slice IS contiguous, and the residual is
+            # updated in place -- a view would write into the caller's input (the decode graph's
+            # static buffer, re-read by the capture warm-ups and the replay)
+            residual = inp[:, :hs].clone(memory_format=torch.contiguous_format)
+            carry = inp[:, hs:].clone(memory_format=torch.contiguous_format)
         else:
             residual = inp.clone()
         h = None   # output of the previous half, not yet added to the residual stream

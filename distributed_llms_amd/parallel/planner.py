@@ -210,11 +210,29 @@ def fine_units_ok(cfg: ModelConfig) -> bool:
     return cfg.arch != "gpt2" and not cfg.is_moe and cfg.intermediate_size % 256 == 0
 
 
+def explicit_plan(cfg: ModelConfig, spec: str, num_stages: int) -> StagePlan:
+    """A hand-placed plan: ``spec`` = "g:a,b;b,c;..." -- unit ranges in units of g per layer
+    (``DLLM_PP_UNITS``; operations / experiments)."""
+    g, _, body = spec.partition(":")
+    group = int(g)
+    units = tuple(tuple(int(x) for x in r.split(",")) for r in body.split(";"))
+    if len(units) != num_stages or units[0][0] != 0 or units[-1][1] != group * cfg.num_layers or \
+            any(a[1] != b[0] or a[0] >= a[1] for a, b in zip(units, units[1:] + ((units[-1][1], 0),))):
+        raise ValueError(f"DLLM_PP_UNITS={spec!r} is not a contiguous {num_stages}-stage cover")
+    ranges = tuple((a // group, (b + group - 1) // group) for a, b in units)
+    return StagePlan(ranges, tuple(0.0 for _ in units), units, group)
+
+
 def plan_units(cfg: ModelConfig, num_stages: int, batch: int = 256, ctx: int = 192,
                device: str = "cuda", fine: bool = False) -> StagePlan:
     """Runtime-pipeline plan (see module doc): half-layer units, or sub-layer units with ``fine``
     (GPU stages of a dense model; ignored elsewhere).  ``device`` picks the cost model (GPU decode
-    time model, or :func:`unit_costs_cpu` for CPU stages)."""
+    time model, or :func:`unit_costs_cpu` for CPU stages).  ``DLLM_PP_UNITS`` overrides the plan
+    (:func:`explicit_plan`)."""
+    import os
+    spec = os.environ.get("DLLM_PP_UNITS", "")
+    if spec and num_stages > 1:
+        return explicit_plan(cfg, spec, num_stages)
     cpu = str(device).startswith("cpu")
     cut = None
     group = HALF_GROUP

@@ -169,6 +169,29 @@ def test_sub_layer_stage_chain_matches_full(cuts):
         sch.complete(step, ref.argmax(-1).to(torch.int32).numpy(), 0.0)
 
 
+def test_sub_layer_stage_leaves_its_input_untouched():
+    """A one-row [1, H + W] input's column slices are 'contiguous' views: the stage must copy them
+    (its residual is updated in place), or decode-graph capture warm-ups would compound into the
+    static input buffer."""
+    from distributed_llms_amd.engine.batch import build_host_batch, to_device_meta
+    from distributed_llms_amd.engine.llm_engine import make_block_manager
+    from distributed_llms_amd.engine.scheduler import Scheduler
+    from distributed_llms_amd.engine.sequence import Sequence
+    from distributed_llms_amd.models.stage import ModelStage
+    cfg = get_model_config("tiny-llama")
+    for a in (1, 2, 4):                            # receives qkv / attention output / partial MLP sum
+        st = ModelStage(cfg, 0, 0, "cpu", torch.float32, units=(a, 10), unit_group=5).init_synthetic(5)
+        st.allocate_kv(16, 32)
+        bm = make_block_manager(16, 32)
+        sch = Scheduler(bm, 1, 4, 1024, 128)
+        sch.add(Sequence([3]))
+        ids, meta = to_device_meta(build_host_batch(sch.schedule(0), bm, 32), "cpu")
+        x = torch.randn(1, st.in_width)
+        x0 = x.clone()
+        st.forward(x, meta)
+        assert torch.equal(x, x0), a
+
+
 def test_fine_unit_plan_balances_8_stages():
     from distributed_llms_amd.parallel.planner import plan_units
     cfg = get_model_config("llama3-8b")
