@@ -23,8 +23,10 @@ from .pipeline import PipelineDriver, inflight_window, stage_worker_loop
 from .planner import plan_units
 
 log = logging.getLogger("dllm.dist")
-# pipelines of dense models cut at sub-layer units (planner.py; DLLM_PP_FINE=0: half layers only)
-FINE_UNITS = os.environ.get("DLLM_PP_FINE", "1") != "0"
+# DLLM_PP_FINE=1: pipelines of dense models may cut at sub-layer units (planner.py).  Off by
+# default: measured per-stage decode times on MI355X (profiles/pp_stage_balance.md) show the cuts'
+# own costs (re-normalisation, half-width MLP GEMMs, wider hops) eat the balance they buy
+FINE_UNITS = os.environ.get("DLLM_PP_FINE", "0") == "1"
 
 
 @dataclass

@@ -285,7 +285,7 @@ def run_loopback_pipeline(ecfg: EngineConfig, num_stages: int, prompts, params: 
     mcfg = ecfg.model_config()
     plan = plan_units(mcfg, num_stages, batch=ecfg.max_batch, ctx=max(32, ecfg.max_seq_len // 2),
                       device=str(device or resolve_device(ecfg.device)),
-                      fine=os.environ.get("DLLM_PP_FINE", "1") != "0")
+                      fine=os.environ.get("DLLM_PP_FINE", "0") == "1")
     hub = LoopbackHub(num_stages)
     runners = []
     for s, (a, b) in enumerate(plan.ranges):

@@ -13,13 +13,13 @@ Two granularities:
   layer l (norm, qkv, RoPE + KV append, attention, o-proj), unit 2l+1 = its MLP half.  Llama-3-8B
   on 8 stages at batch 256 is capped at ~80 % balance by whole-layer cuts (32 layers + an LM head
   worth ~1.35 layers of time) and at ~93 % by half-layer cuts;
-* sub-layer units (``group`` 5, GPU pipelines of dense models) -- unit 5l + j of layer l is
-  j = 0 norm + qkv projection, 1 RoPE + KV append + attention, 2 o-projection, 3 / 4 the MLP over
-  the first / second half of the intermediate columns (models/stage.py).  The ~100 us attention
-  half is the grain that caps 8 stages at 93 %: a cut can now fall after the qkv projection, after
-  the attention core or between the MLP halves (the hop then carries the residual stream plus the
-  pending qkv / attention output / partial MLP sum), and the DP reaches ~98 % at 8 stages, ~99.4 %
-  at 4 (each cut inside a half prices the extra norm / slicing / wider hop on both sides).
+* sub-layer units (``group`` 5, opt-in for GPU pipelines of dense models) -- unit 5l + j of layer
+  l is j = 0 norm + qkv projection, 1 RoPE + KV append + attention, 2 o-projection, 3 / 4 the MLP
+  over the first / second half of the intermediate columns (models/stage.py).  A cut inside a half
+  hands over the residual stream plus the pending qkv / attention output / partial MLP sum, and
+  the DP prices each such cut on both stages it separates (CUT_US, fitted to measured stage
+  times).  Measured on MI355X (profiles/pp_stage_balance.md) the cuts' own costs eat the balance
+  they buy (pp8 slowest stage -1.3 %, pp2 / pp4 slower), so pipelines default to halves.
 Costs come from a decode time model calibrated on MI355X kernel profiles
 (profiles/llama3_8b_b256_kernels_current.md): each GEMM takes max(weight bytes / HBM rate, FLOPs /
 achieved MFMA rate), attention reads the KV of ``ctx`` tokens per sequence, plus fixed per-half
@@ -44,7 +44,8 @@ ATTN_FIXED_US = 11.4          # qkv split-K reduce + residual/RMSNorm
 MLP_FIXED_US = 6.3            # residual/RMSNorm (SwiGLU is in the GEMM epilogue)
 # a stage cut inside a half (sub-layer units): the receiving side re-normalises the residual
 # stream, half-width MLP GEMMs fill fewer CUs, partial sums are materialised, the hop is wider
-CUT_US = {1: 4.0, 2: 4.0, 4: 12.0}   # by position j of the cut (after unit 5l + j - 1)
+CUT_US = {1: 6.0, 2: 15.0, 4: 45.0}   # by position j of the cut (after unit 5l + j - 1); fitted to
+# bench/pp_stage_times.py on MI355X (profiles/pp_stage_balance.md)
 
 HALF_GROUP, FINE_GROUP = 2, 5
 
