@@ -26,7 +26,8 @@ def _json_lines(out):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("n,par,trace", [(2, "pp", True), (3, "pp", False), (2, "dp", False), (2, "tp", False)])
+@pytest.mark.parametrize("n,par,trace", [(2, "pp", True), (3, "pp", False), (8, "pp", False), (2, "dp", False),
+                                         (2, "tp", False)])
 def test_torchrun_bench_cpu(n, par, trace, tmp_path):
     env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
