@@ -21,11 +21,13 @@ def sample(logits: torch.Tensor, temperatures: Optional[Seq[float]] = None, top_
     temps = torch.tensor([max(t, 1e-5) for t in temperatures], device=logits.device, dtype=torch.float32)
     lf = logits.float() / temps.unsqueeze(1)
     if top_k is not None and any(k > 0 for k in top_k):
-        kmax = max(top_k)
-        vals, _ = torch.topk(lf, min(kmax, lf.shape[1]), dim=-1)
-        for i, k in enumerate(top_k):
-            if k > 0:
-                lf[i][lf[i] < vals[i, min(k, vals.shape[1]) - 1]] = float("-inf")
+        # one batched mask: row i keeps logits >= its k-th largest (k <= 0: every logit)
+        kmax = min(max(top_k), lf.shape[1])
+        vals, _ = torch.topk(lf, kmax, dim=-1)
+        ks = torch.tensor(list(top_k), device=lf.device)
+        thresh = vals.gather(1, (ks.clamp(1, kmax) - 1).unsqueeze(1))
+        thresh = thresh.masked_fill((ks <= 0).unsqueeze(1), float("-inf"))
+        lf = lf.masked_fill(lf < thresh, float("-inf"))
     probs = torch.softmax(lf, dim=-1)
     if top_p is not None and any(p < 1.0 for p in top_p):
         sp, si = torch.sort(probs, dim=-1, descending=True)
