@@ -96,8 +96,10 @@ def unit_to_atom(u: int, group: int) -> int:
 class ModelStage:
     """Layers ``[layer_start, layer_end)``, or -- finer -- half-layer *units* ``[u0, u1)``:
     unit 2l is the attention half of layer l (norm, qkv, RoPE + KV append, attention, o-proj),
-    unit 2l+1 its MLP half.  Pipeline stages may start or end in the middle of a layer; the
-    stage hand-off is always the closed residual stream (one [T, H] tensor)."""
+    unit 2l+1 its MLP half (``unit_group`` 2), or sub-layer atoms (``unit_group`` 5, see NATOM).
+    Pipeline stages may start or end in the middle of a layer; at a half boundary the hand-off is
+    the closed residual stream ([T, H]), at a cut inside a half it is [T, H + W] (``in_width`` /
+    ``out_width``)."""
 
     def __init__(self, cfg: ModelConfig, layer_start: int, layer_end: int, device="cpu",
                  dtype=torch.bfloat16, units: Optional[tuple] = None, tp=None, unit_group: int = 2):
