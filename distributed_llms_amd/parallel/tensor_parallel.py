@@ -116,8 +116,9 @@ def shard_block(cfg, w: Dict[str, torch.Tensor], rank: int, size: int, moe: str 
     i, a = cfg.intermediate_size, rank * i_l
     if cfg.is_moe and moe == "ep":
         e_l = cfg.num_experts // size
-        out["experts_gate_up"] = w["experts_gate_up"][rank * e_l:(rank + 1) * e_l].contiguous()
-        out["experts_down"] = w["experts_down"][rank * e_l:(rank + 1) * e_l].contiguous()
+        # clone: a leading-dim slice is a contiguous VIEW, which would keep every expert resident
+        out["experts_gate_up"] = w["experts_gate_up"][rank * e_l:(rank + 1) * e_l].clone()
+        out["experts_down"] = w["experts_down"][rank * e_l:(rank + 1) * e_l].clone()
     elif cfg.is_moe:
         gu = w["experts_gate_up"]
         out["experts_gate_up"] = torch.cat([gu[:, a:a + i_l], gu[:, i + a:i + a + i_l]], 1).contiguous()
@@ -133,7 +134,7 @@ def shard_vocab(t: torch.Tensor, rank: int, size: int) -> torch.Tensor:
     if size <= 1:
         return t
     v = t.shape[0] // size
-    return t[rank * v:(rank + 1) * v].contiguous()
+    return t[rank * v:(rank + 1) * v].clone()     # not a view: the full head must not stay resident
 
 
 # ------------------------------------------------------------------ sampling over a vocab shard

@@ -172,3 +172,20 @@ def test_pipeline_of_tensor_parallel_stages_matches_single(model, world, pp, tp)
     assert [r for r in results if results[r] is not None] == [0]     # one driver: stage 0, TP rank 0
     for rnd in results[0]:
         assert rnd == expected
+
+
+def test_shards_own_their_storage():
+    """Every TP / EP shard is a copy, not a view into the full tensor (a leading-dim slice is
+    'contiguous', and a view would keep the whole layer / LM head resident on every rank)."""
+    from distributed_llms_amd.models import weights as W
+    from distributed_llms_amd.parallel.tensor_parallel import shard_block, shard_vocab
+    for name, moe in (("tiny-llama", "tp"), ("tiny-mixtral", "tp"), ("tiny-mixtral", "ep")):
+        cfg = get_model_config(name)
+        full = {n: W.synth_tensor(1, 0, n, s, torch.float32, "cpu") for n, s in W.block_shapes(cfg).items()}
+        for r in range(2):
+            for n, t in shard_block(cfg, full, r, 2, moe).items():
+                if t is not full.get(n):
+                    assert t.untyped_storage().nbytes() == t.numel() * t.element_size(), (name, moe, n)
+    head = torch.randn(64, 16)
+    sh = shard_vocab(head, 1, 4)
+    assert torch.equal(sh, head[16:32]) and sh.untyped_storage().nbytes() == sh.numel() * 4
