@@ -56,7 +56,7 @@ __device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ ((row >
 // wait until at most `younger` tiles of G LDS-DMA instructions each are still in flight
 template <int G>
 __device__ __forceinline__ void wait_tiles(int younger) {
-  static_assert(G == 3 || G == 4 || G == 5 || G == 6, "G");
+  static_assert(G == 3 || G == 4 || G == 5 || G == 6 || G == 7, "G");
   if (younger <= 0) { DLLM_VM(0); return; }
   if constexpr (G == 3) {
     if (younger == 1) DLLM_VM(3); else if (younger == 2) DLLM_VM(6); else DLLM_VM(9);
@@ -64,8 +64,10 @@ __device__ __forceinline__ void wait_tiles(int younger) {
     if (younger == 1) DLLM_VM(4); else if (younger == 2) DLLM_VM(8); else DLLM_VM(12);
   } else if constexpr (G == 5) {
     if (younger == 1) DLLM_VM(5); else if (younger == 2) DLLM_VM(10); else DLLM_VM(15);
-  } else {
+  } else if constexpr (G == 6) {
     if (younger == 1) DLLM_VM(6); else if (younger == 2) DLLM_VM(12); else DLLM_VM(18);
+  } else {
+    if (younger == 1) DLLM_VM(7); else if (younger == 2) DLLM_VM(14); else DLLM_VM(21);
   }
 }
 #undef DLLM_VM
@@ -180,12 +182,23 @@ __device__ __forceinline__ void wide_epilogue(const f32x4 (&acc)[BM / 64][4], bf
 // The K loop shared by the dense and the grouped (MoE) wide kernels: stages A/B tiles through
 // NBUF LDS buffers (LDS-DMA, counted vmcnt, raw barrier) and accumulates acc = A_tile B_tile^T
 // over `nt` 64-deep K-tiles.  srcA/srcB: this lane's staging source for K-tile 0.
+// VAR & 128 (PF): every staging slot also issues one 4-byte LDS-DMA per lane into a 256-byte
+// scratch (`pf_lds`) from `pfB`, a line of the weight tile PFD slots ahead: the weight lines are
+// then in the XCD's L2 when their staging pieces go out, so a tile waits for an L2 hit instead of
+// an HBM round trip.  One more vm op per slot (counted waits use G + 1); results are unchanged.
+constexpr int PFD = 2;
 template <int BM, int NBUF, int VAR, bool FP8 = false>
 __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&srcA)[BM / 64],
                                               const bf16* const (&srcB)[2], int nt, f32x4 (&acc)[BM / 64][4],
-                                              int wv, int lane) {
+                                              int wv, int lane, const bf16* pfB = nullptr, bf16* pf_lds = nullptr) {
   constexpr int AEL = BM * WBK, BEL = WBN * WBK, BUF = AEL + BEL;
-  constexpr int AI = BM / 64, BI = 2, G = AI + BI, RT = BM / 64;
+  constexpr bool PF = (VAR & 128) != 0;
+  constexpr int AI = BM / 64, BI = 2, G0 = AI + BI, G = PF ? G0 + 1 : G0, RT = BM / 64;
+  // the L2 prefetch of the weight tile staged PFD slots after this one (clamped: counts stay static)
+  auto prefetch = [&](int tile) {
+    if constexpr (PF)
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(pfB + min(tile, nt - 1) * WBK), (lds_vptr_w)pf_lds, 4, 0, 0);
+  };
   const int wm = wv >> 1, wn = wv & 1;
   // cache policy of the staging loads (aux: 2 = nt): VAR 2 streams the weights nt, VAR 3 both operands
   constexpr int BAUX = (VAR & 7) >= 2 ? 2 : 0, AAUX = (VAR & 7) == 3 ? 2 : 0;
@@ -239,7 +252,7 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       }
     }
     constexpr int NMF = 2 * RT * 4;
-    constexpr int EVERY = NMF / (G + 1);
+    constexpr int EVERY = NMF / (G0 + 1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -249,18 +262,18 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
           acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][rt], fb[s][ct], acc[rt][ct], 0, 0, 0);
           if constexpr (STG) {
             const int i = (s * RT + rt) * 4 + ct + 1;
-            if (i % EVERY == 0 && i / EVERY <= G) piece(dst, ko, i / EVERY - 1);
+            if (i % EVERY == 0 && i / EVERY <= G0) piece(dst, ko, i / EVERY - 1);
           }
         }
     if constexpr (STG) {
-      // pin the interleave: 8 LDS reads of substep 0, then (EVERY MFMAs, 1 VMEM) x G, rest
+      // pin the interleave: 8 LDS reads of substep 0, then (EVERY MFMAs, 1 VMEM) x G0, rest
       __builtin_amdgcn_sched_group_barrier(0x100, 2 * (RT + 4), 0);
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
+      for (int g = 0; g < G0; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, EVERY, 0);
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, NMF - G * EVERY, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF - G0 * EVERY, 0);
     }
   };
 
@@ -299,8 +312,8 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       if constexpr (STG) {
         const int r = s * RT + rt;
 #pragma unroll
-        for (int p = 0; p < G; ++p)
-          if ((p * ROWS) / G == r) piece(dst, ko, p);
+        for (int p = 0; p < G0; ++p)
+          if ((p * ROWS) / G0 == r) piece(dst, ko, p);
       }
       __builtin_amdgcn_sched_barrier(0);
     };
@@ -346,7 +359,7 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       fb[ct] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     }
     constexpr int NMF = RT * 4;
-    constexpr int EVERY = NMF / (G + 1) > 0 ? NMF / (G + 1) : 1;
+    constexpr int EVERY = NMF / (G0 + 1) > 0 ? NMF / (G0 + 1) : 1;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -354,17 +367,17 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
         acc[rt][ct] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[rt], fb[ct], acc[rt][ct], 0, 0, 0, 127, 0, 127);
         if constexpr (STG) {
           const int i = rt * 4 + ct + 1;
-          if (i % EVERY == 0 && i / EVERY <= G) piece(dst, ko, i / EVERY - 1);
+          if (i % EVERY == 0 && i / EVERY <= G0) piece(dst, ko, i / EVERY - 1);
         }
       }
     if constexpr (STG) {
       __builtin_amdgcn_sched_group_barrier(0x100, 2 * (RT + 4), 0);
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
+      for (int g = 0; g < G0; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, EVERY, 0);
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, NMF - G * EVERY, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF - G0 * EVERY, 0);
     }
   };
   constexpr bool SPLITRD = (VAR & 32) != 0 && RT <= 4 && !FP8;
@@ -372,7 +385,10 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
   if (nt > 0) {
 #pragma unroll
     for (int p = 0; p < NBUF - 1; ++p)
-      if (p < nt) stage(p, p);
+      if (p < nt) {
+        prefetch(p + PFD);
+        stage(p, p);
+      }
     int cur = 0;
     int t = 0;
     // steady state: tile t + NBUF - 1 exists, NBUF - 2 younger tiles stay in flight
@@ -380,6 +396,7 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       wait_tiles<G>(NBUF - 2);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      prefetch(t + NBUF - 1 + PFD);
       // buffer (t-1) % NBUF was last read in iteration t-1, which every wave finished before
       // this barrier: refill it with tile t + NBUF - 1
       const int nb = cur == 0 ? NBUF - 1 : cur - 1;
@@ -418,8 +435,9 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
   constexpr int BI = 2;                       // B glds instructions per thread per tile
   constexpr int G = AI + BI;                  // glds per thread per tile (vmcnt unit)
   constexpr int RT = BM / 64;                 // 16-row fragments per wave in M
-  static_assert(NBUF >= 3 && NBUF * BUF * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BUF];
+  constexpr int PFL = (VAR & 128) ? 128 : 0;  // L2-prefetch scratch (bf16 elements), same LDS array
+  static_assert(NBUF >= 3 && (NBUF * BUF + PFL) * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BUF + PFL];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
@@ -459,8 +477,10 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
     const int r = 8 * i + (lane >> 3);
     srcB[j] = B + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + (size_t)kt0 * WBK + wswz(r, lane & 7) * 8;
   }
+  // PF: lanes l and l + 16k of wave w touch weight row 16 w + (l & 15) of the tile: 128 lines per K-tile
+  const bf16* pfB = B + (size_t)wide_b_row<SWIGLU>(16 * wv + (lane & 15), n_t, N / 2) * K + (size_t)kt0 * WBK;
   f32x4 acc[RT][4];
-  wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, nt, acc, wv, lane);
+  wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, nt, acc, wv, lane, pfB, smem + NBUF * BUF);
   if ((VAR & 8) && nsplit >= 0) return;
   wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
 }
@@ -679,6 +699,7 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   // ablations (A/B timing only): variant | 8 = no epilogue stores, | 16 = no K loop
   const int abl = variant & 56;
   const bool grp = (variant & 64) != 0 && S == 1;   // grouped row-tile order (large M)
+  const bool pf = (variant & 128) != 0;            // L2 prefetch of the weight tile (wide_mainloop PF)
   variant &= 7;
   if (variant == 1 && S == 1) variant = grp ? 1 : 2;
   else if (variant == 4) variant = 1;
@@ -689,6 +710,8 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   do {                                                                                                         \
     if (abl == 8) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 10); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 9); } \
     else if (abl == 16) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 18); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 17); } \
+    else if (pf && abl == 32) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 162); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 161); } \
+    else if (pf) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 130); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 129); } \
     else if (abl == 32) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 34); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 33); } \
     else if (grp && !SPLIT_) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 65);                                              \
     else if (variant == 0) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 0);                                                 \

@@ -153,6 +153,22 @@ def test_wide_split_fragment_waits_bit_exact(cuda, m, n, k, splits, swiglu):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("m,n,k,splits,swiglu", [(256, 28672, 4096, 1, True), (256, 4096, 14336, 8, False),
+                                                (256, 6144, 4096, 5, False), (192, 4096, 4096, 4, False),
+                                                (128, 2048, 1024, 2, False), (40, 1024, 512, 1, False),
+                                                (256, 2048, 192, 3, False), (64, 2048, 128, 2, True)])
+def test_wide_l2_prefetch_bit_exact(cuda, m, n, k, splits, swiglu):
+    """Variant bit 128 (one extra LDS-DMA per staging slot pulls a weight line PFD slots ahead into
+    L2; counted waits move to G + 1) only changes timing: bit-identical to the same variant without
+    it, for the unsplit SwiGLU grid (33), split-K grids (1), short K (fewer tiles than the prefetch
+    distance) and the 64-row tile."""
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    for v in (1, 33):
+        a = gemm.linear_wide(x, w, splits=splits, swiglu=swiglu, variant=v)
+        b = gemm.linear_wide(x, w, splits=splits, swiglu=swiglu, variant=v | 128)
+        assert torch.equal(a, b), v
+
+
 @pytest.mark.parametrize("m,n,k,swiglu", [(4500, 1024, 512, False), (5000, 2048, 256, True), (2048, 256, 128, False)])
 def test_wide_grouped_tile_order_bit_exact(cuda, m, n, k, swiglu):
     """Variant bit 64 (grouped row-tile order for prefill M) only reorders the workgroups: every
