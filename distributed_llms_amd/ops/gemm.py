@@ -295,6 +295,25 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     return y
 
 
+def linear_big(x: torch.Tensor, w: torch.Tensor, splits: int = 2, swiglu: bool = False, defer: bool = False):
+    """Experimental 256 x 256 x 32 tile with one 128 x 128 wave per SIMD (csrc/kernels/gemm_big.hip);
+    split-K only for SwiGLU / deferred outputs."""
+    k = x.shape[-1]
+    n = w.shape[0]
+    m = x.numel() // k
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        raise ValueError("linear_big: bf16 contiguous operands")
+    ws = _workspace(x.device)
+    stream = torch.cuda.current_stream().cuda_stream
+    if defer and not swiglu and splits > 1:
+        se = _ext.kernels().gemm_big(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, splits, 2, stream)
+        return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
+    y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
+    _ext.kernels().gemm_big(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, splits,
+                            1 if swiglu else 0, stream)
+    return y
+
+
 # 256 x 256-tile decode GEMM (gemm_sq.hip) for 128 < M <= 256: a third fewer staged bytes per FLOP
 # than the wide kernel's 256 x 128 tile.  Measured (profiles/wide_gemm.md, "256 x 256 tile"): it
 # wins only where the grid needs no K split -- the LM head (1.05x) and the 70B MLP gate|up (1.07x);

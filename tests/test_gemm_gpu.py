@@ -328,3 +328,19 @@ def test_sq_deferred_into_fused_norm(cuda):
     yr, rr = ref.fused_add_rms_norm(ref.linear(x.float(), w.float()), res0.float(), g.float(), 1e-5)
     torch.testing.assert_close(r.float(), rr, atol=6e-2, rtol=3e-2)
     torch.testing.assert_close(y.float(), yr, atol=6e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m,n,k,splits,swiglu", [(256, 28672, 4096, 2, True), (256, 4096, 14336, 8, False),
+                                                (256, 6144, 4096, 5, False), (200, 1024, 512, 1, False),
+                                                (100, 2048, 1024, 3, False), (256, 512, 64, 2, True),
+                                                (300, 1024, 256, 1, False)])
+def test_big_linear(cuda, m, n, k, splits, swiglu):
+    """gemm_big (256 x 256 x 32 tile, one wave per SIMD): against the fp32 product, SwiGLU through
+    the split-K reduce, rows past M masked, short K (fewer tiles than the three in flight)."""
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear_big(x, w, splits=splits, swiglu=swiglu)
+    ref = x.float() @ w.float().t()
+    if swiglu:
+        g, u = ref.chunk(2, -1)
+        ref = F.silu(g) * u
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
