@@ -48,7 +48,7 @@ def main():
             for s in a.splits:
                 if sw and s == 1:
                     continue
-                if (k // 32) < s:
+                if (k // 32) < s or (s > 1 and s * m * n > gemm._workspace(x.device).numel()):
                     continue
                 impls[f"big_s{s}"] = (lambda w, s=s: gemm.linear_big(x, w, splits=s, swiglu=sw))
             reps = max(copies, 8)
