@@ -48,6 +48,9 @@ def main():
                          "tok/s with a 512 MB buffer vs 23.4k with the warm-tuned table), so it is off")
     ap.add_argument("--max-ms", type=int, default=30, help="per-solution tuning budget")
     ap.add_argument("--out", default=OUT)
+    ap.add_argument("--merge", default=None, metavar="CSV",
+                    help="start from this table (its results are kept; only new shapes are tuned)")
+    ap.add_argument("--skip-decode", action="store_true", help="tune only the --prefill-tokens shapes")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     tmp = a.out + ".tmp%d.csv"     # TunableOp's own end-of-process dump (discarded)
@@ -58,13 +61,16 @@ def main():
     if a.rotating_mb:
         tun.set_rotating_buffer_size(a.rotating_mb)
     tun.enable(True)
+    if a.merge:
+        assert tun.read_file(a.merge), f"could not load {a.merge}"
+        print(f"loaded {len(tun.get_results())} results from {a.merge}", flush=True)
     tun.tuning_enable(True)
     t0 = time.time()
     seen = set()
     for model in a.models:
         for name, (n, k) in shapes(model).items():
             w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
-            ms = list(a.decode_batches) + ([] if name == "lm_head" else list(a.prefill_tokens))
+            ms = ([] if a.skip_decode else list(a.decode_batches)) + ([] if name == "lm_head" else list(a.prefill_tokens))
             for m in ms:
                 if (m, n, k) in seen:
                     continue
