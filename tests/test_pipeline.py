@@ -284,3 +284,23 @@ def test_chunked_prefill_matches_whole_prompt_prefill(stages):
     else:
         out, _, _ = run_loopback_pipeline(cfg, stages, prompts, params)
     assert out == whole
+
+
+def test_explicit_plan_knob(monkeypatch):
+    """DLLM_PP_UNITS places stages by hand (group:ranges); a non-contiguous or incomplete cover is
+    refused; single-stage plans ignore it."""
+    from distributed_llms_amd.parallel.planner import plan_units
+    cfg = get_model_config("tiny-llama")
+    monkeypatch.setenv("DLLM_PP_UNITS", "5:0,8;8,11;11,20")
+    p = plan_units(cfg, 3)
+    assert p.group == 5 and p.units == ((0, 8), (8, 11), (11, 20)) and p.ranges == ((0, 2), (1, 3), (2, 4))
+    for bad in ("5:0,8;9,20", "5:0,8;8,19", "5:0,8;8,8;8,20", "2:1,4;4,8"):   # gap, short, empty, not from 0
+        monkeypatch.setenv("DLLM_PP_UNITS", bad)
+        with pytest.raises(ValueError):
+            plan_units(cfg, bad.count(";") + 1)
+    monkeypatch.setenv("DLLM_PP_UNITS", "5:0,8;8,11;11,20")
+    with pytest.raises(ValueError):
+        plan_units(cfg, 2)                                  # wrong stage count
+    monkeypatch.setenv("DLLM_PP_UNITS", "2:0,3;3,8")
+    assert plan_units(cfg, 2).units == ((0, 3), (3, 8))
+    assert plan_units(cfg, 1).num_stages == 1
