@@ -51,6 +51,10 @@ def test_torchrun_bench_cpu(n, par, trace, tmp_path):
     if trace:   # every rank wrote a timeline; every stage reports its busy fraction
         assert sorted(os.listdir(tmp_path)) == [f"trace_rank{r}.json" for r in range(n)]
         assert len(rec["stage_busy_frac"]) == n and all(0 < b <= 1.0 for b in rec["stage_busy_frac"])
+        # the per-rank host-cost summary (scripts/trace_host_summary.py) reads those timelines
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "trace_host_summary.py"), str(tmp_path)],
+                             capture_output=True, text=True, timeout=120).stdout
+        assert all(f"rank {r}:" in out for r in range(n)) and "stage.decode" in out
 
 
 def test_single_process_bench_json_cpu():
@@ -78,3 +82,14 @@ def test_torchrun_bench_hybrid_dp_pp_cpu():
     rec = _json_lines(r.stdout)[0]
     assert rec["config"]["parallelism"] == "dp2xpp2" and rec["n_gpus"] == 4
     assert rec["microbatch_slots"] == 2 and rec["config"]["global_batch"] == 2 * 3 * 2   # CPU: pp slots
+
+
+def test_pp_stage_times_cpu():
+    """bench/pp_stage_times.py builds every stage of the half-layer and sub-layer plans and times
+    its decode step (CPU, tiny model): both plans print, with per-stage times."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench", "pp_stage_times.py"), "--model", "tiny-llama",
+                        "--pp", "2", "--batch", "4", "--ctx", "40", "--iters", "1", "--device", "cpu"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "pp2 half-layer" in r.stdout and "pp2 sub-layer" in r.stdout and r.stdout.count("stage us") == 2
