@@ -139,12 +139,13 @@ class Scheduler:
         return min(self.max_batch, -(-total // self.num_slots))
 
     # ------------------------------------------------------------ schedule
-    def schedule(self, slot: int = 0) -> Optional[Step]:
+    def schedule(self, slot: int = 0, _retry: bool = True) -> Optional[Step]:
         n_running = self.native.num_running(slot)
         if self.waiting:
             admitted: List[Sequence] = []
             tokens = 0
             target = self._admission_target()
+            blocked = False
             while self.waiting and n_running + len(admitted) < target:
                 seq = self.waiting[0]
                 n = seq.total_len - seq.num_cached
@@ -160,6 +161,7 @@ class Scheduler:
                 seq.chunk = n if n < seq.total_len - seq.num_cached else 0
                 if not self.bm.ensure_capacity(seq.seq_id, seq.num_cached + n):
                     seq.chunk = 0
+                    blocked = True
                     break
                 self.waiting.popleft()
                 seq.status = SeqStatus.RUNNING
@@ -169,6 +171,8 @@ class Scheduler:
             if admitted:
                 self.num_prefilling += len(admitted)
                 return Step(True, admitted, slot)
+            if blocked and _retry and self._break_kv_deadlock():
+                return self.schedule(slot, _retry=False)
         if not n_running:
             return None
         # decode: every running sequence of the slot needs room for one more token; on failure
@@ -179,6 +183,33 @@ class Scheduler:
             return None
         packed, rows, _ = res
         return Step(False, None, slot, rows=rows, packed=packed, live=self.live)
+
+    def _break_kv_deadlock(self) -> bool:
+        """The head of the queue cannot get KV blocks.  While anything runs or a prefill is in
+        flight, blocks will come back (finishes, preemption); when nothing does, the only holders
+        are partly prefilled prompts still waiting for their next chunk, and none of them can
+        advance -- e.g. two long prompts on two slots each holding half of a small pool.  Drop
+        the cached chunks of every waiting prompt but the head (they are recomputed later); if
+        the head alone still cannot fit an otherwise empty pool, it never will: finish it.
+        Returns True when the queue changed (the caller retries once)."""
+        if self.native.num_running_total() > 0 or self.num_prefilling > 0 or not self.waiting:
+            return False
+        head = self.waiting[0]
+        freed = False
+        for s in list(self.waiting)[1:]:
+            if s.num_cached > 0:
+                self.bm.free_sequence(s.seq_id)
+                s.num_cached = 0
+                s.chunk = 0
+                freed = True
+        if freed:
+            return True
+        # nothing else holds blocks: the pool cannot hold the head's next chunk at all
+        self.waiting.popleft()
+        self.bm.free_sequence(head.seq_id)
+        head.finish("kv_capacity")
+        self.finished.append(head)
+        return True
 
     def schedule_lookahead(self, slot: int) -> Optional[Step]:
         """The slot's next decode step, built while its newest decode step is still in flight

@@ -348,12 +348,14 @@ class MasterNode:
         if self.shard_manager is not None:
             ranges = [tuple(r) for r in self.shard_manager.read_plan(self.shard_manager.shard_dir)["ranges"]]
             unit_ranges = [(2 * a, 2 * b) for a, b in ranges]
+            group = 2
             paths = self.shard_manager.get_shard_paths()
         else:
             up = plan_units(cfg, n, batch=self.config.max_batch, ctx=max(32, self.config.max_seq_len // 2),
                             device=self._plan_device())
             ranges = list(up.ranges)
             unit_ranges = list(up.units)
+            group = up.group
             paths = [None] * n
         ecfg = self.config.apply_overrides(model=self.model_spec, num_workers=n)
         ed = ecfg.to_dict()
@@ -368,7 +370,7 @@ class MasterNode:
         hosts += [None] * (n - len(hosts))
         host_workers = [sum(1 for h in hosts if h is not None and h == hosts[i]) or 1 for i in range(n)]
         return [{"shard_id": i, "stage": i, "num_stages": n, "layer_range": list(ranges[i]),
-                 "unit_range": list(unit_ranges[i]), "host_workers": host_workers[i],
+                 "unit_range": list(unit_ranges[i]), "unit_group": group, "host_workers": host_workers[i],
                  "shard_path": paths[i], "engine_config": ed, "dist": dist} for i in range(n)]
 
     def distribute_shards(self, timeout: float = 1800.0, ship_bytes: bool = False) -> Dict[str, Any]:

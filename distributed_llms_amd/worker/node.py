@@ -425,7 +425,9 @@ class WorkerNode:
             state = load_shard_file(plan["shard_path"])
         if state is not None and ecfg.model_config().arch == "gpt2":
             state.pop("lm_head.weight", None)
-        stage = build_stage(ecfg, a, b, device=self.device, shard_state=state, units=plan.get("unit_range"))
+        group = int(plan.get("unit_group", 2))
+        stage = build_stage(ecfg, a, b, device=self.device, shard_state=state, units=plan.get("unit_range"),
+                            unit_group=group)
         del state
         ctx = None
         if world > 1:
@@ -443,9 +445,13 @@ class WorkerNode:
             self.stage_runner = StageRunner(stage, ecfg, num_blocks=nb)
             from ..parallel.dist_engine import make_transport
             from ..parallel.pipeline import inflight_window
+            # hop slots fit the widest hop of the plan: a sub-layer cut (group != 2) also carries the
+            # pending tensor next to the hidden state (as parallel/dist_engine.py sizes it)
+            mc = stage.cfg
+            width = mc.hidden_size + (max(mc.qkv_size, mc.q_size, mc.hidden_size) if group != 2 else 0)
             transport = make_transport(list(range(world)), stage_idx, ctx.ctrl_group, ctx.data_group, self.device,
                                        ctx.ring_group,
-                                       hop=(max(ecfg.max_prefill_tokens, ecfg.max_batch), stage.cfg.hidden_size,
+                                       hop=(max(ecfg.max_prefill_tokens, ecfg.max_batch), width,
                                             stage.dtype, inflight_window(ecfg, world, stage.device)))
             if stage_idx == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)

@@ -257,3 +257,63 @@ def test_abort_of_a_partly_prefilled_prompt_frees_its_blocks():
     sch.complete(sch.schedule(0), [1])
     assert s.num_cached == 16 and bm.num_free() == 63 - 4
     assert sch.abort(s.seq_id) and bm.num_free() == 63
+
+
+def test_partial_prompts_on_two_slots_do_not_deadlock_a_tight_pool():
+    """two long prompts chunk-prefilled on two slots can each hold part of a pool too
+    small for both; with nothing running, the scheduler must drop the other prompt's cached chunks
+    (recomputed later) instead of returning None forever."""
+    bm = make_block_manager(11, 4)                              # 10 usable blocks = 40 tokens
+    sch = Scheduler(bm, num_slots=2, max_batch=4, max_prefill_tokens=16, max_seq_len=64)
+    sch.MIN_CHUNK = 4
+    a, b = _seq(30, 2), _seq(30, 2)
+    sch.add(a)
+    sch.add(b)
+    sa, sb = sch.schedule(0), sch.schedule(1)
+    assert sa.seqs == [a] and sb.seqs == [b] and a.chunk == 16 and b.chunk == 16
+    sch.complete(sa, [0])
+    sch.complete(sb, [0])
+    assert bm.num_free() == 2 and a.num_cached == 16 and b.num_cached == 16
+    steps = 0
+    while sch.has_work():
+        progressed = False
+        for slot in (0, 1):
+            st = sch.schedule(slot)
+            if st is not None:
+                sch.complete(st, [7] * st.size)
+                progressed = True
+        assert progressed, "scheduler stalled with work left"
+        steps += 1
+        assert steps < 100
+    fin = sch.pop_finished()
+    assert sorted(s.seq_id for s in fin) == sorted([a.seq_id, b.seq_id])
+    assert all(s.finish_reason == "length" and len(s.output) == 2 for s in fin)
+    assert bm.num_free() == 10
+
+
+def test_prompt_larger_than_the_whole_pool_is_finished_not_spun():
+    bm = make_block_manager(5, 4)                               # 16 tokens of KV
+    sch = Scheduler(bm, num_slots=1, max_batch=4, max_prefill_tokens=8, max_seq_len=64)
+    sch.MIN_CHUNK = 4
+    s = _seq(30, 2)
+    sch.add(s)
+    for _ in range(4):
+        st = sch.schedule(0)
+        if st is None:
+            break
+        sch.complete(st, [0])
+    assert s.finish_reason == "kv_capacity" and not sch.has_work() and bm.num_free() == 4
+
+
+def test_master_plans_carry_the_unit_group(monkeypatch):
+    """a sub-layer (group 5) plan set on the master must reach the workers with its
+    group, or they would read atom ranges as half-layer units."""
+    m = _master_with([0, 0], model="synthetic:gpt2-small", shards=2)
+    m.assign_shards()
+    plans = m._plans()
+    assert all(p["unit_group"] == 2 for p in plans)
+    monkeypatch.setenv("DLLM_PP_UNITS", "5:0,31;31,60")
+    plans = m._plans()
+    assert [p["unit_group"] for p in plans] == [5, 5]
+    assert [p["unit_range"] for p in plans] == [[0, 31], [31, 60]]
+    assert [p["layer_range"] for p in plans] == [[0, 7], [6, 12]]
