@@ -49,8 +49,18 @@ def checkpoint_files(model_path: str) -> List[str]:
     raise FileNotFoundError(f"no checkpoint (model.safetensors[.index.json] / pytorch_model.bin) in {model_path}")
 
 
+def _load_bin(path: str) -> Dict[str, torch.Tensor]:
+    """A ``.bin`` checkpoint, memory-mapped where the file is a zip archive (tensors are paged in
+    when touched, never unpickled objects: weights_only)."""
+    try:
+        return torch.load(path, map_location="cpu", weights_only=True, mmap=True)
+    except RuntimeError:            # legacy (non-zip) torch.save format cannot be mmapped
+        return torch.load(path, map_location="cpu", weights_only=True)
+
+
 def iter_checkpoint(model_path: str, keys: Optional[set] = None) -> Iterable[Tuple[str, torch.Tensor]]:
-    """Yield (name, tensor); safetensors files are read lazily, key by key."""
+    """Yield (name, tensor); safetensors files are read lazily, key by key, and ``.bin`` files
+    memory-mapped -- a file whose keys are all outside ``keys`` is not read at all."""
     for f in checkpoint_files(model_path):
         if f.endswith(".safetensors"):
             from safetensors import safe_open
@@ -59,22 +69,40 @@ def iter_checkpoint(model_path: str, keys: Optional[set] = None) -> Iterable[Tup
                     if keys is None or k in keys:
                         yield k, sf.get_tensor(k)
         else:
-            sd = torch.load(f, map_location="cpu", weights_only=True)
+            sd = _load_bin(f)
             for k, v in sd.items():
                 if keys is None or k in keys:
                     yield k, v
+            del sd
 
 
-def checkpoint_keys(model_path: str) -> List[str]:
-    out = []
+def checkpoint_index(model_path: str) -> Dict[str, Tuple[str, int]]:
+    """name -> (file, bytes) without materialising any tensor (safetensors headers; mmapped .bin)."""
+    out: Dict[str, Tuple[str, int]] = {}
     for f in checkpoint_files(model_path):
         if f.endswith(".safetensors"):
             from safetensors import safe_open
             with safe_open(f, framework="pt") as sf:
-                out.extend(sf.keys())
+                for k in sf.keys():
+                    sl = sf.get_slice(k)
+                    n = 1
+                    for d in sl.get_shape():
+                        n *= int(d)
+                    out[k] = (f, n * _DTYPE_BYTES.get(sl.get_dtype(), 4))
         else:
-            out.extend(torch.load(f, map_location="cpu", weights_only=True).keys())
+            sd = _load_bin(f)
+            for k, v in sd.items():
+                out[k] = (f, v.numel() * v.element_size())
+            del sd
     return out
+
+
+_DTYPE_BYTES = {"F64": 8, "F32": 4, "F16": 2, "BF16": 2, "I64": 8, "I32": 4, "I16": 2, "I8": 1, "U8": 1,
+                "BOOL": 1, "F8_E4M3": 1, "F8_E5M2": 1}
+
+
+def checkpoint_keys(model_path: str) -> List[str]:
+    return list(checkpoint_index(model_path))
 
 
 def load_shard_file(path: str) -> Dict[str, torch.Tensor]:
@@ -127,6 +155,11 @@ class ModelShardManager:
             return json.load(f)
 
     def shard_model(self, write_safetensors: bool = False, checksums: bool = True) -> str:
+        """Write ``shards/`` one shard at a time: the key -> stage assignment comes from the
+        checkpoint index (no tensor read), then each shard's tensors are read (safetensors: per
+        key; ``.bin``: memory-mapped), written and dropped before the next shard is read.  Peak host
+        memory is about one shard -- a 141 GB Llama-3-70B checkpoint shards on a host with far less
+        RAM (the reference's shard_model held the whole state dict, src/model/shard_manager.py:17-61)."""
         hf = self._hf_config()
         cfg = self.config or ModelConfig.from_hf_config(hf)
         n = min(self.num_shards, cfg.num_layers)
@@ -134,18 +167,22 @@ class ModelShardManager:
             raise ValueError(f"{self.num_shards} shards > {cfg.num_layers} layers")
         self.plan = plan_stages(cfg, n)
         os.makedirs(self.shard_dir, exist_ok=True)
-        shards: List[Dict[str, torch.Tensor]] = [dict() for _ in range(n)]
+        index = checkpoint_index(self.model_path)
         tied = cfg.tie_embeddings
-        for k, v in iter_checkpoint(self.model_path):
+        members: List[List[str]] = [[] for _ in range(n)]
+        for k in index:
             if k == "lm_head.weight" and tied:
                 continue          # tied head == embedding (GPT-2 style); the last stage re-uses it
-            shards[assign_key(k, self.plan, cfg.num_layers)][k] = v
+            members[assign_key(k, self.plan, cfg.num_layers)].append(k)
         if tied and n > 1:
             emb = W.hf_embed_names(cfg)["embed"]
-            if emb in shards[0]:
-                shards[-1][emb] = shards[0][emb]
+            if emb in index:
+                members[-1].append(emb)
         sizes, sums = [], {}
-        for i, sd in enumerate(shards):
+        for i, keys in enumerate(members):
+            want = set(keys)
+            sd = {k: v for k, v in iter_checkpoint(self.model_path, want)}
+            sd = {k: sd[k] for k in keys if k in sd}         # checkpoint order within the shard
             path = os.path.join(self.shard_dir, f"shard_{i}.pt")
             torch.save(sd, path)
             if write_safetensors:
@@ -154,6 +191,7 @@ class ModelShardManager:
                           os.path.join(self.shard_dir, f"shard_{i}.safetensors"))
             self.shard_info[i] = list(sd.keys())
             sizes.append(sum(t.numel() * t.element_size() for t in sd.values()))
+            del sd
             if checksums:
                 sums[f"shard_{i}.pt"] = _sha256(path)
         with open(os.path.join(self.shard_dir, "shard_info.json"), "w") as f:

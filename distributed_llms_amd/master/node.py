@@ -53,11 +53,14 @@ def _free_port() -> int:
 
 class MasterNode:
     def __init__(self, host: str = "0.0.0.0", port: int = 65432, config: Optional[EngineConfig] = None,
-                 auto_recover: bool = False):
+                 auto_recover: bool = False, max_retries: Optional[int] = None):
         self.host = host
         self.port = port
         self.config = config or EngineConfig()
         self.auto_recover = auto_recover
+        # in-flight requests of a failed pipeline are re-run from their prompts after recovery, at
+        # most this many times each (reference intent: retry + state recovery, plan.md:430-436)
+        self.max_retries = (3 if auto_recover else 0) if max_retries is None else max_retries
         self.workers: Dict[str, Dict[str, Any]] = {}
         self.model_path: Optional[str] = None
         self.model_spec: Optional[str] = None
@@ -75,6 +78,8 @@ class MasterNode:
         self._lock = threading.RLock()
         self._ids = itertools.count()
         self._tasks: Dict[str, cf.Future] = {}
+        self._reqs: Dict[str, Dict[str, Any]] = {}       # task_id -> prompt / params / attempts (for retry)
+        self._retry: List[Dict[str, Any]] = []           # requests parked while the pipeline recovers
         self._streams: Dict[str, "queue.Queue"] = {}     # task_id -> (offset, new ids) chunks, None = done
         self._acks: Dict[str, cf.Future] = {}
         self._status_futs: Dict[str, cf.Future] = {}
@@ -179,7 +184,9 @@ class MasterNode:
             if q is not None:
                 q.put((int(header.get("offset", 0)), unpack_ids(payload)))
         elif command == "RESULT":
-            fut = self._tasks.pop(header.get("task_id"), None)
+            with self._lock:
+                fut = self._tasks.pop(header.get("task_id"), None)
+                self._reqs.pop(header.get("task_id"), None)
             if fut and not fut.done():
                 fut.set_result((header, unpack_ids(payload)))
             q = self._streams.get(header.get("task_id"))
@@ -191,7 +198,9 @@ class MasterNode:
                 fut.set_result(header.get("status"))
         elif command == "ERROR":
             log.error("worker %s error: %s", worker_id, header.get("error"))
-            fut = self._tasks.pop(header.get("task_id"), None) if header.get("task_id") else None
+            with self._lock:
+                fut = self._tasks.pop(header.get("task_id"), None) if header.get("task_id") else None
+                self._reqs.pop(header.get("task_id"), None)
             if fut and not fut.done():
                 fut.set_exception(RuntimeError(header.get("error")))
             ack = self._acks.get(worker_id)
@@ -218,7 +227,11 @@ class MasterNode:
                 ack.set_exception(WorkerFailure(f"{worker_id} {reason}"))
             if in_plan and self.state == "ready":
                 self.state = "degraded"
-                self._fail_all(WorkerFailure(f"pipeline stage worker {worker_id} {reason}"))
+                exc = WorkerFailure(f"pipeline stage worker {worker_id} {reason}")
+                if self.auto_recover and self.max_retries > 0:
+                    self._park_inflight(exc)
+                else:
+                    self._fail_all(exc)
                 # tear the surviving stages down: their RCCL group lost a member
                 for wid in self.stage_workers:
                     ww = self.workers.get(wid)
@@ -228,12 +241,50 @@ class MasterNode:
                     threading.Thread(target=self._recover_when_possible, daemon=True).start()
 
     def _fail_all(self, exc: Exception):
-        for tid, fut in list(self._tasks.items()):
+        with self._lock:
+            tasks, self._tasks = self._tasks, {}
+            self._reqs.clear()
+            parked, self._retry = self._retry, []
+            streams = list(self._streams.values())
+        for fut in list(tasks.values()) + [r["future"] for r in parked]:
             if not fut.done():
                 fut.set_exception(exc)
-        self._tasks.clear()
-        for q in list(self._streams.values()):
+        for q in streams:
             q.put(None)                               # streams end; their futures carry the error
+
+    def _park_inflight(self, exc: Exception):
+        """The pipeline lost a stage: keep every in-flight request's future pending and park it
+        for re-submission once the pipeline is back (requests out of retries fail now)."""
+        with self._lock:
+            tasks, self._tasks = self._tasks, {}
+            reqs, self._reqs = self._reqs, {}
+            fail = []
+            for tid, fut in tasks.items():
+                r = reqs.get(tid)
+                if fut.done():
+                    continue
+                if r is None or r["attempts"] >= self.max_retries:
+                    fail.append(fut)
+                    continue
+                r["future"] = fut
+                r["stream"] = self._streams.pop(tid, None)
+                self._retry.append(r)
+        for fut in fail:
+            fut.set_exception(exc)
+        log.warning("%d in-flight requests parked for retry, %d failed", len(self._retry), len(fail))
+
+    def _resubmit_parked(self):
+        with self._lock:
+            parked, self._retry = self._retry, []
+        for r in parked:
+            r["attempts"] += 1
+            try:
+                self._send_request(r["ids"], r["params"], r["future"], r["stream"], r["hint"], r["attempts"])
+            except WorkerFailure as e:
+                if not r["future"].done():
+                    r["future"].set_exception(e)
+        if parked:
+            log.info("re-submitted %d requests after recovery", len(parked))
 
     def _monitor(self):
         """Heartbeat-timeout eviction (the reference records last_heartbeat and never reads it, D15)."""
@@ -402,7 +453,10 @@ class MasterNode:
         return acks
 
     def _recover_when_possible(self, timeout: float = 600.0):
+        """Re-admit a full set of stage workers (waits for replacements), reload the plan, then
+        re-run the parked requests from their prompts.  Failed attempts back off exponentially."""
         t_end = time.time() + timeout
+        backoff = 0.5
         while self.running and time.time() < t_end and self.state == "degraded":
             with self._lock:
                 have = len(self.workers)
@@ -412,35 +466,49 @@ class MasterNode:
                     self.assign_shards()
                     self.distribute_shards()
                     log.info("pipeline recovered")
+                    self._resubmit_parked()
                     return
                 except Exception as e:
-                    log.error("recovery attempt failed: %s", e)
-            time.sleep(1.0)
+                    log.error("recovery attempt failed: %s (next in %.1fs)", e, backoff)
+                    time.sleep(backoff)
+                    backoff = min(30.0, backoff * 2)
+                    continue
+            time.sleep(0.5)
+        if self.state != "ready":
+            self._fail_all(WorkerFailure("pipeline did not recover"))
 
     # ---------------------------------------------------------------- inference
     def submit(self, prompt_ids: Sequence[int], params: Optional[Dict[str, Any]] = None, _stream_queue=None,
                _task_out=None) -> cf.Future:
         if self.state != "ready":
             raise WorkerFailure(f"pipeline not ready (state={self.state})")
-        task_id = f"task_{next(self._ids)}_{int(time.time() * 1000)}"
         fut: cf.Future = cf.Future()
         fut.t_submit = time.perf_counter()
-        fut.task_id = task_id
-        self._tasks[task_id] = fut
-        if _stream_queue is not None:
-            self._streams[task_id] = _stream_queue
-            _task_out["task_id"] = task_id
-        with self._lock:
-            w0 = self.workers.get(self.stage_workers[0])
-        if w0 is None:
-            self._tasks.pop(task_id, None)
-            raise WorkerFailure("stage-0 worker is gone")
-        ok = self.proto.send_message(w0["socket"], "RUN_INFERENCE", payload=pack_ids(prompt_ids),
-                                     metadata={"task_id": task_id, "params": params or {}})
-        if not ok:
-            self._tasks.pop(task_id, None)
-            raise WorkerFailure("cannot send request to stage 0")
+        self._send_request(list(prompt_ids), dict(params or {}), fut, _stream_queue, _task_out, 0)
         return fut
+
+    def _send_request(self, ids: List[int], params: Dict[str, Any], fut: cf.Future, stream_q, hint, attempts: int):
+        """Register ``fut`` under a fresh task id and send the prompt to stage 0 (first try or a
+        retry after recovery: a retry streams from offset 0 again and the stream consumer skips
+        what it already yielded)."""
+        task_id = f"task_{next(self._ids)}_{int(time.time() * 1000)}"
+        fut.task_id = task_id
+        with self._lock:
+            self._tasks[task_id] = fut
+            self._reqs[task_id] = {"ids": ids, "params": params, "attempts": attempts, "hint": hint}
+            if stream_q is not None:
+                self._streams[task_id] = stream_q
+                if hint is not None:
+                    hint["task_id"] = task_id
+            w0 = self.workers.get(self.stage_workers[0]) if self.stage_workers else None
+        ok = w0 is not None and self.proto.send_message(w0["socket"], "RUN_INFERENCE", payload=pack_ids(ids),
+                                                        metadata={"task_id": task_id, "params": params})
+        if not ok:
+            with self._lock:
+                self._tasks.pop(task_id, None)
+                self._reqs.pop(task_id, None)
+                self._streams.pop(task_id, None)
+            raise WorkerFailure("stage-0 worker is gone" if w0 is None else "cannot send request to stage 0")
 
     def stream(self, prompt_ids: Sequence[int], timeout: float = 600, **params):
         """Generate with token streaming: yields lists of new token ids as stage 0 produces them

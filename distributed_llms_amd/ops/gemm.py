@@ -314,6 +314,42 @@ def linear_big(x: torch.Tensor, w: torch.Tensor, splits: int = 2, swiglu: bool =
     return y
 
 
+def pp_splits(m: int, n: int, k: int, bn: int = 256, target_wgs: int = 256) -> int:
+    """K slices for gemm_pp: about one workgroup per CU (tiles x slices <= target), >= 4 K-steps
+    (128) per slice."""
+    tiles = (n // bn) * (-(-m // 256))
+    return max(1, min(target_wgs // max(1, tiles), (k // 32) // 4, 32))
+
+
+def linear_pp(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = False, defer: bool = False,
+              variant: int = 0):
+    """Ping-pong 256-row-tile GEMM (csrc/kernels/gemm_pp.hip).  ``variant``: bit 0 = 128-column tile
+    (else 256), bit 1 = weights nontemporal, bit 2 = grouped row-tile order (large M).  Split-K
+    partials are reduced by splitk_reduce(_swiglu), or returned as a :class:`SplitKPartial` with
+    ``defer`` (no SwiGLU)."""
+    k = x.shape[-1]
+    n = w.shape[0]
+    m = x.numel() // k
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        raise ValueError("linear_pp: bf16 contiguous operands")
+    bn = 128 if variant & 1 else 256
+    if n % bn or k % 32:
+        raise ValueError(f"linear_pp: N % {bn} and K % 32")
+    s = splits or pp_splits(m, n, k, bn)
+    ws = _workspace(x.device)
+    if s > 1 and s * m * n > ws.numel():
+        s = max(1, ws.numel() // (m * n))
+    stream = torch.cuda.current_stream().cuda_stream
+    if defer and not swiglu and s > 1:
+        se = _ext.kernels().gemm_pp(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, variant,
+                                    stream)
+        return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
+    y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
+    _ext.kernels().gemm_pp(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s,
+                           1 if swiglu else 0, variant, stream)
+    return y
+
+
 # 256 x 256-tile decode GEMM (gemm_sq.hip) for 128 < M <= 256: a third fewer staged bytes per FLOP
 # than the wide kernel's 256 x 128 tile.  Measured (profiles/wide_gemm.md, "256 x 256 tile"): it
 # wins only where the grid needs no K split -- the LM head (1.05x) and the 70B MLP gate|up (1.07x);

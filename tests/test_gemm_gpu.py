@@ -344,3 +344,55 @@ def test_big_linear(cuda, m, n, k, splits, swiglu):
         g, u = ref.chunk(2, -1)
         ref = F.silu(g) * u
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+# ---- gemm_pp: ping-pong 256-row-tile kernel (decode split-K, prefill grouped + SwiGLU)
+@pytest.mark.parametrize("m", [1, 77, 200, 256, 300, 777])
+@pytest.mark.parametrize("n,k,splits", [(6144, 4096, 1), (6144, 4096, 10), (4096, 14336, 16), (512, 96, 3)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4])
+def test_pp_linear(cuda, m, n, k, splits, variant):
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear_pp(x, w, splits=splits, variant=variant)
+    ref = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [64, 256, 1000])
+@pytest.mark.parametrize("inter,k,splits", [(14336, 4096, 1), (14336, 4096, 2), (384, 256, 1)])
+@pytest.mark.parametrize("variant", [0, 1, 4])
+def test_pp_swiglu(cuda, m, inter, k, splits, variant):
+    if variant & 1 == 0 and (2 * inter) % 256:
+        pytest.skip("256-column tile needs 2I % 256 == 0")
+    x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
+    y = gemm.linear_pp(x, w, splits=splits, swiglu=True, variant=variant)
+    gu = x.float() @ w.float().t()
+    ref = F.silu(gu[:, :inter]) * gu[:, inter:]
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+def test_pp_deferred_splitk_matches_materialized_and_wide(cuda):
+    x, w = _bf(256, 14336), _bf(4096, 14336, scale=0.05)
+    p = gemm.linear_pp(x, w, splits=16, defer=True)
+    assert isinstance(p, gemm.SplitKPartial) and p.splits == 16
+    y = p.materialize()
+    ref = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+    # the slabs feed the fused add + RMSNorm exactly as gemm_wide's do
+    res = _bf(256, 4096)
+    g = _bf(4096)
+    a, ra = ops.fused_add_rms_norm(gemm.linear_pp(x, w, splits=16, defer=True), res.clone(), g, 1e-5)
+    b, rb = ops.fused_add_rms_norm(y, res.clone(), g, 1e-5)
+    torch.testing.assert_close(ra.float(), rb.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(a.float(), b.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_pp_graph_replay_and_determinism(cuda):
+    x, w = _bf(256, 4096), _bf(6144, 4096, scale=0.05)
+    y0 = gemm.linear_pp(x, w, splits=10)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = gemm.linear_pp(x, w, splits=10)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
