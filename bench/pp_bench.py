@@ -69,7 +69,7 @@ def decode_impls(x, n, k, sw, role):
         if n % bn:
             continue
         base = gemm.pp_splits(m, n, k, bn)
-        for s in sorted({max(1, base // 2), base, min(32, base * 2)} | ({1, 2} if sw else set())):
+        for s in sorted({max(1, base // 2), base} | ({1, 2} if sw else set())):
             for nt in (0, 2):
                 v = vb | nt
 
@@ -116,11 +116,12 @@ def main():
                 continue
             w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
             x = torch.randn(T, k, device="cuda").to(torch.bfloat16)
-            impls = {
-                "blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w)),
-                "pp": lambda w: gemm.linear_pp(x, w, splits=1, swiglu=sw, variant=4),
-                "pp_nogrp": lambda w: gemm.linear_pp(x, w, splits=1, swiglu=sw, variant=0),
-            }
+            impls = {"blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w))}
+            for bn, vb in ((256, 0), (128, 1)):
+                for grp in (0, 4):
+                    v = vb | grp
+                    impls[f"pp{bn}{'g' if grp else ''}"] = (lambda w, v=v: gemm.linear_pp(x, w, splits=1, swiglu=sw,
+                                                                                           variant=v))
             graphs = {key: graph_of(f, [w], 2) for key, f in impls.items()}
             res = {key: [] for key in graphs}
             for _ in range(a.rounds):
@@ -128,8 +129,8 @@ def main():
                     res[key].append(timeit(g.replay, max(3, a.iters // 2)) / 2)
             t = {key: min(v) * 1e6 for key, v in res.items()}
             fl = 2.0 * T * n * k
-            print(f"prefill {name:8s} T={T:6d} " + " ".join(f"{key} {v:8.1f} us ({fl / v / 1e6:5.0f} TF)"
-                                                           for key, v in t.items()), flush=True)
+            print(f"prefill {name:8s} T={T:6d} " + " ".join(f"{key} {fl / v / 1e6:5.0f}"
+                                                           for key, v in t.items()) + " TF", flush=True)
             del graphs, x, w
             torch.cuda.empty_cache()
 

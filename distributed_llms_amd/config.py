@@ -237,6 +237,11 @@ class EngineConfig:
     num_kv_blocks: int = 0             # 0 -> derive from kv_cache_fraction
     use_graphs: bool = True            # HIP-graph capture of the decode step
     quant: str = "none"                # "fp8": W8A8 e4m3 dense projections (ops/quant.py)
+    # pipeline activation transport between GPU stages: "auto" (= "rccl" on GPUs), "rccl" (native
+    # RCCL p2p, one communicator per edge, static rings), "torch" (torch.distributed's RCCL group),
+    # "ipc" (HIP-IPC peer writes); CPU stages always use torch.distributed (gloo)
+    transport: str = "auto"
+    comm_timeout_s: float = 600.0      # a pipeline peer silent this long -> the rank raises (no hang)
     graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
     host: str = "0.0.0.0"
     port: int = 65432
@@ -257,6 +262,10 @@ class EngineConfig:
             raise ValueError("kv_block_size must be 16, 32 or 64")
         if self.quant not in ("none", "fp8"):
             raise ValueError(f"quant {self.quant!r} (none, fp8)")
+        if self.transport not in ("auto", "rccl", "torch", "ipc"):
+            raise ValueError(f"transport {self.transport!r} (auto, rccl, torch, ipc)")
+        if self.comm_timeout_s <= 0:
+            raise ValueError("comm_timeout_s must be > 0")
         if self.max_batch < 1 or self.max_seq_len < 2:
             raise ValueError("max_batch/max_seq_len")
         cfg = get_model_config(self.model if self.shard_dir is None else self.shard_dir)

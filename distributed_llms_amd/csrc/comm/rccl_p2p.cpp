@@ -14,10 +14,12 @@
 #include <pybind11/pybind11.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 namespace py = pybind11;
 
@@ -40,14 +42,25 @@ py::bytes unique_id() {
 
 class RcclComm {
  public:
-  RcclComm(int nranks, int rank, const std::string& uid, int device) : nranks_(nranks), rank_(rank) {
+  // timeout_s > 0: a NON-BLOCKING communicator -- init and every enqueue that returns
+  // ncclInProgress (lazy p2p connection setup) are polled against the deadline, and a peer that
+  // never shows up aborts the communicator and raises instead of hanging the rank forever.
+  RcclComm(int nranks, int rank, const std::string& uid, int device, double timeout_s)
+      : nranks_(nranks), rank_(rank), timeout_s_(timeout_s) {
     if (uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("unique id must be 128 bytes");
     if (rank < 0 || rank >= nranks) throw std::invalid_argument("rank out of range");
     ncclUniqueId id;
     std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
     hip_check(hipSetDevice(device), "hipSetDevice");
     py::gil_scoped_release nogil;   // init rendezvous blocks until every rank joins
-    check(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+    if (timeout_s_ > 0) {
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      cfg.blocking = 0;
+      check(ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg), "ncclCommInitRankConfig");
+      settle("ncclCommInitRank");
+    } else {
+      check(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+    }
   }
   ~RcclComm() {
     if (comm_) ncclCommDestroy(comm_);
@@ -55,24 +68,37 @@ class RcclComm {
 
   void send(uintptr_t ptr, long nbytes, int peer, uintptr_t stream) {
     live();
-    check(ncclSend(reinterpret_cast<const void*>(ptr), (size_t)nbytes, ncclUint8, peer, comm_,
-                   reinterpret_cast<hipStream_t>(stream)), "ncclSend");
+    enqueue(ncclSend(reinterpret_cast<const void*>(ptr), (size_t)nbytes, ncclUint8, peer, comm_,
+                     reinterpret_cast<hipStream_t>(stream)), "ncclSend");
   }
   void recv(uintptr_t ptr, long nbytes, int peer, uintptr_t stream) {
     live();
-    check(ncclRecv(reinterpret_cast<void*>(ptr), (size_t)nbytes, ncclUint8, peer, comm_,
-                   reinterpret_cast<hipStream_t>(stream)), "ncclRecv");
+    enqueue(ncclRecv(reinterpret_cast<void*>(ptr), (size_t)nbytes, ncclUint8, peer, comm_,
+                     reinterpret_cast<hipStream_t>(stream)), "ncclRecv");
   }
-  // fused exchange (both directions in one group: no ordering deadlock between the two)
+  // fused exchange (both directions in one group: no ordering deadlock between the two; also the
+  // only legal form of a send to self)
   void sendrecv(uintptr_t sptr, long sbytes, int speer, uintptr_t rptr, long rbytes, int rpeer, uintptr_t stream) {
     live();
     check(ncclGroupStart(), "ncclGroupStart");
-    send(sptr, sbytes, speer, stream);
-    recv(rptr, rbytes, rpeer, stream);
-    check(ncclGroupEnd(), "ncclGroupEnd");
+    check(ncclSend(reinterpret_cast<const void*>(sptr), (size_t)sbytes, ncclUint8, speer, comm_,
+                   reinterpret_cast<hipStream_t>(stream)), "ncclSend");
+    check(ncclRecv(reinterpret_cast<void*>(rptr), (size_t)rbytes, ncclUint8, rpeer, comm_,
+                   reinterpret_cast<hipStream_t>(stream)), "ncclRecv");
+    enqueue(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  // the communicator's asynchronous error state: "" (healthy), "in_progress", or the error text
+  std::string status() const {
+    if (!comm_) return "aborted";
+    ncclResult_t r = ncclSuccess;
+    ncclCommGetAsyncError(comm_, &r);
+    if (r == ncclSuccess) return "";
+    if (r == ncclInProgress) return "in_progress";
+    return ncclGetErrorString(r);
   }
   void abort() {
     if (comm_) {
+      py::gil_scoped_release nogil;
       ncclCommAbort(comm_);
       comm_ = nullptr;
     }
@@ -91,8 +117,34 @@ class RcclComm {
   void live() const {
     if (!comm_) throw std::runtime_error("RCCL communicator was aborted/destroyed");
   }
+  void enqueue(ncclResult_t r, const char* what) {
+    check(r, what);
+    if (r == ncclInProgress || timeout_s_ > 0) settle(what);
+  }
+  // poll a non-blocking communicator until its last call finished; abort + raise at the deadline
+  void settle(const char* what) {
+    if (timeout_s_ <= 0) return;
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s_);
+    for (;;) {
+      ncclResult_t r = ncclSuccess;
+      ncclCommGetAsyncError(comm_, &r);
+      if (r == ncclSuccess) return;
+      if (r != ncclInProgress) {
+        ncclCommAbort(comm_);
+        comm_ = nullptr;
+        throw std::runtime_error(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(r));
+      }
+      if (std::chrono::steady_clock::now() > t_end) {
+        ncclCommAbort(comm_);
+        comm_ = nullptr;
+        throw std::runtime_error(std::string("RCCL ") + what + ": peer did not respond within the timeout");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
   ncclComm_t comm_ = nullptr;
   int nranks_, rank_;
+  double timeout_s_;
 };
 
 }  // namespace
@@ -109,12 +161,13 @@ PYBIND11_MODULE(_C_rccl, m) {
     return v;
   });
   py::class_<RcclComm>(m, "RcclComm")
-      .def(py::init<int, int, const std::string&, int>(), py::arg("nranks"), py::arg("rank"), py::arg("uid"),
-           py::arg("device"))
+      .def(py::init<int, int, const std::string&, int, double>(), py::arg("nranks"), py::arg("rank"), py::arg("uid"),
+           py::arg("device"), py::arg("timeout_s") = 0.0)
       .def("send", &RcclComm::send, py::arg("ptr"), py::arg("nbytes"), py::arg("peer"), py::arg("stream"))
       .def("recv", &RcclComm::recv, py::arg("ptr"), py::arg("nbytes"), py::arg("peer"), py::arg("stream"))
       .def("sendrecv", &RcclComm::sendrecv)
       .def("abort", &RcclComm::abort)
+      .def("status", &RcclComm::status)
       .def("destroy", &RcclComm::destroy)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("nranks", &RcclComm::nranks)

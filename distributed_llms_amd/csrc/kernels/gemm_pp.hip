@@ -1,26 +1,25 @@
-// Ping-pong MFMA GEMM for 256-row tiles: C[M,N] = A[M,K] . B[N,K]^T, bf16 in, f32 accumulate.
-// Serves the decode projections at batch 129..256 (one row tile, split-K over workgroups) and the
-// prefill projections (M = tokens, grouped row-tile order, SwiGLU fused into the epilogue).
+// 4-wave software-pipelined MFMA GEMM for 256-row tiles: C[M,N] = A[M,K] . B[N,K]^T, bf16 in, f32
+// accumulate.  Serves the decode projections at batch 129..256 (one row tile, split-K over
+// workgroups) and the prefill projections (M = tokens, grouped row-tile order, SwiGLU fused into
+// the epilogue).
 //
-// Why (profiles/round3_decode_gemms.md): the 256 x 128 / 3-buffer kernel (gemm_wide.hip) runs
-// all 8 waves in lock step -- one barrier per 64-deep K-tile, every wave of a SIMD reading its
-// fragments at the same moment -- so its MFMA phase alone reaches ~55 % of peak, and its split-K
-// epilogue stores one 2-byte element per lane (4 x 32-byte segments per store instruction).
-//
-// Structure (gfx950, wave64, 512 threads = 8 waves):
-//  * tile 256 x BN (BN = 256: waves 2 (M) x 4 (N), wave tile 128 x 64; BN = 128: 4 x 2, 64 x 64),
-//    v_mfma_f32_16x16x32_bf16, 16 independent accumulators per phase;
-//  * K advances in 32-deep K-steps held in an LDS ring of NS slots (BN 256: 5 x 32 KiB, BN 128:
-//    6 x 24 KiB, 160 / 144 KiB): slot = A [256][64 B] + B [BN][64 B] filled by
-//    global_load_lds_dwordx4 (1 KiB = 16 rows per wave-instruction), the 16-byte chunk swizzle
-//    c ^ ((row >> 1) & 3) on the per-lane SOURCE address and on the fragment read (conflict-free
-//    ds_read_b128 for the 16 x 16 x 32 operand pattern on 64-byte rows; rule 21);
-//  * NS - 1 K-steps in flight (96 KiB per CU), COUNTED s_waitcnt vmcnt(N) once per K-step, raw
-//    s_barrier (never __syncthreads, which would drain the LDS-DMA queue);
-//  * ping-pong: each K-step is P = rows / 64 phases of {fragment reads + staging issue | barrier |
-//    16 MFMAs | barrier}; waves 4-7 (one per SIMD) start one barrier late, so on every SIMD one
-//    wave's fragment reads and LDS-DMA issue run beside its partner's MFMA burst
-//    (MI355X_MICROARCH "Two waves per SIMD", cdna_hip_programming §5 8-phase template);
+// Why this shape (profiles/round3_gemm_counters.md): hipBLASLt's 256 x 256 kernel keeps the MFMA
+// pipe ~82 % busy with ONE wave per SIMD and a 128 x 128 wave tile, while 8-wave designs that
+// synchronise twice per 16-MFMA phase (the 2-waves-per-SIMD ping-pong this file first held, the
+// lock-step gemm_wide) reach ~62 %: a workgroup barrier every 256 MFMA cycles costs more than the
+// partner wave hides.  Here:
+//  * tile 256 x BN, 4 waves as 2 x 2, wave tile 128 x BN/2 (8 x 8 or 8 x 4 accumulators of
+//    v_mfma_f32_16x16x32_bf16: up to 256 accumulator registers, one wave per SIMD);
+//  * 64-deep K-tiles in an LDS ring (BN 256: 2 x 64 KiB, BN 128: 3 x 48 KiB), filled by
+//    global_load_lds_dwordx4 in full 128-byte rows (8 rows per wave-instruction), the 16-byte
+//    chunk swizzle c ^ ((row >> 1) & 7) on the per-lane SOURCE address and on the fragment read
+//    (conflict-free ds_read_b128; rule 21);
+//  * ONE barrier per K-tile, in its middle: K-half 0's MFMAs run while K-half 1's fragments are
+//    read; at the barrier every read of the tile is done and the next tile has landed (counted
+//    vmcnt, never 0 in the loop at BN 128); K-half 1's MFMAs run while the next tile's K-half 0 is
+//    read and the tile NB ahead is staged into the slot just freed -- fragment reads and LDS-DMA
+//    pieces interleave with the MFMAs in program order (sched_barrier), so the wave's own MFMA
+//    stream covers their latency;
 //  * operands swapped in the MFMA (B fragment first), so a lane's accumulator holds 4 CONSECUTIVE
 //    output columns of one row: the epilogue packs them 8 bytes at a time into an LDS image of the
 //    output tile (padded rows, conflict-free), then every lane stores 16-byte row chunks --
@@ -30,14 +29,17 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <type_traits>
+#include <utility>
+
 namespace dllm {
 
 namespace {
-constexpr int PBK = 32;                       // K per ring slot (64-byte rows)
+constexpr int PBK = 64;                       // K per ring slot (128-byte rows)
 typedef __attribute__((address_space(3))) void* lds_vptr_p;
 typedef __attribute__((address_space(1))) void* glb_vptr_p;
 
-__device__ __forceinline__ int pswz(int row, int chunk) { return chunk ^ ((row >> 1) & 3); }
+__device__ __forceinline__ int pswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
 template <int OFF>
 __device__ __forceinline__ bf16x8 pp_frag(uint32_t addr) {
@@ -46,25 +48,85 @@ __device__ __forceinline__ bf16x8 pp_frag(uint32_t addr) {
   return r;
 }
 
+// fragment read at an LDS byte address, in inline asm: hipcc does not count it, so the only waits
+// are the counted ones of PpSched (its own waitcnt insertion falls back to lgkmcnt(0) at the loop
+// head and before every MFMA that uses a read from the previous iteration)
+__device__ __forceinline__ bf16x8 pp_frag_dyn(uint32_t addr) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+
 #define PP_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 // wait until at most `younger` K-steps of G LDS-DMA instructions each are still in flight
 template <int G>
-__device__ __forceinline__ void pp_wait(int younger) {
-  static_assert(G == 3 || G == 4, "G");
-  if constexpr (G == 4) {
-    if (younger <= 0) PP_VM(0);
-    else if (younger == 1) PP_VM(4);
-    else if (younger == 2) PP_VM(8);
-    else PP_VM(12);
-  } else {
-    if (younger <= 0) PP_VM(0);
-    else if (younger == 1) PP_VM(3);
-    else if (younger == 2) PP_VM(6);
-    else if (younger == 3) PP_VM(9);
-    else PP_VM(12);
-  }
+__device__ __forceinline__ void pp_wait_n(int younger) {   // younger: compile-time after inlining
+  static_assert(G == 12 || G == 16, "G");
+  if (younger <= 0) PP_VM(0);
+  else if constexpr (G == 12) { if (younger == 1) PP_VM(12); else PP_VM(24); }
+  else { if (younger == 1) PP_VM(16); else PP_VM(32); }
 }
 #undef PP_VM
+
+// f(integral_constant<int, i>) for i = 0 .. N-1, each i a constant expression
+template <int... I, class F>
+__device__ __forceinline__ void pp_static_for_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void pp_static_for(F&& f) {
+  pp_static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+// s_waitcnt lgkmcnt(N) for a compile-time N (16 = no wait); a sched_barrier keeps hipcc from
+// hoisting register-only MFMAs above an inline-asm wait (guide rule 18)
+template <int N>
+__device__ __forceinline__ void pp_lgkm() {
+  static_assert(N >= 0 && N <= 16, "lgkmcnt");
+  if constexpr (N < 16) {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Fragment-read schedule of one K-half (RT A-fragments, CT B-fragments; MFMA i uses A r = i / CT,
+// B c = i % CT).  The reads for the OTHER K-half go out after MFMA pos(): A fragment a right after
+// its register's last MFMA in this K-half (a * CT + CT - 1), B fragment b spread over the first
+// half of the stream; in K-half 1 nothing before the barrier at EB - 1.  wait_before(h, i): the
+// lgkmcnt that makes MFMA i of K-half h wait for exactly its operands' reads (issued during the
+// previous K-half), counting the younger reads of that K-half and this K-half's reads so far.
+template <int RT, int CT>
+struct PpSched {
+  static constexpr int NMF = RT * CT, EB = CT, BE = (NMF / 2) / CT > 0 ? (NMF / 2) / CT : 1;
+  static constexpr int pos(int half, int kind, int k) {
+    if (kind == 0) return k * CT + CT - 1 > (half ? EB - 1 : -1) ? k * CT + CT - 1 : EB - 1;
+    return half == 0 ? k * BE : EB - 1 + k * BE;
+  }
+  static constexpr int key(int half, int kind, int k) { return pos(half, kind, k) * 64 + kind * 32 + k; }
+  static constexpr int younger(int half, int kind, int k) {   // reads of `half` issued after (kind, k)
+    int n = 0;
+    for (int a = 0; a < RT; ++a) n += key(half, 0, a) > key(half, kind, k);
+    for (int b = 0; b < CT; ++b) n += key(half, 1, b) > key(half, kind, k);
+    return n;
+  }
+  static constexpr int issued_before(int half, int i) {        // this K-half's reads before MFMA i
+    int n = 0;
+    for (int a = 0; a < RT; ++a) n += pos(half, 0, a) < i;
+    for (int b = 0; b < CT; ++b) n += pos(half, 1, b) < i;
+    return n;
+  }
+  static constexpr int wait_before(int half, int i) {
+    const int r = i / CT, c = i % CT, prev = 1 - half;
+    // the first MFMA of a row needs its A fragment, the first row needs every B fragment
+    const bool need_a = c == 0, need_b = r == 0;
+    if (!need_a && !need_b) return 16;
+    int n = 1 << 20;
+    if (need_a) n = younger(prev, 0, r);
+    if (need_b) { const int nb = younger(prev, 1, c); n = nb < n ? nb : n; }
+    n += issued_before(half, i);
+    return n > 15 ? 15 : n;
+  }
+};
 
 // B-tile row r -> weight row.  SwiGLU: 16-row group g alternates gate (even g) and up (odd g) rows
 // of output columns n_t * BN/2 + (g / 2) * 16 + r % 16.
@@ -79,33 +141,28 @@ __device__ __forceinline__ int pp_b_row(int r, int n_t, int half) {
 // MODE 0: C bf16 [M, N];  1: split-K slab P (f16 x 2^-6, common.h) [S, M, N];  2: SwiGLU C [M, N/2].
 // VAR bit 0: weights nontemporal (read once); bit 1: grouped row-tile order (prefill, no split).
 template <int BN, int MODE, int VAR>
-__global__ void __launch_bounds__(512, 2) gemm_pp_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+__global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                          bf16* __restrict__ C, float* __restrict__ P, int M, int N,
                                                          int K, int ks_per_split, int nsplit) {
-  constexpr int BM = 256;
-  constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
-  constexpr int TM = BM / WM, TN = BN / WN;            // wave tile: 128 x 64 or 64 x 64
-  constexpr int RT = TM / 16, CT = TN / 16;            // 16 x 16 fragments per wave
-  static_assert(CT == 4 && (RT == 4 || RT == 8), "wave tile");
-  constexpr int PH = RT / 4;                           // phases per K-step (4 A x 4 B fragments each)
-  constexpr int SLOT = (BM + BN) * PBK;                // bf16 elements per ring slot
-  constexpr int NS = BN == 256 ? 5 : 6;
-  constexpr int GA = BM * PBK / 512 / 8, GB = BN * PBK / 512 / 8;   // glds per wave per K-step
-  constexpr int G = GA + GB, GP = G / PH;              // glds per wave per phase
-  static_assert(G % PH == 0, "staging split");
+  constexpr int BM = 256, TM = 128, TN = BN / 2;       // 4 waves as 2 (M) x 2 (N)
+  constexpr int RT = TM / 16, CT = TN / 16;            // 16 x 16 fragments per wave: 8 x 8 or 8 x 4
+  constexpr int SLOT = (BM + BN) * PBK;                // bf16 elements per ring slot (one K-tile)
+  constexpr int NB = BN == 256 ? 2 : 3;                // K-tiles held in LDS
+  constexpr int GA = BM * PBK * 2 / 1024 / 4, GB = BN * PBK * 2 / 1024 / 4;   // glds per wave per K-tile
+  constexpr int G = GA + GB;
   constexpr bool NT = (VAR & 1) != 0, GROUPED = (VAR & 2) != 0;
   constexpr bool SWIGLU = MODE == 2;
   constexpr int OUTW = SWIGLU ? BN / 2 : BN;           // output tile width (elements)
   constexpr int OPITCH = OUTW + 8;                     // LDS output row pitch (elements): +16 B
-  static_assert(NS * SLOT * 2 <= 160 * 1024 && BM * OPITCH <= NS * SLOT, "LDS");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NS * SLOT];
+  constexpr int SMEM = NB * SLOT > BM * OPITCH ? NB * SLOT : BM * OPITCH;   // ring, then output image
+  static_assert(SMEM * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16 smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wv >> 2;                             // ping-pong group: waves w and w+4 share a SIMD
-  const int wm = BN == 256 ? (wv >> 2) : (wv >> 1), wn = BN == 256 ? (wv & 3) : (wv & 1);
+  const int wm = wv >> 1, wn = wv & 1;
   const int mtiles = (M + BM - 1) / BM;
-  const int ntiles = SWIGLU ? (N / 2) / (BN / 2) : N / BN;
+  const int ntiles = N / BN;
   const int total = gridDim.x;
   int b = blockIdx.x;
   {   // bijective XCD remap: consecutive logical blocks share an XCD
@@ -128,35 +185,52 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(const bf16* __restrict_
   const int ks0 = split * ks_per_split;
   const int nt = max(0, min(K / PBK, ks0 + ks_per_split) - ks0);
 
-  // staging sources: wave-instruction i covers 16 slot rows, lane -> (row 16 i + lane / 4,
-  // physical chunk lane % 4) <- logical chunk pswz(row, lane % 4) of the source row
-  const bf16* srcA[GA];
-  const bf16* srcB[GB];
+  // staging sources: wave-instruction i covers 8 slot rows, lane -> (row 8 i + lane / 8,
+  // physical chunk lane % 8) <- logical chunk pswz(row, lane % 8) of the source row.  Byte
+  // offsets are 32-bit from a wave-uniform base (operands < 4 GiB, checked on the host): one VGPR
+  // per A piece (rows past M clamp to M - 1) and ONE for every B piece -- a B piece's row is a
+  // uniform function of the piece index plus lane / 8, also for the SwiGLU row interleave
+  const char* Ab = reinterpret_cast<const char*>(A) + (size_t)ks0 * PBK * 2;
+  const char* Bb = reinterpret_cast<const char*>(B) + (size_t)ks0 * PBK * 2;
+  // the swizzle of row 8 q + lane / 8 depends on q's parity: ((8 q + x) >> 1) & 7 = (4 q + x / 2) & 7
+  uint32_t chunk_q[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) chunk_q[par] = (uint32_t)(pswz(8 * par + (lane >> 3), lane & 7) * 16);
+  uint32_t offA[GA];
 #pragma unroll
   for (int j = 0; j < GA; ++j) {
-    const int r = 16 * (wv * GA + j) + (lane >> 2);
-    srcA[j] = A + (size_t)min(m0 + r, M - 1) * K + (size_t)ks0 * PBK + pswz(r, lane & 3) * 8;
+    const int q = wv * GA + j, r = 8 * q + (lane >> 3);
+    offA[j] = (uint32_t)min(m0 + r, M - 1) * (uint32_t)(K * 2) + chunk_q[q & 1];
   }
+  uint32_t offB[2];
 #pragma unroll
-  for (int j = 0; j < GB; ++j) {
-    const int r = 16 * (wv * GB + j) + (lane >> 2);
-    srcB[j] = B + (size_t)pp_b_row<BN, SWIGLU>(r, n_t, N / 2) * K + (size_t)ks0 * PBK + pswz(r, lane & 3) * 8;
-  }
-  // piece p (0..G-1) of K-step ks into ring slot `slot`
+  for (int par = 0; par < 2; ++par) offB[par] = (uint32_t)(lane >> 3) * (uint32_t)(K * 2) + chunk_q[par];
+  // piece p (0..G-1) of K-tile ks into ring slot `slot`.  ks >= nt (past this split's range):
+  // a DUMMY piece -- K-tile nt - 1 again (L2-resident), into a slot nobody reads again -- so that
+  // every K-tile of the loop issues exactly G pieces: straight-line MFMA streams and static vmcnt
+  // counts
   auto piece = [&](int slot, int ks, int p) {
     bf16* base = smem + slot * SLOT;
-    if (p < GA)
-      __builtin_amdgcn_global_load_lds((glb_vptr_p)(srcA[p] + ks * PBK), (lds_vptr_p)(base + (wv * GA + p) * 512), 16,
-                                       0, 0);
-    else
-      __builtin_amdgcn_global_load_lds((glb_vptr_p)(srcB[p - GA] + ks * PBK),
-                                       (lds_vptr_p)(base + BM * PBK + (wv * GB + p - GA) * 512), 16, 0, NT ? 2 : 0);
+    ks = min(ks, nt - 1);                              // wave-uniform: SALU, no per-lane select
+    if (p < GA) {
+      __builtin_amdgcn_global_load_lds((glb_vptr_p)(Ab + offA[p] + ks * PBK * 2),
+                                       (lds_vptr_p)(base + (wv * GA + p) * 512), 16, 0, 0);
+    } else {
+      const int q = wv * GB + p - GA;                  // 8-row group of the B tile
+      const int brow = pp_b_row<BN, SWIGLU>(8 * q, n_t, N / 2);   // row of lane 0 (uniform)
+      __builtin_amdgcn_global_load_lds((glb_vptr_p)(Bb + (size_t)brow * K * 2 + offB[q & 1] + ks * PBK * 2),
+                                       (lds_vptr_p)(base + BM * PBK + q * 512), 16, 0, NT ? 2 : 0);
+    }
   };
 
-  // fragment read offsets: lane (row l & 15, logical chunk l >> 4) of a 16-row fragment
-  const uint32_t lane_off = (uint32_t)((lane & 15) * 64 + ((lane >> 4) ^ (((lane & 15) >> 1) & 3)) * 16);
-  const uint32_t lds0 = (uint32_t)(size_t)(lds_vptr_p)smem + lane_off;
-  const uint32_t a_off = (uint32_t)(wm * TM * 64), b_off = (uint32_t)(BM * 64 + wn * TN * 64);
+  // fragment read offsets: lane (row l & 15, logical chunk 4 kh + (l >> 4)) of a 16-row fragment
+  // in K-half kh; the swizzle of rows r0 + x (r0 % 16 == 0) depends on x only
+  const uint32_t lds_base = (uint32_t)(size_t)(lds_vptr_p)smem;
+  uint32_t lane_off[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+    lane_off[kh] = (uint32_t)((lane & 15) * 128 + ((4 * kh + (lane >> 4)) ^ (((lane & 15) >> 1) & 7)) * 16);
+  const uint32_t a_off = (uint32_t)(wm * TM * 128), b_off = (uint32_t)(BM * 128 + wn * TN * 128);
 
   f32x4 acc[RT][CT];
 #pragma unroll
@@ -164,66 +238,94 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(const bf16* __restrict_
 #pragma unroll
     for (int j = 0; j < CT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nt > 0) {
-    // prologue: K-steps 0 .. NS-2 in flight, wait for K-step 0, one barrier for everyone
-#pragma unroll
-    for (int j = 0; j < NS - 1; ++j)
-      if (j < nt) {
-#pragma unroll
-        for (int p = 0; p < G; ++p) piece(j, j, p);
-      }
-    pp_wait<G>(min(nt - 1, NS - 2));
-    __builtin_amdgcn_s_barrier();
-    if (grp == 1) __builtin_amdgcn_s_barrier();        // the stagger
-    asm volatile("" ::: "memory");
+  // fragments of one K-half: fa[RT] (A rows of the wave tile), fb[CT] (B rows); two sets, so
+  // the next K-half's reads are in flight under this one's MFMAs (software pipeline)
+  bf16x8 fa0[RT], fb0[CT], fa1[RT], fb1[CT];
 
-    int slot = 0;                                      // ring slot of K-step t
-    for (int t = 0; t < nt; ++t) {
-      const uint32_t rb = lds0 + (uint32_t)(slot * SLOT * 2);
-      const int islot = slot == 0 ? NS - 1 : slot - 1; // slot of K-step t + NS - 1 (= t - 1's)
-      const int ks_issue = t + NS - 1;
-      const bool more = t + 1 < nt;
-      const int younger = min(nt - 2 - t, NS - 2);     // K-steps after t + 1 already issued
-      bf16x8 fb[CT];
+  if (nt > 0) {
+    using SC = PpSched<RT, CT>;
+    constexpr int NMF = RT * CT;                       // 64 or 32 MFMAs per K-half
+    // prologue: K-tiles 0 .. NB-1 in flight; wait for K-tile 0; read K-half 0 of it in the
+    // order a K-half 1 issues its reads (so the counted waits of the first K-half 0 hold)
 #pragma unroll
-      for (int ph = 0; ph < PH; ++ph) {
-        // ---- read section: this phase's staging pieces, fragments, (group 1) next K-step's wait
-        if (ks_issue < nt) {
+    for (int j = 0; j < NB; ++j)
 #pragma unroll
-          for (int p = 0; p < GP; ++p) piece(islot, ks_issue, ph * GP + p);
-        }
-        bf16x8 fa[4];
-        const uint32_t ra = rb + a_off + (uint32_t)(ph * 64 * 64);
-        fa[0] = pp_frag<0>(ra);
-        fa[1] = pp_frag<16 * 64>(ra);
-        fa[2] = pp_frag<32 * 64>(ra);
-        fa[3] = pp_frag<48 * 64>(ra);
-        if (ph == 0) {
-          const uint32_t rbb = rb + b_off;
-          fb[0] = pp_frag<0>(rbb);
-          fb[1] = pp_frag<16 * 64>(rbb);
-          fb[2] = pp_frag<32 * 64>(rbb);
-          fb[3] = pp_frag<48 * 64>(rbb);
-        }
-        if (ph == PH - 1 && more && grp == 1) pp_wait<G>(younger);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- MFMA section
+      for (int p = 0; p < G; ++p) piece(j, j, p);
+    pp_wait_n<G>(NB - 1);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    {
+      const uint32_t base = lds_base + lane_off[0];
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
+      for (int i = 0; i < NMF; ++i) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            acc[ph * 4 + r][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ct], fa[r], acc[ph * 4 + r][ct], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (ph == PH - 1 && more && grp == 0) pp_wait<G>(younger);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
+        for (int r = 0; r < RT; ++r)
+          if (SC::pos(1, 0, r) == i) fa0[r] = pp_frag_dyn(base + a_off + r * 16 * 128);
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+          if (SC::pos(1, 1, c) == i) fb0[c] = pp_frag_dyn(base + b_off + c * 16 * 128);
       }
-      slot = slot == NS - 1 ? 0 : slot + 1;
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if (grp == 0) __builtin_amdgcn_s_barrier();        // balance the stagger
+
+    // One K-half: NMF MFMAs, row-fragment-major, with the other K-half's fragment reads and (in
+    // K-half 1) the LDS-DMA pieces interleaved in program order.  Every MFMA that first uses a
+    // fragment waits with a COUNTED lgkmcnt for exactly that read (PpSched), never lgkmcnt(0)
+    // inside the stream.  K-half 1 holds the K-tile's one barrier after its first fragment row:
+    // the last reads of this slot have had a row of MFMAs to land (WAR), the next tile has
+    // landed for every wave (RAW), and only then are the next tile's fragments read and this
+    // slot re-staged.
+    int slot = 0;                                      // ring slot of K-tile t
+    for (int t = 0; t < nt; ++t) {
+      const uint32_t cur = lds_base + (uint32_t)(slot * SLOT * 2);
+      const int nslot = slot == NB - 1 ? 0 : slot + 1;
+      const uint32_t nxt = lds_base + (uint32_t)(nslot * SLOT * 2);
+      // ---- K-half 0: MFMAs on (fa0, fb0); read K-half 1 of this K-tile into (fa1, fb1)
+      {
+        const uint32_t base = cur + lane_off[1];
+        pp_static_for<NMF>([&](auto ic) {
+          constexpr int i = decltype(ic)::value, r = i / CT, c = i % CT;
+          pp_lgkm<SC::wait_before(0, i)>();
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[c], fa0[r], acc[r][c], 0, 0, 0);
+#pragma unroll
+          for (int a = 0; a < RT; ++a)
+            if (SC::pos(0, 0, a) == i) fa1[a] = pp_frag_dyn(base + a_off + a * 16 * 128);
+#pragma unroll
+          for (int b = 0; b < CT; ++b)
+            if (SC::pos(0, 1, b) == i) fb1[b] = pp_frag_dyn(base + b_off + b * 16 * 128);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      }
+      // ---- K-half 1: MFMAs on (fa1, fb1); after its first row the barrier B_t, then read K-half 0
+      // of K-tile t + 1 into (fa0, fb0) (garbage past the last tile, never used) and stage K-tile
+      // t + NB into this slot (a dummy piece past the range): straight-line, no branch
+      {
+        const uint32_t base = nxt + lane_off[0];
+        constexpr int GE = 2;                          // one LDS-DMA piece every 2 MFMAs after B_t
+        pp_static_for<NMF>([&](auto ic) {
+          constexpr int i = decltype(ic)::value, r = i / CT, c = i % CT;
+          pp_lgkm<SC::wait_before(1, i)>();
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[c], fa1[r], acc[r][c], 0, 0, 0);
+          if constexpr (i == SC::EB - 1) {
+            // B_t: every read of this slot done (WAR), K-tile t + 1 landed for every wave (RAW)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            pp_wait_n<G>(NB - 2);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+          }
+          if constexpr (i >= SC::EB - 1 && (i - SC::EB + 1) % GE == 0 && (i - SC::EB + 1) / GE < G)
+            piece(slot, t + NB, (i - SC::EB + 1) / GE);
+#pragma unroll
+          for (int a = 0; a < RT; ++a)
+            if (SC::pos(1, 0, a) == i) fa0[a] = pp_frag_dyn(base + a_off + a * 16 * 128);
+#pragma unroll
+          for (int b = 0; b < CT; ++b)
+            if (SC::pos(1, 1, b) == i) fb0[b] = pp_frag_dyn(base + b_off + b * 16 * 128);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      }
+      slot = nslot;
+    }
   }
 
   // ---- epilogue: accumulators -> LDS output image (8-byte writes) -> 16-byte row stores.
@@ -265,7 +367,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(const bf16* __restrict_
   }
   __syncthreads();
   constexpr int CPR = OUTW / 8;                        // 16-byte chunks per output row
-  constexpr int RPI = 512 / CPR;                       // rows per pass
+  constexpr int RPI = 256 / CPR;                       // rows per pass
   const int ch = tid % CPR, r0 = tid / CPR;
   const int ldc = SWIGLU ? N / 2 : N;
   const int col0 = n_t * OUTW + ch * 8;
@@ -290,7 +392,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(const bf16* __restrict_
 int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream) {
   DLLM_HOST_CHECK(M >= 1, "M >= 1");
-  DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 32");
+  DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");
   DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
   const int BN = (variant & 1) ? 128 : 256;
@@ -303,11 +405,12 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
   DLLM_HOST_CHECK(mode != 2 || S > 1, "mode 2 needs a K split");
   const int mtiles = (M + 255) / 256;
   const long grid = (long)(N / BN) * mtiles * S;
+  DLLM_HOST_CHECK((long)M * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32), "operands must be < 4 GiB");
   DLLM_HOST_CHECK(grid >= 1 && grid < (1L << 31), "grid");
   const bool nt = (variant & 2) != 0;
   const bool grp = (variant & 4) != 0 && S == 1 && mtiles > 1;
 #define DLLM_PP_GO(BN_, MODE_, VAR_)                                                                     \
-  hipLaunchKernelGGL((gemm_pp_kernel<BN_, MODE_, VAR_>), dim3((unsigned)grid), dim3(512), 0, s, (const bf16*)a, \
+  hipLaunchKernelGGL((gemm_pp_kernel<BN_, MODE_, VAR_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, \
                      (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kps, S)
 #define DLLM_PP_V(BN_, MODE_)                                        \
   do {                                                               \

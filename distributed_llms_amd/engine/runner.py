@@ -59,6 +59,7 @@ class StageRunner:
         stage.allocate_kv(nb, self.block_size)
         self.num_blocks = nb
         self.max_blocks = -(-ecfg.max_seq_len // self.block_size)
+        self._busy = None                 # [(start, end) events or host seconds] while metering
         self.graph_sets = []
         if ecfg.use_graphs and stage.device.type == "cuda":
             sizes = [b for b in ecfg.graph_batch_sizes if b <= ecfg.max_batch] or [ecfg.max_batch]
@@ -79,12 +80,13 @@ class StageRunner:
         """``ids_dev`` (first stage, decode): input token ids already on the device (they replace
         ``hb.ids``, a placeholder then)."""
         tr = self.tracer
+        run = self._execute if self._busy is None else self._metered
         if not tr.enabled:
-            return self._execute(hb, hidden, slot, ids_dev)
+            return run(hb, hidden, slot, ids_dev)
         kind = "prefill" if hb.is_prefill else "decode"
         gspan = tr.gpu_span(kind, cat="stage") if self.stage.device.type == "cuda" else tr.span(kind, cat="stage")
         with tr.span(f"stage.{kind}", cat="host", rows=hb.num_tokens, seqs=hb.num_seqs, slot=slot), gspan:
-            return self._execute(hb, hidden, slot, ids_dev)
+            return run(hb, hidden, slot, ids_dev)
 
     def _execute(self, hb: HostBatch, hidden: Optional[torch.Tensor], slot: int,
                  ids_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -96,6 +98,35 @@ class StageRunner:
         if ids_dev is not None:
             ids = ids_dev.to(torch.int32)
         return st.forward(ids if st.is_first else hidden, meta)
+
+    # ---- busy metering: the stage's device time per microbatch (bench.py's stage_busy_frac)
+    def meter(self, on: bool = True):
+        self._busy = [] if on else None
+
+    def _metered(self, hb, hidden, slot, ids_dev):
+        if self.stage.device.type != "cuda":
+            import time
+            t0 = time.perf_counter()
+            out = self._execute(hb, hidden, slot, ids_dev)
+            self._busy.append(time.perf_counter() - t0)
+            return out
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = self._execute(hb, hidden, slot, ids_dev)
+        b.record()
+        self._busy.append((a, b))
+        return out
+
+    def busy_seconds(self) -> float:
+        """Sum of the metered microbatches' execution spans (synchronises the recorded events)."""
+        tot = 0.0
+        for e in self._busy or ():
+            if isinstance(e, float):
+                tot += e
+            else:
+                e[1].synchronize()
+                tot += e[0].elapsed_time(e[1]) * 1e-3
+        return tot
 
     def warmup_graphs(self, batch_sizes=None, ctx_buckets=(256,)):
         """Pre-capture decode graphs (keeps capture cost out of timed regions)."""

@@ -315,10 +315,10 @@ def linear_big(x: torch.Tensor, w: torch.Tensor, splits: int = 2, swiglu: bool =
 
 
 def pp_splits(m: int, n: int, k: int, bn: int = 256, target_wgs: int = 256) -> int:
-    """K slices for gemm_pp: about one workgroup per CU (tiles x slices <= target), >= 4 K-steps
-    (128) per slice."""
+    """K slices for gemm_pp: about one workgroup per CU (tiles x slices <= target), >= 3 K-tiles
+    (192) per slice."""
     tiles = (n // bn) * (-(-m // 256))
-    return max(1, min(target_wgs // max(1, tiles), (k // 32) // 4, 32))
+    return max(1, min(target_wgs // max(1, tiles), (k // 64) // 3, 32))
 
 
 def linear_pp(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = False, defer: bool = False,
@@ -333,8 +333,8 @@ def linear_pp(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = 
     if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
         raise ValueError("linear_pp: bf16 contiguous operands")
     bn = 128 if variant & 1 else 256
-    if n % bn or k % 32:
-        raise ValueError(f"linear_pp: N % {bn} and K % 32")
+    if n % bn or k % 64:
+        raise ValueError(f"linear_pp: N % {bn} and K % 64")
     s = splits or pp_splits(m, n, k, bn)
     ws = _workspace(x.device)
     if s > 1 and s * m * n > ws.numel():

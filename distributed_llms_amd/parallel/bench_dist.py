@@ -21,7 +21,7 @@ def _sync(ctx):
 def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=None):
     pp = (getattr(args, "pp", 0) or None) if args.parallelism == "pp" else 1
     tp = getattr(args, "tp", 0) or (int(os.environ.get("WORLD_SIZE", "1")) if args.parallelism == "tp" else 1)
-    ctx = init_distributed(pp=pp, tp=tp, moe=getattr(args, "moe", "tp"))
+    ctx = init_distributed(pp=pp, tp=tp, moe=getattr(args, "moe", "tp"), timeout_s=600)
     world = ctx.world
     # pipeline: prefill in ~8K-token microbatches (M large enough for full-rate GEMMs) so the
     # fill/drain bubble of the prefill phase is (pp-1) x ~8K-token stage times, not (pp-1) x a
@@ -55,6 +55,9 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
     for r in range(args.warmup):
         one_round(10_000 + r)
     _sync(ctx)
+    runner = role.runner if role.runner is not None else getattr(role.engine, "runner", None)
+    if runner is not None:
+        runner.meter(True)
     tr = start_trace(args) if start_trace else None
     lat = []
     t0 = time.perf_counter()
@@ -69,10 +72,16 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
     obj = [None] * world
     dist.all_gather_object(obj, lat, group=ctx.ctrl_group)
     all_lat = [x for part in obj for x in part]
-    busy = None
     if tr is not None:
-        busy = [None] * world
-        dist.all_gather_object(busy, finish_trace(args, tr, elapsed, ctx.rank), group=ctx.ctrl_group)
+        finish_trace(args, tr, elapsed, ctx.rank)
+    # per-rank device busy fraction over the timed rounds, and what the data plane ran on
+    mine = {"busy": round(runner.busy_seconds() / elapsed, 4) if runner is not None else None}
+    tp_ = getattr(role, "transport", None)
+    mine["transport"] = getattr(tp_, "kind", "none") if tp_ is not None else "none"
+    mine["rccl_comm_ranks"] = list(getattr(tp_, "comm_ranks", []) or [])
+    info = [None] * world
+    dist.all_gather_object(info, mine, group=ctx.ctrl_group)
+    busy = [i["busy"] for i in info]
     if ctx.rank == 0:
         pj = role.plan.to_json()
         extra = {"load_s": round(load_s, 1), "stage_ranges": pj["ranges"], "backend": dist.get_backend()}
@@ -81,8 +90,13 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
         if role.driver is not None:
             extra["driver_stall_s"] = round(role.driver.stall_s, 3)
         extra["microbatch_slots"] = slots
-        if busy is not None:
-            extra["stage_busy_frac"] = busy
+        extra["stage_busy_frac"] = busy
+        kinds = sorted({i["transport"] for i in info})
+        extra["transport"] = kinds[0] if len(kinds) == 1 else kinds
+        # every native RCCL communicator appears on both of its ranks: count them once
+        extra["rccl_comms"] = sum(len(i["rccl_comm_ranks"]) for i in info) // 2
+        extra["rccl_ranks"] = sum(1 for i in info if i["rccl_comm_ranks"])
+        extra["rccl_comm_nranks"] = sorted({n for i in info for n in i["rccl_comm_ranks"]})
         emit(args, world, elapsed, all_lat, extra, global_batch=per_pipe * ctx.dp)
     role.shutdown()
     _sync(ctx)

@@ -31,6 +31,20 @@ import torch.distributed as dist
 STOP = -1
 
 
+def sync_event(ev, timeout_s: float, what: str = "pipeline peer"):
+    """ev.synchronize() with a deadline: a dead pipeline peer must not hang the host forever."""
+    if ev.query():
+        return
+    import time
+    t_end = time.monotonic() + timeout_s
+    delay = 2e-5
+    while not ev.query():
+        if time.monotonic() > t_end:
+            raise TimeoutError(f"{what}: no data after {timeout_s:.0f} s (peer dead or hung)")
+        time.sleep(delay)
+        delay = min(delay * 2, 1e-3)
+
+
 class PendingIds:
     """One microbatch's sampled ids on their way from the last stage to stage 0.
 
@@ -40,8 +54,9 @@ class PendingIds:
     host read later finds it done."""
 
     def __init__(self, tensor: Optional[torch.Tensor] = None, work=None, ready=None, fetch=None,
-                 copy_stream=None):
+                 copy_stream=None, timeout_s: float = 600.0):
         self.tensor = tensor
+        self.timeout_s = timeout_s
         self._work = work          # torch.distributed Work (NCCL: stream-orders; gloo: blocks)
         self._ready = ready        # torch.cuda.Event recorded when `tensor` was filled
         self._fetch = fetch        # loopback: blocking getter -> (tensor, event or None)
@@ -76,7 +91,7 @@ class PendingIds:
 
     def host(self) -> np.ndarray:
         if self._host_ev is not None:
-            self._host_ev.synchronize()
+            sync_event(self._host_ev, self.timeout_s, "sampled ids from the last stage")
             return self._host.numpy()
         t = self.wait()
         if t.is_cuda:
@@ -99,12 +114,29 @@ class Transport:
 class DistTransport(Transport):
     """One pipeline = ranks ``ranks[0..pp-1]`` (global ranks), stage = index in that list."""
 
-    def __init__(self, ranks, stage: int, ctrl_group=None, data_group=None, ring_group=None):
+    kind = "torch"
+
+    def __init__(self, ranks, stage: int, ctrl_group=None, data_group=None, ring_group=None, hop=None,
+                 device=None, timeout_s: float = 600.0):
         """``data_group`` None = the default group (RCCL on GPU).  A gloo ``data_group`` with GPU
         stages means host-staged activations (D2H -> gloo -> H2D): the TCP fallback.
         ``ring_group``: the {first, last} group of this pipeline for the ids ring closure (None =
-        the data group; fine wherever the activation and ids flows join different rank pairs)."""
+        the data group; fine wherever the activation and ids flows join different rank pairs).
+        ``hop`` = (max rows, hidden, dtype, in-flight window): with GPU stages on the RCCL group the
+        activations then use static send / receive rings of window + 1 slots (no clone, no
+        allocation per hop; torch orders its RCCL stream after the compute stream at enqueue, so
+        a receive into a slot follows that slot's previous consumers)."""
         self.ranks = list(ranks)
+        self.timeout_s = float(timeout_s)
+        self._tx = self._rx = None
+        if hop is not None and device is not None and torch.device(device).type == "cuda" and data_group is None:
+            rows, hidden, dtype, window = hop
+            n = int(rows) * int(hidden)
+            self._ring_n = window + 1
+            self._tx = torch.empty(self._ring_n, n, dtype=dtype, device=device) if stage + 1 < len(ranks) else None
+            self._rx = torch.empty(self._ring_n, n, dtype=dtype, device=device) if stage > 0 else None
+            self._tx_work = [None] * self._ring_n
+            self._tx_i = self._rx_i = 0
         self.ring = ring_group if ring_group is not None else data_group
         self._copy_stream = None
         self.stage = stage
@@ -183,13 +215,22 @@ class DistTransport(Transport):
         if dev.type == "cuda":
             if self._copy_stream is None:
                 self._copy_stream = torch.cuda.Stream(dev)
-            return PendingIds(buf, work=w, copy_stream=self._copy_stream)
-        return PendingIds(buf, work=w)
+            return PendingIds(buf, work=w, copy_stream=self._copy_stream, timeout_s=self.timeout_s)
+        return PendingIds(buf, work=w, timeout_s=self.timeout_s)
 
     # ---- data plane (RCCL on GPU, gloo on CPU)
     def send_hidden(self, t: torch.Tensor):
         # copy: `t` may be a graph's static output that the next replay overwrites while the
         # send (on the comm stream) is still reading it
+        if self._tx is not None and t.is_cuda and t.numel() <= self._tx.shape[1]:
+            slot = self._tx_i % self._ring_n
+            self._tx_i += 1
+            if self._tx_work[slot] is not None:
+                self._tx_work[slot].wait()       # stream-orders the overwrite after that send
+            dst = self._tx[slot, : t.numel()]
+            dst.copy_(t.reshape(-1))
+            self._tx_work[slot] = dist.isend(dst, self.next, group=self.data)
+            return
         if t.is_cuda and self.data is not None and dist.get_backend(self.data) == "gloo":
             t = t.to("cpu")                      # host-staged fallback (synchronous D2H)
         else:
@@ -199,6 +240,12 @@ class DistTransport(Transport):
         self._reap()
 
     def recv_hidden(self, rows, hidden, dtype, device):
+        if self._rx is not None and rows * hidden <= self._rx.shape[1] and dtype == self._rx.dtype:
+            slot = self._rx_i % self._ring_n
+            self._rx_i += 1
+            buf = self._rx[slot, : rows * hidden]
+            dist.irecv(buf, self.prev, group=self.data).wait()   # stream-ordered, no host block
+            return buf.view(rows, hidden)
         staged = torch.device(device).type == "cuda" and self.data is not None \
             and dist.get_backend(self.data) == "gloo"
         buf = torch.empty(rows, hidden, dtype=dtype, device="cpu" if staged else device)
@@ -209,6 +256,14 @@ class DistTransport(Transport):
         for w, _ in self._pending:
             w.wait()
         self._pending = []
+        if self._tx is not None:
+            for w in self._tx_work:
+                if w is not None:
+                    w.wait()
+            self._tx_work = [None] * self._ring_n
+
+    def status(self) -> str:
+        return ""
 
 
 class LoopbackHub:

@@ -137,22 +137,49 @@ def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
                        rings, tp, tpg)
 
 
-def make_transport(ranks, stage: int, ctrl_group, data_group, device: str, ring_group=None, hop=None):
-    """Activation transport for one pipeline stage: torch.distributed's RCCL process group by
-    default; ``DLLM_TRANSPORT=rccl`` selects the native RCCL p2p module (own comm streams),
-    ``DLLM_TRANSPORT=ipc`` the HIP-IPC peer-write data plane (parallel/ipc_transport.py; also
-    between processes sharing one GPU).  ``hop`` = (max rows, hidden, dtype, in-flight window) of an activation hop."""
-    kind = os.environ.get("DLLM_TRANSPORT", "")
+def resolve_transport(kind: str, device: str, host_staged: bool) -> str:
+    """The activation transport a stage uses: CPU stages and host-staged GPU stages always ride
+    torch.distributed (gloo); on GPUs "auto" is the native RCCL edge transport."""
+    if not str(device).startswith("cuda") or host_staged:
+        return "torch"
+    env = os.environ.get("DLLM_TRANSPORT", "")          # test / rehearsal override
+    kind = env or kind or "auto"
+    return "rccl" if kind == "auto" else kind
+
+
+def make_transport(ranks, stage: int, ctrl_group, data_group, device: str, ring_group=None, hop=None,
+                   kind: str = "auto", timeout_s: float = 600.0):
+    """Activation transport for one pipeline stage (see resolve_transport).  ``hop`` = (max rows,
+    hidden, dtype, in-flight window) of an activation hop: every GPU transport sizes its static
+    rings from it.  If the native RCCL communicators cannot be created on some rank, EVERY rank of
+    the job falls back to torch.distributed's RCCL group (agreed over the control group), so a
+    library or topology problem costs speed, not the run."""
+    kind = resolve_transport(kind, device, data_group is not None)
     on_gpu = str(device).startswith("cuda")
     if kind == "ipc" and on_gpu:
         from .ipc_transport import IpcTransport
         rows, hidden, dtype, window = hop
         return IpcTransport(ranks, stage, ctrl_group, device, rows, hidden, dtype, ring_group=ring_group,
                             window=window)
-    if kind == "rccl" and data_group is None and on_gpu:
+    if kind == "rccl" and on_gpu:
         from .rccl_transport import RcclTransport
-        return RcclTransport(ranks, stage, ctrl_group, device)
-    return DistTransport(ranks, stage, ctrl_group=ctrl_group, data_group=data_group, ring_group=ring_group)
+        rows, hidden, dtype, window = hop
+        t, err = None, None
+        try:
+            t = RcclTransport(ranks, stage, ctrl_group, device, rows, hidden, dtype, ring_group=ring_group,
+                              window=window, timeout_s=timeout_s)
+        except Exception as e:          # noqa: BLE001 - reported, then the whole job agrees on a fallback
+            err = e
+        ok = torch.tensor([0 if err is None else 1], dtype=torch.int64)
+        dist.all_reduce(ok, op=dist.ReduceOp.MAX, group=ctrl_group)
+        if int(ok.item()) == 0:
+            return t
+        log.error("native RCCL transport unavailable (%s); every stage falls back to torch.distributed",
+                  err if err is not None else "failed on another rank")
+        if t is not None:
+            t.abort()
+    return DistTransport(ranks, stage, ctrl_group=ctrl_group, data_group=data_group, ring_group=ring_group,
+                         hop=hop, device=device, timeout_s=timeout_s)
 
 
 def agree_min(ctx: DistContext, value: int) -> int:
@@ -203,7 +230,8 @@ class RankRole:
             hop = (max(ecfg.max_prefill_tokens, ecfg.max_batch), width, stage.dtype,
                    inflight_window(ecfg, ctx.pp, stage.device))
             self.transport = make_transport(ctx.pipeline_ranks, ctx.stage, ctx.ctrl_group, ctx.data_group,
-                                            ctx.device, ctx.ring_group, hop=hop)
+                                            ctx.device, ctx.ring_group, hop=hop, kind=ecfg.transport,
+                                            timeout_s=ecfg.comm_timeout_s)
             if ctx.stage == 0 and ctx.tp_rank == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.runner, self.transport, ecfg, bm)

@@ -1,22 +1,29 @@
 """Pipeline transport over the native RCCL p2p module (``csrc/comm/rccl_p2p.cpp``).
 
-Control messages (batch metadata, tokens, markers) stay on the gloo control group exactly as in
-:class:`DistTransport`; activations go through a per-pipeline RCCL communicator on a DEDICATED
-comm stream:
+Control messages (batch metadata, markers) stay on DistTransport's gloo path.  Activations travel
+through one two-rank RCCL communicator per pipeline EDGE (stage s -> s + 1, an xGMI peer link),
+each stage driving its incoming and outgoing edge on two dedicated comm streams -- a stage's
+receive of microbatch n + 1 never queues behind its send of microbatch n.  The sampled-ids ring
+closure (last stage -> stage 0) is a third two-rank communicator with its own streams and rings,
+so the whole data plane runs on communicators this module owns (and aborts: abort()).
 
-  send_hidden : copy the stage output on the compute stream (graph outputs are static buffers the
-                next replay overwrites) -> event -> comm stream waits -> ncclSend
-  recv_hidden : ncclRecv into a fresh buffer on the comm stream -> event -> compute stream waits
+No allocation and no clone per hop (static rings, ``window + 1`` slots, sized once from the
+pipeline's largest hop):
 
-so a stage's next microbatch is never queued behind a transfer, and no host thread blocks on the
-GPU.  The communicator's unique id is created by each pipeline's stage 0 and distributed over the
-control group (all_gather: every rank participates once, any dp x pp layout).
+  send_hidden : [compute] wait until the tx slot's previous send finished -> copy the stage output
+                (a graph-static buffer the next replay overwrites) into the slot -> event
+                [send]    wait event -> ncclSend(slot) -> "sent" event for the slot
+  recv_hidden : [compute] "consumed" event for the previously received slot (everything the stage
+                enqueued since includes its consumer)
+                [recv]    wait until this slot was consumed -> ncclRecv(slot) -> "landed" event
+                [compute] wait "landed" -> the stage reads the slot in place
 
-Opt-in with ``DLLM_TRANSPORT=rccl`` (default: torch.distributed's RCCL process group).
+so no host thread waits on the GPU, and slot reuse is ordered by events, not by the allocator.
+Communicators are non-blocking with a deadline (``timeout_s``): a peer that never joins, or dies
+while a connection is set up, makes this rank raise instead of hanging; the driver's host waits
+on the ids ring are bounded the same way (comm.PendingIds).
 """
 from __future__ import annotations
-
-import collections
 
 import torch
 import torch.distributed as dist
@@ -26,59 +33,230 @@ from .comm import DistTransport
 
 
 class RcclTransport(DistTransport):
-    def __init__(self, ranks, stage: int, ctrl_group, device):
-        super().__init__(ranks, stage, ctrl_group=ctrl_group, data_group=None)
+    kind = "rccl"
+
+    def __init__(self, ranks, stage: int, ctrl_group, device, max_rows: int, hidden: int, dtype=torch.bfloat16,
+                 ring_group=None, window: int = 2, timeout_s: float = 600.0, loopback: bool = False,
+                 max_ids: int = 0):
+        """``window``: the most microbatches in flight (the rings get window + 1 slots).
+        ``loopback``: test mode on ONE rank -- a single one-rank communicator serves both edges
+        (stage 0 sends to itself); each send is deferred and issued together with the matching
+        receive as one grouped exchange, the only legal form of a self send."""
+        super().__init__(ranks, stage, ctrl_group=ctrl_group, data_group=None, ring_group=ring_group,
+                         timeout_s=timeout_s)
         dev = torch.device(device)
         if dev.type != "cuda":
             raise ValueError("RcclTransport needs a GPU stage")
+        if window < 1:
+            raise ValueError("in-flight window must be >= 1")
         self.device = dev
-        m = _ext.rccl()
-        uid = m.unique_id() if stage == 0 else b""
-        allv = [None] * dist.get_world_size(group=ctrl_group)
-        dist.all_gather_object(allv, (self.ranks[0], uid), group=ctrl_group)
-        mine = next(u for (r0, u) in allv if r0 == self.ranks[0] and u)
-        self.comm = m.RcclComm(len(self.ranks), stage, mine, dev.index or 0)
-        self.comm_stream = torch.cuda.Stream(device=dev)
-        self._inflight = collections.deque()        # (done event, tensor kept alive)
+        self.m = _ext.rccl()
+        self.timeout_s = float(timeout_s)
+        self.slots = window + 1
+        self.slot_elems = int(max_rows) * int(hidden)
+        self.dtype = dtype
+        self.loopback = loopback
+        self.comm_in = self.comm_out = self.ring_out = self.ring_in = None
+        first, last = stage == 0, stage == len(self.ranks) - 1
+        di = dev.index or 0
+        if loopback:
+            self.comm_out = self.comm_in = self.m.RcclComm(1, 0, self.m.unique_id(), di, self.timeout_s)
+            self.ring_out = self.ring_in = self.comm_out
+            self.next = self.prev = self.ranks[0]
+        else:
+            # one unique id per communicator, made by its sender; every rank of the ctrl group
+            # takes part in the exchange (any dp x pp layout)
+            mine = {"edge": self.m.unique_id() if self.next is not None else b"",
+                    "ring": self.m.unique_id() if last and not first else b""}
+            allv = [None] * dist.get_world_size(group=ctrl_group)
+            dist.all_gather_object(allv, (dist.get_rank(), mine), group=ctrl_group)
+            table = dict(allv)
+            # ascending edge order on every rank (in-edge first), the ring last: the chain of
+            # inits cannot deadlock
+            if self.prev is not None:
+                self.comm_in = self.m.RcclComm(2, 1, table[self.prev]["edge"], di, self.timeout_s)
+            if self.next is not None:
+                self.comm_out = self.m.RcclComm(2, 0, mine["edge"], di, self.timeout_s)
+            if last and not first:
+                self.ring_out = self.m.RcclComm(2, 0, mine["ring"], di, self.timeout_s)
+            elif first and not last:
+                self.ring_in = self.m.RcclComm(2, 1, table[self.last]["ring"], di, self.timeout_s)
+        self.send_stream = torch.cuda.Stream(device=dev) if self.comm_out is not None else None
+        self.recv_stream = torch.cuda.Stream(device=dev) if self.comm_in is not None else None
+        if loopback:
+            self.recv_stream = self.send_stream
+        self.tx = torch.empty(self.slots, self.slot_elems, dtype=dtype, device=dev) if self.comm_out else None
+        self.rx = torch.empty(self.slots, self.slot_elems, dtype=dtype, device=dev) if self.comm_in else None
+        self._sent = [None] * self.slots          # per tx slot: event after its ncclSend
+        self._consumed = [None] * self.slots      # per rx slot: event after its consumer was enqueued
+        self._tx_n = 0
+        self._rx_n = 0
+        self._last_rx = None
+        self._deferred = []                       # loopback: sends waiting for their receive
+        # sampled-ids ring closure: int32 slots of max_ids, deeper than the in-flight window
+        self.max_ids = int(max_ids or max_rows)
+        self.id_slots = 2 * window + 2
+        self.ring_stream = torch.cuda.Stream(device=dev) if (self.ring_out or self.ring_in) else None
+        self.ids_tx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_out else None
+        self.ids_rx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_in else None
+        self._ids_sent = [None] * self.id_slots
+        self._ids_users = [None] * self.id_slots   # per rx slot: the PendingIds of its last use
+        self._ids_tx_n = self._ids_rx_n = 0
+        self._ids_deferred = []
+        self._copy_stream = None
 
-    def _retire(self):
-        while self._inflight and self._inflight[0][0].query():
-            self._inflight.popleft()
+    @property
+    def comm_ranks(self):
+        """Ranks of this stage's RCCL edge communicators (reported by bench.py)."""
+        return [c.nranks for c in self._comms()]
+
+    def _check_hop(self, numel, dtype):
+        if numel > self.slot_elems or dtype != self.dtype:
+            raise ValueError(f"hop of {numel} x {dtype} exceeds the RCCL ring slot ({self.slot_elems} x {self.dtype})")
 
     def send_hidden(self, t: torch.Tensor):
+        self._check_hop(t.numel(), t.dtype)
+        n = self._tx_n
+        self._tx_n += 1
+        slot = n % self.slots
         cur = torch.cuda.current_stream(self.device)
-        buf = t.clone(memory_format=torch.contiguous_format)
+        if self._sent[slot] is not None:
+            cur.wait_event(self._sent[slot])      # the slot's previous send has left
+        dst = self.tx[slot, : t.numel()]
+        dst.copy_(t.reshape(-1))
+        nbytes = t.numel() * t.element_size()
         ready = torch.cuda.Event()
         ready.record(cur)
-        self.comm_stream.wait_event(ready)
-        self.comm.send(buf.data_ptr(), buf.numel() * buf.element_size(), self.stage + 1,
-                       self.comm_stream.cuda_stream)
-        done = torch.cuda.Event()
-        done.record(self.comm_stream)
-        buf.record_stream(self.comm_stream)
-        self._inflight.append((done, buf))
-        self._retire()
+        if self.loopback:
+            self._deferred.append((slot, nbytes, ready))
+            return
+        self.send_stream.wait_event(ready)
+        self.comm_out.send(dst.data_ptr(), nbytes, 1, self.send_stream.cuda_stream)
+        sent = torch.cuda.Event()
+        sent.record(self.send_stream)
+        self._sent[slot] = sent
 
     def recv_hidden(self, rows, hidden, dtype, device):
+        self._check_hop(rows * hidden, dtype)
         cur = torch.cuda.current_stream(self.device)
-        buf = torch.empty(rows, hidden, dtype=dtype, device=self.device)
-        # the buffer comes from the compute stream's pool: order the comm stream after its
-        # allocation point, and tell the allocator the comm stream uses it
-        alloc = torch.cuda.Event()
-        alloc.record(cur)
-        self.comm_stream.wait_event(alloc)
-        self.comm.recv(buf.data_ptr(), buf.numel() * buf.element_size(), self.stage - 1,
-                       self.comm_stream.cuda_stream)
-        buf.record_stream(self.comm_stream)
-        got = torch.cuda.Event()
-        got.record(self.comm_stream)
-        cur.wait_event(got)
-        return buf
+        if self._last_rx is not None:             # everything enqueued so far consumed that slot
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self._consumed[self._last_rx] = ev
+        n = self._rx_n
+        self._rx_n += 1
+        slot = n % self.slots
+        rs = self.recv_stream
+        if self._consumed[slot] is not None:
+            rs.wait_event(self._consumed[slot])
+        buf = self.rx[slot, : rows * hidden]
+        nbytes = rows * hidden * buf.element_size()
+        if self.loopback:
+            tslot, tbytes, ready = self._deferred.pop(0)
+            if tbytes != nbytes:
+                raise RuntimeError(f"loopback hop size mismatch: sent {tbytes} B, receiving {nbytes} B")
+            rs.wait_event(ready)
+            self.comm_out.sendrecv(self.tx[tslot].data_ptr(), tbytes, 0, buf.data_ptr(), nbytes, 0, rs.cuda_stream)
+            sent = torch.cuda.Event()
+            sent.record(rs)
+            self._sent[tslot] = sent
+        else:
+            self.comm_in.recv(buf.data_ptr(), nbytes, 0, rs.cuda_stream)
+        landed = torch.cuda.Event()
+        landed.record(rs)
+        cur.wait_event(landed)
+        self._last_rx = slot
+        return buf.view(rows, hidden)
+
+    # ---- ring closure: sampled ids, last stage -> stage 0, on the ring communicator
+    def send_ids(self, ids: torch.Tensor):
+        n_ids = ids.shape[0]
+        if n_ids > self.max_ids:
+            raise ValueError(f"{n_ids} sampled ids exceed the ring slot ({self.max_ids})")
+        n = self._ids_tx_n
+        self._ids_tx_n += 1
+        slot = n % self.id_slots
+        cur = torch.cuda.current_stream(self.device)
+        if self._ids_sent[slot] is not None:
+            cur.wait_event(self._ids_sent[slot])
+        dst = self.ids_tx[slot, :n_ids]
+        dst.copy_(ids.reshape(-1))
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        if self.loopback:
+            self._ids_deferred.append((slot, n_ids, ready))
+            return
+        self.ring_stream.wait_event(ready)
+        self.ring_out.send(dst.data_ptr(), n_ids * 4, 1, self.ring_stream.cuda_stream)
+        sent = torch.cuda.Event()
+        sent.record(self.ring_stream)
+        self._ids_sent[slot] = sent
+
+    def recv_ids(self, n_ids: int, device) -> "PendingIds":
+        from .comm import PendingIds
+        if n_ids > self.max_ids:
+            raise ValueError(f"{n_ids} sampled ids exceed the ring slot ({self.max_ids})")
+        cur = torch.cuda.current_stream(self.device)
+        n = self._ids_rx_n
+        self._ids_rx_n += 1
+        slot = n % self.id_slots
+        rs = self.ring_stream
+        # the slot's previous ids: consumed by device work enqueued before now (lookahead gathers)
+        # and by their host copy
+        free = torch.cuda.Event()
+        free.record(cur)
+        rs.wait_event(free)
+        old = self._ids_users[slot]
+        if old is not None and old._host_ev is not None:
+            rs.wait_event(old._host_ev)
+        buf = self.ids_rx[slot, :n_ids]
+        if self.loopback:
+            tslot, tn, ready = self._ids_deferred.pop(0)
+            if tn != n_ids:
+                raise RuntimeError(f"loopback ids mismatch: sent {tn}, receiving {n_ids}")
+            rs.wait_event(ready)
+            self.ring_out.sendrecv(self.ids_tx[tslot].data_ptr(), tn * 4, 0, buf.data_ptr(), n_ids * 4, 0,
+                                   rs.cuda_stream)
+            sent = torch.cuda.Event()
+            sent.record(rs)
+            self._ids_sent[tslot] = sent
+        else:
+            self.ring_in.recv(buf.data_ptr(), n_ids * 4, 0, rs.cuda_stream)
+        landed = torch.cuda.Event()
+        landed.record(rs)
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(device=self.device)
+        p = PendingIds(buf, ready=landed, copy_stream=self._copy_stream, timeout_s=self.timeout_s)
+        self._ids_users[slot] = p
+        return p
+
+    def _comms(self):
+        return list({id(c): c for c in (self.comm_in, self.comm_out, self.ring_in, self.ring_out)
+                     if c is not None}.values())
+
+    def status(self) -> str:
+        """"" when every communicator is healthy, else the first communicator error."""
+        for c in self._comms():
+            if c is not None:
+                s = c.status()
+                if s and s != "in_progress":
+                    return s
+        return ""
 
     def drain(self):
         super().drain()
-        self.comm_stream.synchronize()
-        self._inflight.clear()
+        for s in (self.send_stream, self.recv_stream, self.ring_stream):
+            if s is not None:
+                s.synchronize()
 
     def abort(self):
-        self.comm.abort()
+        """ncclCommAbort on every communicator of this stage: kernels still waiting on a dead
+        peer return, so the process can tear down (membership change)."""
+        for c in self._comms():
+            c.abort()
+
+    def close(self):
+        self.drain()
+        for c in self._comms():
+            c.destroy()
+        self.comm_in = self.comm_out = self.ring_in = self.ring_out = None

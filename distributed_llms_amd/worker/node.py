@@ -452,7 +452,9 @@ class WorkerNode:
             transport = make_transport(list(range(world)), stage_idx, ctx.ctrl_group, ctx.data_group, self.device,
                                        ctx.ring_group,
                                        hop=(max(ecfg.max_prefill_tokens, ecfg.max_batch), width,
-                                            stage.dtype, inflight_window(ecfg, world, stage.device)))
+                                            stage.dtype, inflight_window(ecfg, world, stage.device)),
+                                       kind=ecfg.transport, timeout_s=ecfg.comm_timeout_s)
+            self._transport = transport
             if stage_idx == 0:
                 bm = make_block_manager(nb, ecfg.kv_block_size)
                 self.driver = PipelineDriver(self.stage_runner, transport, ecfg, bm)
@@ -586,23 +588,25 @@ class WorkerNode:
             th.join(timeout=5)
         self._serve_thread = None
         self.stage_runner = None
+        tp = getattr(self, "_transport", None)
+        self._transport = None
+        if tp is not None and send_stop is False and hasattr(tp, "abort"):
+            # membership changed (a peer died or the master re-planned): ncclCommAbort on the
+            # communicators this stage owns (parallel/rccl_transport.py), so p2p still pending
+            # against a dead peer returns instead of hanging
+            try:
+                tp.abort()
+            except Exception as e:          # noqa: BLE001 - teardown continues regardless
+                log.warning("transport abort: %s", e)
         if self._dist_ctx is not None:
-            # membership changed (a peer died or the master re-planned): ABORT the communicators
-            # first (ncclCommAbort under RCCL) so collectives/p2p still pending against a dead
-            # peer return instead of hanging, then destroy; the next LOAD_SHARD re-initialises
+            # the control / default groups hold no pending p2p of the data plane any more;
+            # destroy them (the next LOAD_SHARD re-initialises)
             try:
                 import torch.distributed as dist
-                from torch.distributed import distributed_c10d as c10d
                 if dist.is_initialized():
-                    if send_stop is False and hasattr(c10d, "_abort_process_group"):
-                        try:
-                            c10d._abort_process_group()
-                        except Exception:
-                            pass
-                    if dist.is_initialized():
-                        dist.destroy_process_group()
-            except Exception:
-                pass
+                    dist.destroy_process_group()
+            except Exception as e:          # noqa: BLE001
+                log.warning("process group teardown: %s", e)
             self._dist_ctx = None
 
     def status(self) -> Dict[str, Any]:

@@ -348,8 +348,9 @@ def test_big_linear(cuda, m, n, k, splits, swiglu):
 
 # ---- gemm_pp: ping-pong 256-row-tile kernel (decode split-K, prefill grouped + SwiGLU)
 @pytest.mark.parametrize("m", [1, 77, 200, 256, 300, 777])
-@pytest.mark.parametrize("n,k,splits", [(6144, 4096, 1), (6144, 4096, 10), (4096, 14336, 16), (512, 96, 3)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 4])
+@pytest.mark.parametrize("n,k,splits", [(6144, 4096, 1), (6144, 4096, 10), (4096, 14336, 16), (512, 192, 3),
+                                        (512, 128, 2), (256, 320, 1)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_pp_linear(cuda, m, n, k, splits, variant):
     x, w = _bf(m, k), _bf(n, k, scale=0.05)
     y = gemm.linear_pp(x, w, splits=splits, variant=variant)
@@ -359,7 +360,7 @@ def test_pp_linear(cuda, m, n, k, splits, variant):
 
 @pytest.mark.parametrize("m", [64, 256, 1000])
 @pytest.mark.parametrize("inter,k,splits", [(14336, 4096, 1), (14336, 4096, 2), (384, 256, 1)])
-@pytest.mark.parametrize("variant", [0, 1, 4])
+@pytest.mark.parametrize("variant", [0, 1, 4, 5, 6])
 def test_pp_swiglu(cuda, m, inter, k, splits, variant):
     if variant & 1 == 0 and (2 * inter) % 256:
         pytest.skip("256-column tile needs 2I % 256 == 0")

@@ -32,7 +32,8 @@ def test_config_json_yaml_roundtrip_and_overrides(tmp_path):
 
 
 @pytest.mark.parametrize("bad", [{"dtype": "int8"}, {"kv_block_size": 24}, {"num_workers": 0},
-                                 {"max_batch": 0}, {"num_workers": 99}])
+                                 {"max_batch": 0}, {"num_workers": 99}, {"transport": "tcp"},
+                                 {"comm_timeout_s": 0}])
 def test_config_validation_rejects(bad):
     with pytest.raises(ValueError):
         EngineConfig(model="synthetic:tiny-llama", **bad).validate()
