@@ -156,6 +156,8 @@ def run_single(args):
     for r in range(args.warmup):
         round_(10_000 + r)
     sync()
+    if eng.runner is not None:
+        eng.runner.meter(True)
     tr = start_trace(args)
     lat = []
     t0 = time.perf_counter()
@@ -165,9 +167,10 @@ def run_single(args):
     sync()
     elapsed = time.perf_counter() - t0
     assert all(len(s.output) == args.gen_len for s in seqs)
-    extra = {"load_s": round(load_s, 1)}
+    extra = {"load_s": round(load_s, 1), "transport": "none",
+             "stage_busy_frac": [round(eng.runner.busy_seconds() / elapsed, 4) if eng.runner else None]}
     if tr is not None:
-        extra["stage_busy_frac"] = [finish_trace(args, tr, elapsed, 0)]
+        finish_trace(args, tr, elapsed, 0)
     emit(args, 1, elapsed, lat, extra)
 
 
