@@ -151,6 +151,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   constexpr int GA = BM * PBK * 2 / 1024 / 4, GB = BN * PBK * 2 / 1024 / 4;   // glds per wave per K-tile
   constexpr int G = GA + GB;
   constexpr bool NT = (VAR & 1) != 0, GROUPED = (VAR & 2) != 0;
+  constexpr bool PROF = (VAR & 4) != 0;                // diagnostic build: cycle stamps around B_t
   constexpr bool SWIGLU = MODE == 2;
   constexpr int OUTW = SWIGLU ? BN / 2 : BN;           // output tile width (elements)
   constexpr int OPITCH = OUTW + 8;                     // LDS output row pitch (elements): +16 B
@@ -276,6 +277,12 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
     // landed for every wave (RAW), and only then are the next tile's fragments read and this
     // slot re-staged.
     int slot = 0;                                      // ring slot of K-tile t
+    [[maybe_unused]] unsigned long long st0 = 0, sbt = 0, sbt0 = 0, rt0 = 0;
+    if constexpr (PROF) {
+      rt0 = __builtin_amdgcn_s_memrealtime();
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0) :: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
     for (int t = 0; t < nt; ++t) {
       const uint32_t cur = lds_base + (uint32_t)(slot * SLOT * 2);
       const int nslot = slot == NB - 1 ? 0 : slot + 1;
@@ -308,10 +315,20 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
           acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[c], fa1[r], acc[r][c], 0, 0, 0);
           if constexpr (i == SC::EB - 1) {
             // B_t: every read of this slot done (WAR), K-tile t + 1 landed for every wave (RAW)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (PROF)
+              asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sbt0) :: "memory");
+            else
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             pp_wait_n<G>(NB - 2);
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
+            if constexpr (PROF) {
+              __builtin_amdgcn_sched_barrier(0);
+              unsigned long long s1;
+              asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(s1) :: "memory");
+              sbt += s1 - sbt0;
+              __builtin_amdgcn_sched_barrier(0);
+            }
           }
           if constexpr (i >= SC::EB - 1 && (i - SC::EB + 1) % GE == 0 && (i - SC::EB + 1) / GE < G)
             piece(slot, t + NB, (i - SC::EB + 1) / GE);
@@ -326,6 +343,18 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
       }
       slot = nslot;
     }
+    if constexpr (PROF) {   // per wave: loop cycles, cycles in B_t (counter waits + barrier), K-tiles, 100 MHz ticks
+      unsigned long long st1;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1) :: "memory");
+      const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      const float vals[4] = {(float)(st1 - st0), (float)sbt, (float)nt, (float)(rt1 - rt0)};
+      if (lane < 4) P[((size_t)blockIdx.x * 4 + wv) * 4 + lane] = vals[lane & 3];
+    }
+  }
+  if constexpr (PROF) {                                // diagnostic build: no output
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
   }
 
   // ---- epilogue: accumulators -> LDS output image (8-byte writes) -> 16-byte row stores.
@@ -417,6 +446,13 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
     if (grp) { if (nt) DLLM_PP_GO(BN_, MODE_, 3); else DLLM_PP_GO(BN_, MODE_, 2); } \
     else { if (nt) DLLM_PP_GO(BN_, MODE_, 1); else DLLM_PP_GO(BN_, MODE_, 0); }     \
   } while (0)
+  if (variant & 8) {   // diagnostic: cycle stamps per wave into ws (4 floats per wave), no output
+    DLLM_HOST_CHECK(S == 1 && !swiglu && ws != 0 && grid * 16 <= ws_floats, "profile build: S == 1, ws >= 16 / block");
+    if (BN == 256) { if (grp) DLLM_PP_GO(256, 0, 6); else DLLM_PP_GO(256, 0, 4); }
+    else { if (grp) DLLM_PP_GO(128, 0, 6); else DLLM_PP_GO(128, 0, 4); }
+    DLLM_HIP_CHECK(hipGetLastError());
+    return 1;
+  }
   if (S == 1) {
     if (BN == 256) { if (swiglu) DLLM_PP_V(256, 2); else DLLM_PP_V(256, 0); }
     else { if (swiglu) DLLM_PP_V(128, 2); else DLLM_PP_V(128, 0); }

@@ -139,11 +139,13 @@ def init_distributed(pp: Optional[int] = None, backend: Optional[str] = None,
 
 def resolve_transport(kind: str, device: str, host_staged: bool) -> str:
     """The activation transport a stage uses: CPU stages and host-staged GPU stages always ride
-    torch.distributed (gloo); on GPUs "auto" is the native RCCL edge transport."""
-    if not str(device).startswith("cuda") or host_staged:
+    torch.distributed (gloo) -- or HIP IPC when asked for (stages sharing one GPU); on GPUs "auto"
+    is the native RCCL edge transport."""
+    if not str(device).startswith("cuda"):
         return "torch"
-    env = os.environ.get("DLLM_TRANSPORT", "")          # test / rehearsal override
-    kind = env or kind or "auto"
+    kind = os.environ.get("DLLM_TRANSPORT", "") or kind or "auto"    # env: test / rehearsal override
+    if host_staged:                     # stages sharing one GPU: HIP IPC if asked, else gloo
+        return "ipc" if kind == "ipc" else "torch"
     return "rccl" if kind == "auto" else kind
 
 

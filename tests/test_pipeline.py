@@ -304,3 +304,20 @@ def test_explicit_plan_knob(monkeypatch):
     monkeypatch.setenv("DLLM_PP_UNITS", "2:0,3;3,8")
     assert plan_units(cfg, 2).units == ((0, 3), (3, 8))
     assert plan_units(cfg, 1).num_stages == 1
+
+
+def test_transport_resolution(monkeypatch):
+    """Which activation transport a stage gets: CPU -> torch (gloo); stages sharing one GPU
+    (host-staged) -> gloo unless HIP IPC is asked for; separate GPUs -> native RCCL for "auto",
+    with DLLM_TRANSPORT overriding the config."""
+    from distributed_llms_amd.parallel.dist_engine import resolve_transport
+    monkeypatch.delenv("DLLM_TRANSPORT", raising=False)
+    assert resolve_transport("auto", "cpu", False) == "torch"
+    assert resolve_transport("auto", "cuda:0", True) == "torch"
+    assert resolve_transport("auto", "cuda:3", False) == "rccl"
+    assert resolve_transport("torch", "cuda:3", False) == "torch"
+    monkeypatch.setenv("DLLM_TRANSPORT", "ipc")
+    assert resolve_transport("auto", "cuda:0", True) == "ipc"
+    assert resolve_transport("auto", "cpu", False) == "torch"
+    monkeypatch.setenv("DLLM_TRANSPORT", "torch")
+    assert resolve_transport("rccl", "cuda:1", False) == "torch"

@@ -88,7 +88,17 @@ def _run_ranks(world, prompts, transport, rounds, fine="0"):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in range(world))
+    import queue
+    import time
+    res, deadline = {}, time.monotonic() + 240
+    while len(res) < world:             # fail fast (and loudly) when a rank dies instead of reporting
+        try:
+            r, o = q.get(timeout=2)
+            res[r] = o
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"stage process exited with {dead}"
+            assert time.monotonic() < deadline, "stage processes did not finish within 240 s"
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
