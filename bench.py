@@ -87,6 +87,11 @@ def _par_name(args, world):
     return name or f"dp{world}"
 
 
+def _knobs_changed():
+    from distributed_llms_amd import knobs
+    return knobs.changed()
+
+
 def emit(args, world, elapsed, lat, extra, global_batch=None):
     """global_batch = requests per round over the whole job (default batch x world)."""
     global_batch = global_batch or args.batch * world
@@ -103,6 +108,7 @@ def emit(args, world, elapsed, lat, extra, global_batch=None):
         "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.prompt_len + args.gen_len,
                    "prompt_len": args.prompt_len, "gen_len": args.gen_len,
                    "parallelism": _par_name(args, world)},
+        "kernel_knobs": _knobs_changed(),            # non-default kernel-dispatch knobs (none = defaults)
     }
     rec.update(extra)
     line = json.dumps(rec)

@@ -1,8 +1,8 @@
-"""Decode GEMM microbenchmark: hand-written skinny MFMA kernel vs hipBLASLt (torch).
-
-Reports per-shape time and effective weight-streaming bandwidth (weight bytes / time),
-interleaving the two implementations in one process (CDNA guide rule 24).
-    python bench/gemm_bench.py [--m 64] [--iters 50]
+"""Decode GEMM microbenchmark: the engine's hand-written wide-M MFMA kernel (gemm_wide.hip, plus
+gemm_sq.hip with --sq and extra variants) vs hipBLASLt (torch), cold (rotating > 768 MB of weight
+copies, in-engine-like) or --warm, each implementation graph-captured, interleaved in one process
+(CDNA guide rule 24).  Reports time, weight-streaming TB/s and TFLOP/s.
+    python bench/gemm_bench.py [--m 64 256] [--shapes qkv_8b gate_up_8b]
 """
 import argparse
 import os
@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import torch.nn.functional as F
 
-from distributed_llms_amd import ops
+from distributed_llms_amd import knobs, ops
 from distributed_llms_amd.ops import gemm
 
 SHAPES = {  # name: (N, K, swiglu)
@@ -39,56 +39,25 @@ def timeit(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--m", type=int, nargs="+", default=[1, 16, 64])
+    ap.add_argument("--m", type=int, nargs="+", default=[1, 16, 64, 256])
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
-    ap.add_argument("--tiled", action="store_true", help="compare the split-K tiled kernel instead")
-    ap.add_argument("--wide", action="store_true", help="three-way: wide-M kernel vs tiled kernel vs hipBLASLt")
     ap.add_argument("--warm", action="store_true", help="no cache flush between calls (in-engine-like)")
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--variants", type=int, nargs="*", default=[0],
-                    help="--wide: extra gemm_wide variants timed beside the default (1)")
-    ap.add_argument("--sq", action="store_true", help="--wide: also time the 256 x 256-tile gemm_sq kernel")
+                    help="extra gemm_wide variants timed beside the engine's choice")
+    ap.add_argument("--sq", action="store_true", help="also time the 256 x 256-tile gemm_sq kernel")
     ap.add_argument("--sq-alt", type=int, default=0, help="--sq: second gemm_sq variant timed (sq0)")
     a = ap.parse_args()
-    # a scratch buffer larger than the 256 MiB Infinity Cache to flush it between calls
-    flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
-    print(f"{'shape':12s} {'M':>4s} {'ours_us':>9s} {'ours_TB/s':>10s} {'blas_us':>9s} {'blas_TB/s':>10s} {'speedup':>8s}")
-    if a.wide:
-        return wide(a, flush)
-    for name in a.shapes:
-        n, k, sw = SHAPES[name]
-        w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
-        for m in a.m:
-            x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
-            if a.tiled:
-                ours = lambda: (flush.zero_(), gemm.linear_tiled(x, w, swiglu=sw))
-                blas = (lambda: (flush.zero_(), ops.silu_mul(F.linear(x, w)))) if sw else (lambda: (flush.zero_(), F.linear(x, w)))
-            elif sw:
-                ours = lambda: (flush.zero_(), gemm.linear_swiglu(x, w, force_skinny=True))
-                blas = lambda: (flush.zero_(), ops.silu_mul(F.linear(x, w)))
-            else:
-                ours = lambda: (flush.zero_(), gemm.linear(x, w, force_skinny=True))
-                blas = lambda: (flush.zero_(), F.linear(x, w))
-            base = timeit(lambda: flush.zero_(), a.iters)
-            for _ in range(3):
-                ours(); blas()
-            to, tb = [], []
-            for _ in range(3):
-                to.append(timeit(ours, a.iters) - base)
-                tb.append(timeit(blas, a.iters) - base)
-            to, tb = min(to), min(tb)
-            byt = n * k * 2
-            print(f"{name:12s} {m:4d} {to*1e6:9.1f} {byt/to/1e12:10.2f} {tb*1e6:9.1f} {byt/tb/1e12:10.2f} {tb/to:8.2f}",
-                  flush=True)
+    return wide(a)
 
 
-def wide(a, flush):
-    """Three-way comparison.  Cold = rotate through enough weight copies (> 768 MB) that every call
+def wide(a):
+    """Comparison.  Cold = rotate through enough weight copies (> 768 MB) that every call
     streams its weight from HBM, with no dirty flush buffer competing for write-back (in-engine-like:
     each layer's weights are read once per step).  --warm = one copy (MALL-resident)."""
-    print(f"{'shape':12s} {'M':>4s} {'wide_us':>8s} {'TB/s':>6s} {'TF':>6s} {'tiled_us':>8s} {'blas_us':>8s} "
-          f"{'vs_tiled':>8s} {'vs_blas':>8s}  ({'warm' if a.warm else 'cold, rotating weights'})")
+    print(f"{'shape':12s} {'M':>4s} {'wide_us':>8s} {'TB/s':>6s} {'TF':>6s} {'blas_us':>8s} "
+          f"{'vs_blas':>8s}  ({'warm' if a.warm else 'cold, rotating weights'})")
     for name in a.shapes:
         n, k, sw = SHAPES[name]
         copies = 1 if a.warm else max(2, -(-(768 << 20) // (n * k * 2)))
@@ -98,14 +67,13 @@ def wide(a, flush):
             # one HIP graph per implementation: `copies` back-to-back calls, each on its own weight
             # copy (launch overhead out of the measurement, like the engine's captured decode step)
             split = (a.splits or gemm.wide_splits(m, n, k, sw)) > 1
-            wv = gemm.WIDE_VARIANT_SPLIT if split else gemm.WIDE_VARIANT     # the engine's choice
+            wv = knobs.K.wide_variant_split if split else knobs.K.wide_variant     # the engine's choice
             impls = {
                 "wide": lambda w: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=wv),
                 **{f"v{v}": (lambda w, v=v: gemm.linear_wide(x, w, splits=a.splits, swiglu=sw, variant=v))
                    for v in a.variants},
                 **({"sq": lambda w: gemm.linear_sq(x, w, swiglu=sw, variant=4),
                     "sq0": lambda w: gemm.linear_sq(x, w, swiglu=sw, variant=a.sq_alt)} if a.sq and n % 256 == 0 else {}),
-                "tiled": lambda w: gemm.linear_tiled(x, w, swiglu=sw),
                 "blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w)),
             }
             reps = max(copies, 8)
@@ -131,7 +99,7 @@ def wide(a, flush):
             t = {key: min(v) for key, v in res.items()}
             byt, fl_ = n * k * 2, 2.0 * m * n * k
             print(f"{name:12s} {m:4d} {t['wide']*1e6:8.1f} {byt/t['wide']/1e12:6.2f} {fl_/t['wide']/1e12:6.0f} "
-                  f"{t['tiled']*1e6:8.1f} {t['blas']*1e6:8.1f} {t['tiled']/t['wide']:8.2f} {t['blas']/t['wide']:8.2f} "
+                  f"{t['blas']*1e6:8.1f} {t['blas']/t['wide']:8.2f} "
                   + " ".join(f"v{v} {t[f'v{v}']*1e6:6.1f}" for v in a.variants)
                   + (f" sq {t['sq']*1e6:6.1f} ({t['wide']/t['sq']:.2f}x) sq0 {t['sq0']*1e6:6.1f}" if "sq" in t else ""),
                   flush=True)

@@ -1,12 +1,13 @@
-"""Cycle stamps inside gemm_pp (diagnostic build, variant bit 3): where a K-tile's cycles go.
+"""Cycle stamps inside gemm_pp (diagnostic build, variant bit 3): where a workgroup's time goes.
 
-Per wave: loop cycles, cycles spent in the once-per-K-tile block B_t (counted vmcnt wait for the
-next K-tile's LDS-DMA + s_barrier), and K-tiles; the rest of the loop is the MFMA stream with its
-counted LDS waits.  Ideal MFMA time per K-tile = 2 x RT x CT x 16 cycles (v_mfma_f32_16x16x32_bf16).
+Per wave: main-loop cycles, cycles spent in the once-per-K-tile block B_t (counted vmcnt wait for
+the next K-tile's LDS-DMA + s_barrier) and K-tiles; the rest of the loop is the MFMA stream with
+its counted LDS waits.  Ideal MFMA time per K-tile = 2 x RT x CT x 16 cycles
+(v_mfma_f32_16x16x32_bf16).  The kernel time of the normal build is printed beside it, and the
+sum of workgroup loop spans / 256 CUs (what the loops alone would take if the CUs never idled).
 
-    python bench/pp_stamps.py [--m 32768] [--n 14336] [--k 4096] [--variant 4]
+    python bench/pp_stamps.py
 """
-import argparse
 import os
 import statistics
 import sys
@@ -15,65 +16,61 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
-from distributed_llms_amd.ops import _ext
+from distributed_llms_amd.ops import gemm
+
+CASES = [  # name, M, N, K, swiglu, splits, variant
+    ("gate_up dec", 256, 28672, 4096, True, 1, 1), ("gate_up dec", 256, 28672, 4096, True, 2, 0),
+    ("gate_up dec", 256, 28672, 4096, True, 1, 0),
+    ("down dec", 256, 4096, 14336, False, 8, 1), ("down dec", 256, 4096, 14336, False, 16, 0),
+    ("qkv dec", 256, 6144, 4096, False, 5, 1), ("qkv dec", 256, 6144, 4096, False, 10, 0),
+    ("gate pf", 8192, 14336, 4096, False, 1, 4), ("gate pf", 8192, 14336, 4096, False, 1, 5),
+]
+
+
+def timed(fn, it=10):
+    ts = []
+    for _ in range(it):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3)
+    return statistics.median(ts)
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--m", type=int, nargs="+", default=[32768, 8192, 256])
-    ap.add_argument("--n", type=int, default=14336)
-    ap.add_argument("--k", type=int, default=4096)
-    ap.add_argument("--variant", type=int, nargs="+", default=[4, 1, 5])
-    a = ap.parse_args()
     torch.manual_seed(0)
-    kern = _ext.kernels()
-    w = (torch.randn(a.n, a.k, device="cuda") * 0.02).to(torch.bfloat16)
-    for m in a.m:
-        x = torch.randn(m, a.k, device="cuda").to(torch.bfloat16)
-        y = torch.empty(m, a.n, dtype=torch.bfloat16, device="cuda")
-        for v in a.variant:
-            bn = 128 if v & 1 else 256
-            grid = (a.n // bn) * ((m + 255) // 256)
-            ws = torch.zeros(grid * 16, dtype=torch.float32, device="cuda")
-            st = torch.cuda.current_stream().cuda_stream
-            for _ in range(20):        # warm clocks; the last launch's stamps are read
-                kern.gemm_pp(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, a.n, a.k, 1, 0,
-                             v | 8, st)
-            torch.cuda.synchronize()
-            s = ws.view(-1, 4).cpu()
+    dev = torch.device("cuda")
+    for name, m, n, k, sw, s, v in CASES:
+        copies = max(1, -(-(768 << 20) // (n * k * 2))) if m <= 256 else 1
+        ws_ = [(torch.randn(n, k, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+        x = torch.randn(m, k, device=dev).to(torch.bfloat16)
+        it = iter(range(10 ** 9))
 
-            def launch(var):
-                kern.gemm_pp(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, a.n, a.k, 1, 0,
-                             var, st)
-
-            def time_us(var, it=10):
-                ts = []
-                for _ in range(it):
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    launch(var)
-                    e1.record()
-                    e1.synchronize()
-                    ts.append(e0.elapsed_time(e1) * 1e3)
-                return statistics.median(ts)
-            t_diag, t_real = time_us(v | 8), time_us(v)
-            s2 = ws.view(-1, 4).cpu()
-            wg_us = (s2[:, 3] * 10.0 / 1e3).view(-1, 4).max(dim=1).values
-            print(f"   kernel us: diagnostic (no epilogue) {t_diag:.1f}, real {t_real:.1f}; grid {grid} WGs = "
-                  f"{grid / 256:.2f} per CU; sum of WG loop spans / 256 = {wg_us.sum().item() / 256:.1f} us; "
-                  f"TF real {2.0 * m * a.n * a.k / t_real / 1e6:.0f}", flush=True)
-            tot, bt, nt, rt = s[:, 0], s[:, 1], s[:, 2], s[:, 3]
-            rt_ns = rt * 10.0
-            ghz = statistics.median((tot / rt_ns).tolist())
-            rtile = 8 * (bn // 32)
-            ideal = 2 * rtile * 16
-            per = (tot / nt).tolist()
-            frac = (bt / tot).tolist()
-            print(f"M={m:6d} N={a.n} K={a.k} variant={v} BN={bn}: clock {ghz:.2f} GHz | cycles/K-tile median "
-                  f"{statistics.median(per):7.0f} (ideal {ideal}, {ideal / statistics.median(per) * 100:.0f} %) "
-                  f"p10 {sorted(per)[len(per) // 10]:.0f} p90 {sorted(per)[9 * len(per) // 10]:.0f} | B_t share "
-                  f"median {statistics.median(frac) * 100:.1f} % p90 {sorted(frac)[9 * len(frac) // 10] * 100:.1f} % | "
-                  f"loop us median {statistics.median(rt_ns.tolist()) / 1e3:.1f}", flush=True)
+        def run(var):
+            return gemm.linear_pp(x, ws_[next(it) % copies], splits=s, swiglu=sw, variant=var)
+        for _ in range(10):
+            run(v | 8)
+        torch.cuda.synchronize()
+        bn = 128 if v & 1 else 256
+        grid = (n // bn) * (-(-m // 256)) * s
+        rec = gemm._workspace(dev)[-grid * 512:].view(grid * 4, 128)[:, :4].cpu()
+        tot, bt, nt, rt = rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3]
+        rt_ns = rt * 10.0
+        ghz = statistics.median((tot / rt_ns).tolist())
+        ideal = 2 * 8 * (bn // 32) * 16
+        per = (tot / nt).tolist()
+        frac = (bt / tot).tolist()
+        t_real = timed(lambda: run(v))
+        wg_us = (rt_ns / 1e3).view(-1, 4).max(dim=1).values
+        print(f"{name:12s} M={m:5d} N={n:5d} K={k:5d} S={s:2d} BN={bn} var={v}: kernel {t_real:7.1f} us "
+              f"({2.0 * m * n * k / t_real / 1e6:5.0f} TF) | WG loop median {statistics.median(wg_us.tolist()):6.1f} us, "
+              f"sum/256 {wg_us.sum().item() / 256:7.1f} us | clock {ghz:.2f} GHz | cycles/K-tile "
+              f"{statistics.median(per):6.0f} (ideal {ideal}, {ideal / statistics.median(per) * 100:3.0f} %) | "
+              f"B_t share {statistics.median(frac) * 100:4.1f} %", flush=True)
+        del ws_, x
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

@@ -39,8 +39,7 @@ def main():
         flops = 4.0 * b * hq * d * L * (L + 1) / 2
         row = []
         for ver in a.versions:
-            os.environ["DLLM_PREFILL_ATTN"] = ver
-            f = lambda: ops.paged_attention_prefill(q, k, v, bt, cu, sl, d ** -0.5)
+            f = lambda: ops.paged_attention_prefill(q, k, v, bt, cu, sl, d ** -0.5, version=int(ver))
             f()
             ts = []
             for _ in range(a.reps):

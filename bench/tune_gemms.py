@@ -5,7 +5,7 @@ engine issues, written to an in-tree CSV that the engine loads read-only at star
 Shapes per model: the decode graph buckets (M = EngineConfig.graph_batch_sizes) and the prefill
 chunk (M = --prefill-tokens) for qkv / o / gate_up / down, plus the LM head at every decode
 bucket.  Shapes the engine routes to its own HIP kernels are tuned anyway (cheap) so the
-DLLM_GEMM=blas fallback is tuned too.
+library fallback (kernel knob wide=none) is tuned too.
 
     python bench/tune_gemms.py --models llama3-8b llama3-70b mixtral-8x7b
 """

@@ -15,7 +15,7 @@ from __future__ import annotations
 import dataclasses
 import json
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Any, Dict, Optional
 
 
@@ -243,6 +243,9 @@ class EngineConfig:
     transport: str = "auto"
     comm_timeout_s: float = 600.0      # a pipeline peer silent this long -> the rank raises (no hang)
     graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256)
+    # kernel-dispatch overrides ({knob: value}, distributed_llms_amd/knobs.py), applied when a stage
+    # runner is built; empty = the measured defaults
+    kernel_knobs: Dict[str, Any] = field(default_factory=dict)
     host: str = "0.0.0.0"
     port: int = 65432
     worker_port: int = 65433
@@ -266,6 +269,10 @@ class EngineConfig:
             raise ValueError(f"transport {self.transport!r} (auto, rccl, torch, ipc)")
         if self.comm_timeout_s <= 0:
             raise ValueError("comm_timeout_s must be > 0")
+        from . import knobs
+        unknown = set(self.kernel_knobs) - set(knobs.as_dict())
+        if unknown:
+            raise ValueError(f"unknown kernel_knobs {sorted(unknown)}")
         if self.max_batch < 1 or self.max_seq_len < 2:
             raise ValueError("max_batch/max_seq_len")
         cfg = get_model_config(self.model if self.shard_dir is None else self.shard_dir)

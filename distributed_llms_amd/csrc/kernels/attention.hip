@@ -14,7 +14,6 @@
 #include "common.h"
 #include "launchers.h"
 
-#include <cstdlib>
 
 namespace dllm {
 
@@ -845,7 +844,7 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
 void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
                              uintptr_t block_tables, uintptr_t cu_seqlens_q, uintptr_t seq_lens, int batch,
                              int hq, int hkv, int d, int block_size, int max_blocks, int max_q_len, float scale,
-                             uintptr_t stream) {
+                             int version, uintptr_t stream) {
   DLLM_HOST_CHECK(block_size == kBS, "paged attention requires block_size 32");
   DLLM_HOST_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
   DLLM_HOST_CHECK(hq % hkv == 0, "Hq % Hkv");
@@ -853,10 +852,10 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
   const int G = hq / hkv;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float sl2 = scale * 1.4426950408889634f;
-  const char* pe = getenv("DLLM_PREFILL_ATTN");   // A/B and tests; eager (prefill) path only
-  // default 4: the LDS-shared kernel (bench/prefill_attn_bench.py: 1.6-1.7x v3 from 128- to
-  // 8192-token prompts); 5 = the same at 4 tiles per wave (one wave per SIMD: slower)
-  int version = (pe && pe[0] >= '1' && pe[0] <= '5') ? pe[0] - '0' : 4;
+  // version (knobs.prefill_attn): 4 = the LDS-shared kernel (default; bench/prefill_attn_bench.py:
+  // 1.6-1.7x v3 from 128- to 8192-token prompts); 5 = the same at 4 tiles per wave (one wave per
+  // SIMD: slower); 1-3 = the earlier register-tiled kernels (tests)
+  DLLM_HOST_CHECK(version >= 1 && version <= 5, "prefill attention version 1..5");
   // the LDS kernel stages the block ids of a whole sequence: fall back beyond 32k context
   if (version >= 4 && max_blocks > kPfMaxChunks) version = 3;
   if (d == 128)

@@ -18,8 +18,6 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("silu_mul", &dllm::silu_mul);
   m.def("argmax", &dllm::argmax);
   m.def("add_inplace", &dllm::add_inplace);
-  m.def("gemm_skinny", &dllm::gemm_skinny);
-  m.def("gemm_tiled", &dllm::gemm_tiled);
   m.def("moe_route", &dllm::moe_route);
   m.def("moe_grouped_gemm", &dllm::moe_grouped_gemm);
   m.def("splitk_add_rms_norm", &dllm::splitk_add_rms_norm);
@@ -32,7 +30,6 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("splitk_add_rms_norm_q8", &dllm::splitk_add_rms_norm_q8);
   m.def("gemm_sq", &dllm::gemm_sq);
   m.def("gemm_pp", &dllm::gemm_pp);
-  m.def("gemm_big", &dllm::gemm_big);
   m.def("moe_combine", &dllm::moe_combine);
   m.def("moe_wide_gemm", &dllm::moe_wide_gemm);
   m.def("moe_router_route", &dllm::moe_router_route);

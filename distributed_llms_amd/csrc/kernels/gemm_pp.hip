@@ -143,7 +143,7 @@ __device__ __forceinline__ int pp_b_row(int r, int n_t, int half) {
 template <int BN, int MODE, int VAR>
 __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                          bf16* __restrict__ C, float* __restrict__ P, int M, int N,
-                                                         int K, int ks_per_split, int nsplit) {
+                                                         int K, int ks_per_split, int nsplit, float* __restrict__ D) {
   constexpr int BM = 256, TM = 128, TN = BN / 2;       // 4 waves as 2 (M) x 2 (N)
   constexpr int RT = TM / 16, CT = TN / 16;            // 16 x 16 fragments per wave: 8 x 8 or 8 x 4
   constexpr int SLOT = (BM + BN) * PBK;                // bf16 elements per ring slot (one K-tile)
@@ -349,14 +349,10 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
       const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_s_waitcnt(0xC07F);
       const float vals[4] = {(float)(st1 - st0), (float)sbt, (float)nt, (float)(rt1 - rt0)};
-      if (lane < 4) P[((size_t)blockIdx.x * 4 + wv) * 4 + lane] = vals[lane & 3];
+      float* rec = D + ((size_t)blockIdx.x * 4 + wv) * 128;
+      if (lane < 4) rec[lane] = vals[lane & 3];
     }
   }
-  if constexpr (PROF) {                                // diagnostic build: no output
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
-  }
-
   // ---- epilogue: accumulators -> LDS output image (8-byte writes) -> 16-byte row stores.
   // acc[rt][ct] lane l holds C[row wm*TM + rt*16 + (l & 15)][col wn*TN + ct*16 + 4*(l >> 4) + v]
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -440,19 +436,21 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
   const bool grp = (variant & 4) != 0 && S == 1 && mtiles > 1;
 #define DLLM_PP_GO(BN_, MODE_, VAR_)                                                                     \
   hipLaunchKernelGGL((gemm_pp_kernel<BN_, MODE_, VAR_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, \
-                     (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kps, S)
+                     (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kps, S, dbg)
+  // variant bit 3: diagnostic build -- per-wave cycle stamps (loop, B_t waits) into the LAST
+  // grid x 512 floats of ws (after the slabs); output as usual
+  const bool prof = (variant & 8) != 0;
+  float* dbg = nullptr;
+  if (prof) {
+    DLLM_HOST_CHECK(ws != 0 && grid * 512 + (S > 1 ? (long)S * M * N : 0) <= ws_floats, "profile build: ws too small");
+    dbg = (float*)ws + (ws_floats - grid * 512);
+  }
 #define DLLM_PP_V(BN_, MODE_)                                        \
   do {                                                               \
-    if (grp) { if (nt) DLLM_PP_GO(BN_, MODE_, 3); else DLLM_PP_GO(BN_, MODE_, 2); } \
+    if (prof) { if (grp) DLLM_PP_GO(BN_, MODE_, 6); else DLLM_PP_GO(BN_, MODE_, 4); } \
+    else if (grp) { if (nt) DLLM_PP_GO(BN_, MODE_, 3); else DLLM_PP_GO(BN_, MODE_, 2); } \
     else { if (nt) DLLM_PP_GO(BN_, MODE_, 1); else DLLM_PP_GO(BN_, MODE_, 0); }     \
   } while (0)
-  if (variant & 8) {   // diagnostic: cycle stamps per wave into ws (4 floats per wave), no output
-    DLLM_HOST_CHECK(S == 1 && !swiglu && ws != 0 && grid * 16 <= ws_floats, "profile build: S == 1, ws >= 16 / block");
-    if (BN == 256) { if (grp) DLLM_PP_GO(256, 0, 6); else DLLM_PP_GO(256, 0, 4); }
-    else { if (grp) DLLM_PP_GO(128, 0, 6); else DLLM_PP_GO(128, 0, 4); }
-    DLLM_HIP_CHECK(hipGetLastError());
-    return 1;
-  }
   if (S == 1) {
     if (BN == 256) { if (swiglu) DLLM_PP_V(256, 2); else DLLM_PP_V(256, 0); }
     else { if (swiglu) DLLM_PP_V(128, 2); else DLLM_PP_V(128, 0); }

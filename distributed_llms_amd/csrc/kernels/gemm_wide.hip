@@ -618,7 +618,7 @@ void moe_wide_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uint
   DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ntiles = mode == 1 ? (N / 2) / 64 : N / WBN;
-  static const int nt = [] { const char* e = getenv("DLLM_MOE_WIDE_NT"); return e ? atoi(e) : 1; }();
+  constexpr int nt = 1;   // expert weights are read once per step: nontemporal
   if (mode == 1)
     hipLaunchKernelGGL((moe_wide_kernel<true, false>), dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
                        (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt,
@@ -641,7 +641,7 @@ void moe_wide_gemm_fp8(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, 
   DLLM_HOST_CHECK(sa != 0 && wscale != 0, "fp8 grouped GEMM needs both scale vectors");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ntiles = mode == 1 ? (N / 2) / 64 : N / WBN;
-  static const int nt = [] { const char* e = getenv("DLLM_MOE_WIDE_NT"); return e ? atoi(e) : 1; }();
+  constexpr int nt = 1;   // expert weights are read once per step: nontemporal
   if (mode == 1)
     hipLaunchKernelGGL((moe_wide_kernel<true, true>), dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
                        (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt,

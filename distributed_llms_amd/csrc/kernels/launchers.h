@@ -22,11 +22,6 @@ void silu_mul(uintptr_t out, uintptr_t gu, int tokens, int inter, uintptr_t stre
 void add_inplace(uintptr_t a, uintptr_t b, long n, uintptr_t stream);
 void argmax(uintptr_t out, uintptr_t logits, int rows, int vocab, long row_stride, uintptr_t stream);
 
-void gemm_skinny(uintptr_t y, uintptr_t x, uintptr_t w, uintptr_t bias, int M, int N, int K, int mode,
-                 uintptr_t stream);
-
-void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t ws, long ws_floats, int M, int N,
-                int K, int splits, int mode, uintptr_t stream);
 void splitk_add_rms_norm(uintptr_t y, uintptr_t residual, uintptr_t ws, int S, int M, int N, uintptr_t w, float eps,
                          uintptr_t stream);
 void splitk_reduce(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M, int N, uintptr_t stream);
@@ -37,8 +32,6 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
 int gemm_wide_fp8(uintptr_t c, uintptr_t a, uintptr_t a_scale, uintptr_t b, uintptr_t b_scale, uintptr_t ws,
                   long ws_floats, int M, int N, int K, int splits, int mode, int variant, uintptr_t stream);
 void quant_fp8_rows(uintptr_t q, uintptr_t scale, uintptr_t x, int M, int K, uintptr_t stream);
-int gemm_big(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
-             int mode, uintptr_t stream);
 int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream);
 int gemm_sq(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
@@ -69,6 +62,6 @@ void paged_attention_decode_rope(uintptr_t out, uintptr_t qkv, uintptr_t positio
 void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
                              uintptr_t block_tables, uintptr_t cu_seqlens_q, uintptr_t seq_lens, int batch,
                              int hq, int hkv, int d, int block_size, int max_blocks, int max_q_len, float scale,
-                             uintptr_t stream);
+                             int version, uintptr_t stream);
 
 }  // namespace dllm

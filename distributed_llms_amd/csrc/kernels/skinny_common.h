@@ -1,5 +1,5 @@
-// Building blocks of the weight-streaming (small-M) MFMA GEMMs: dense decode projections
-// (gemm_skinny.hip) and the Mixtral grouped expert GEMM (moe.hip).
+// Building blocks of the weight-streaming (small-M) MFMA GEMM: the Mixtral grouped expert GEMM
+// for few tokens per expert (moe.hip).
 //
 // v_mfma_f32_16x16x32_bf16 fragments, k permuted inside each 128-wide k-group identically
 // for X and W (a dot product is order-invariant): load i of lane (r, g) reads elements

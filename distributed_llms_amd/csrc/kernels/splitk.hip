@@ -1,134 +1,15 @@
-// Large-batch decode GEMM (M = 64..512): C[M,N] = A[M,K] . B[N,K]^T, bf16 in, f32 accumulate.
-//
-// Why: at these M hipBLASLt's tiles leave most of the 256 CUs idle for N <= 6144
-// (qkv / o / down run at 1.1-2 TB/s and 0.3-0.5 PF, bench/blas_graph_probe.py).  This kernel
-// splits K across workgroups so (N/128) x (M/128) x S fills the chip, and reduces the S f32
-// partial slabs in a second, fully parallel pass (optionally with the SwiGLU epilogue).
-//
-// Structure (the guide's minimum 2-phase LDS pipeline, gfx950):
-//  * tile 128 x 128 x 64, 256 threads = 4 waves in 2 x 2, wave tile 64 x 64 = 4 x 4
-//    v_mfma_f32_16x16x32_bf16 accumulators (64 VGPRs);
-//  * global -> LDS with global_load_lds_dwordx4 (16 B per lane, lane-linear 1 KiB per
-//    wave-instruction = 8 rows x 128 B); the bank-conflict swizzle (16-B chunk c of row r
-//    stored at c ^ ((r >> 1) & 7)) is applied on the per-lane SOURCE address and on the
-//    ds_read address (guide rule 21), which makes the 16-lane ds_read_b128 groups
-//    conflict-free;
-//  * double-buffered LDS (64 KiB): stage tile t+1 before the MFMAs of tile t, one
-//    vmcnt(0) + barrier per K-tile.
+// Split-K slab consumers: every split-K GEMM (gemm_wide / gemm_sq / gemm_pp, MoE) leaves S partial
+// slabs (f16 x 2^-6 by default, common.h DLLM_PART_TYPE) in the per-stream workspace; these kernels
+// turn them into the next op's input without another round trip:
+//  * splitk_add_rms_norm(_q8): reduce + residual add + RMSNorm (+ per-token e4m3 for a W8A8 GEMM),
+//    the o / down projections' epilogue in every Llama block;
+//  * splitk_reduce(_ex): plain reduce (+bias) or reduce + SwiGLU.
+// Slab counts 2..8 are compile-time instantiations: all of a vector's slab loads are in flight
+// before the first add (nontemporal: slabs are read once).
 #include "common.h"
 #include "launchers.h"
 
-#include <cstdlib>
-
 namespace dllm {
-
-typedef __attribute__((address_space(3))) void* lds_vptr;
-typedef __attribute__((address_space(1))) void* glb_vptr;
-
-constexpr int TBM = 128, TBN = 128, TBK = 64;
-constexpr int TILE_ELEMS = TBM * TBK;   // 8192 bf16 = 16 KiB
-
-__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-
-template <bool SPLIT>
-__global__ void __launch_bounds__(256, 2) gemm_tiled_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                            bf16* __restrict__ C, float* __restrict__ P, int M, int N,
-                                                            int K, int k_per_split) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE_ELEMS];   // [buf][A|B][128][64]
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
-  // 1-D grid, XCD-aware: hardware dispatches block b to XCD b % 8, so logical tile
-  // (b % 8) * (total / 8) + b / 8 gives each XCD a contiguous run of logical ids; M is the
-  // fastest logical axis, so the M tiles that share a W tile run back-to-back on ONE XCD and
-  // the second reads W from that XCD's L2 instead of HBM.
-  const int mtiles = (M + TBM - 1) / TBM, total = gridDim.x;
-  int b = blockIdx.x;
-  if ((total & 7) == 0) b = (b & 7) * (total >> 3) + (b >> 3);
-  const int m_t = b % mtiles, rest = b / mtiles;
-  const int nsplit = total / (mtiles * (N / TBN));
-  const int split = rest % nsplit, n_t = rest / nsplit;
-  const int n0 = n_t * TBN, m0 = m_t * TBM;
-  const int kb = split * k_per_split;
-  const int ke = min(K, kb + k_per_split);
-  const int nt = max(0, (ke - kb) / TBK);
-
-  // staging addresses (per lane): instruction i = wv*4 + j covers tile rows 8i .. 8i+7
-  const bf16* srcA[4];
-  const bf16* srcB[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int i = wv * 4 + j;
-    const int r = 8 * i + (lane >> 3);
-    const int c = swz_chunk(r, lane & 7);
-    srcA[j] = A + (size_t)min(m0 + r, M - 1) * K + c * 8;
-    srcB[j] = B + (size_t)(n0 + r) * K + c * 8;
-  }
-  auto stage = [&](int buf, int k0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = wv * 4 + j;
-      __builtin_amdgcn_global_load_lds((glb_vptr)(srcA[j] + k0), (lds_vptr)(smem + (buf * 2 + 0) * TILE_ELEMS + i * 512),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((glb_vptr)(srcB[j] + k0), (lds_vptr)(smem + (buf * 2 + 1) * TILE_ELEMS + i * 512),
-                                       16, 0, 0);
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  if (nt > 0) {
-    stage(0, kb);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-      const int cur = t & 1;
-      if (t + 1 < nt) stage(cur ^ 1, kb + (t + 1) * TBK);
-      const bf16* sa = smem + (cur * 2 + 0) * TILE_ELEMS;
-      const bf16* sb = smem + (cur * 2 + 1) * TILE_ELEMS;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 fa[4], fb[4];
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          const int row = wm * 64 + rt * 16 + fr;
-          fa[rt] = *reinterpret_cast<const bf16x8*>(sa + row * TBK + swz_chunk(row, 4 * s + fq) * 8);
-        }
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          const int row = wn * 64 + ct * 16 + fr;
-          fb[ct] = *reinterpret_cast<const bf16x8*>(sb + row * TBK + swz_chunk(row, 4 * s + fq) * 8);
-        }
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct)
-            acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rt], fb[ct], acc[rt][ct], 0, 0, 0);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  }
-  // epilogue: lane holds col (lane&15), rows 4*(lane>>4)+i of each 16x16 tile
-#pragma unroll
-  for (int rt = 0; rt < 4; ++rt) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + rt * 16 + 4 * fq + i;
-      if (m >= M) continue;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const int n = n0 + wn * 64 + ct * 16 + fr;
-        if (SPLIT) part_store(P, ((size_t)split * M + m) * N + n, acc[rt][ct][i]);
-        else C[(size_t)m * N + n] = f2bf(acc[rt][ct][i]);
-      }
-    }
-  }
-}
 
 // out[m, n] = sum_s P[s, m, n] (+ bias[n]);  swiglu: out[m, j] = silu(sum P[m, j]) * sum P[m, I + j]
 template <bool SWIGLU, int SC>
@@ -268,35 +149,14 @@ void splitk_add_rms_norm_q8(uintptr_t y, uintptr_t residual, uintptr_t ws, int S
   DLLM_HOST_CHECK(S >= 1 && M >= 0, "S >= 1");
   if (M == 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  // DLLM_SKN_THREADS=512: 512-thread workgroups (8 waves per row, one vector per thread at hidden
-  // 4096); the sum of squares is then reduced over 8 wave partials, so the output is no longer
-  // bit-identical to splitk_reduce + rms_norm_kernel (A/B knob, profiles/wide_gemm.md).  Only
-  // instantiated for S == 8 slabs and 2048 < hidden <= 4096 (256 < N/8 <= 512); every other shape
-  // keeps the 256-thread kernel.  Read once per process (first call).
-  // tests/test_gemm_gpu.py::test_skn_512_threads covers it in a subprocess.
-  static const int nth = [] {
-    const char* e = getenv("DLLM_SKN_THREADS");
-    return e && atoi(e) == 512 ? 512 : 256;
-  }();
-  const int nvec = N / 8;
-  const int bth = (nth == 512 && nvec > 256 && nvec <= 512 && S == 8) ? 512 : 256;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(M), dim3(bth), 0, s, (bf16*)y, (bf16*)residual, (const float*)ws, S, M, N,
+    hipLaunchKernelGGL(kern, dim3(M), dim3(256), 0, s, (bf16*)y, (bf16*)residual, (const float*)ws, S, M, N,
                        (const bf16*)w, eps, (uint8_t*)q8, (float*)qs);
   };
-  if (bth == 512) {
-    go(splitk_add_rms_norm_kernel<1, 8, 512>);
-    DLLM_HIP_CHECK(hipGetLastError());
-    return;
-  }
-  static const bool const_slabs = [] {
-    const char* e = getenv("DLLM_SKN_CONST");
-    return !(e && e[0] == '0');
-  }();
+  const int nvec = N / 8;
 #define DLLM_SKN(MV)                                                   \
   do {                                                                 \
-    if (!const_slabs) go(splitk_add_rms_norm_kernel<MV, 0>);           \
-    else if (S == 8) go(splitk_add_rms_norm_kernel<MV, 8>);                 \
+    if (S == 8) go(splitk_add_rms_norm_kernel<MV, 8>);                 \
     else if (S == 4) go(splitk_add_rms_norm_kernel<MV, 4>);            \
     else if (S == 2) go(splitk_add_rms_norm_kernel<MV, 2>);            \
     else if (S == 3) go(splitk_add_rms_norm_kernel<MV, 3>);            \
@@ -313,7 +173,7 @@ void splitk_add_rms_norm_q8(uintptr_t y, uintptr_t residual, uintptr_t ws, int S
   DLLM_HIP_CHECK(hipGetLastError());
 }
 
-// plain split-K reduce of partials left by gemm_tiled(mode 2): out = bf16(sum_s P[s]) (+bias)
+// plain split-K reduce of the partial slabs a split GEMM left (mode 2 of gemm_wide / gemm_sq / gemm_pp): out = bf16(sum_s P[s]) (+bias)
 void splitk_reduce_ex(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M, int N, int swiglu,
                       uintptr_t stream) {
   DLLM_HOST_CHECK(N % (swiglu ? 8 : 4) == 0, "N alignment");
@@ -345,33 +205,6 @@ void splitk_reduce_ex(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M,
 
 void splitk_reduce(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M, int N, uintptr_t stream) {
   splitk_reduce_ex(out, ws, bias, S, M, N, 0, stream);
-}
-
-// mode 0: C[M,N] = A B^T (+bias);  mode 1 (SwiGLU): C[M, N/2] = silu(A Bg^T) * (A Bu^T), B = [Bg; Bu]
-void gemm_tiled(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t bias, uintptr_t ws, long ws_floats, int M, int N,
-                int K, int splits, int mode, uintptr_t stream) {
-  DLLM_HOST_CHECK(M >= 1, "M >= 1");
-  DLLM_HOST_CHECK(N % TBN == 0, "N must be a multiple of 128");
-  DLLM_HOST_CHECK(K % TBK == 0, "K must be a multiple of 64");
-  DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
-  DLLM_HOST_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");   // 2: leave partial slabs in ws, no reduce
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int kps = (K / TBK + splits - 1) / splits * TBK;
-  const int S = (K + kps - 1) / kps;
-  dim3 grid((N / TBN) * ((M + TBM - 1) / TBM) * S);
-  DLLM_HOST_CHECK(mode != 2 || S > 1, "mode 2 needs a K split");
-  if (S == 1 && mode == 0 && bias == 0) {
-    hipLaunchKernelGGL(gemm_tiled_kernel<false>, grid, dim3(256), 0, s, (const bf16*)a, (const bf16*)b, (bf16*)c,
-                       (float*)nullptr, M, N, K, kps);
-    DLLM_HIP_CHECK(hipGetLastError());
-    return;
-  }
-  DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
-  hipLaunchKernelGGL(gemm_tiled_kernel<true>, grid, dim3(256), 0, s, (const bf16*)a, (const bf16*)b, (bf16*)nullptr,
-                     (float*)ws, M, N, K, kps);
-  DLLM_HIP_CHECK(hipGetLastError());
-  if (mode == 2) return;
-  splitk_reduce_ex(c, ws, bias, S, M, N, mode == 1, stream);
 }
 
 }  // namespace dllm

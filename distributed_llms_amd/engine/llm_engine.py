@@ -9,14 +9,13 @@ from __future__ import annotations
 
 import collections
 import logging
-import os
 import time
 from typing import Iterable, List, Optional
 
 import numpy as np
 import torch
 
-from .. import _ext
+from .. import _ext, knobs
 from ..config import EngineConfig, resolve_device, torch_dtype
 from ..models.stage import ModelStage
 from .batch import build_host_batch
@@ -83,8 +82,8 @@ class LLMEngine:
         self.busy = [False] * self.num_slots
         # lookahead: issue a slot's next decode step before completing the one in flight (input
         # ids gathered on device from the in-flight step's samples), so the host's complete /
-        # schedule / build work overlaps the GPU instead of idling it (DLLM_LOOKAHEAD=0: off)
-        self.lookahead = gpu and os.environ.get("DLLM_LOOKAHEAD", "1") != "0" and self.tp is None
+        # schedule / build work overlaps the GPU instead of idling it (knobs.lookahead off: synchronous)
+        self.lookahead = gpu and knobs.K.lookahead and self.tp is None
         self.num_lookahead = 0
         if gpu:
             dev = self.stage.device

@@ -9,6 +9,7 @@ from typing import Optional
 
 import torch
 
+from .. import knobs
 from ..config import EngineConfig, ModelConfig, pipeline_slots
 from ..models.stage import KVCache, ModelStage
 from ..ops.tuning import enable_tuned_gemms
@@ -52,6 +53,8 @@ class StageRunner:
         self.stage = stage
         self.ecfg = ecfg
         self.tracer = get_tracer()
+        if ecfg.kernel_knobs:
+            knobs.update(ecfg.kernel_knobs)   # before any launch / graph capture
         if stage.device.type == "cuda":
             enable_tuned_gemms()          # before any graph capture fixes the GEMM solutions
         self.block_size = ecfg.kv_block_size

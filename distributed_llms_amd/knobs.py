@@ -1,0 +1,128 @@
+"""Kernel-dispatch knobs: every A/B switch of the GPU op layer, in one place.
+
+The defaults are the measured best on MI355X (each field cites its profile).  They change only
+through :func:`update` -- called with ``EngineConfig.kernel_knobs`` when an engine or a pipeline
+rank is built (so the values a run used are part of its config and of the bench JSON line) --
+or, for experiments, from ONE environment variable read once at import::
+
+    DLLM_KNOBS="wide_variant=1,defer_qkv=1"        # or a JSON object
+
+Nothing else in the package reads kernel switches from the environment.  The op layer reads
+``knobs.K.<field>`` at call time, so an update applies to every launch after it (HIP graphs
+captured before an update keep the dispatch they were captured with).
+
+Environment variables the package still reads (all documented in README "Environment"):
+DLLM_KNOBS, DLLM_TRACE, DLLM_ROCTX, DLLM_JSON_LOGS, DLLM_DEVICE, DLLM_DIST_ADDR, DLLM_TRANSPORT,
+DLLM_SHARE_GPU, DLLM_DATA_BACKEND, DLLM_PP_UNITS, DLLM_PP_FINE, DLLM_OFFLOAD_ARCH, DLLM_PART_TYPE,
+DLLM_TUNABLEOP_FILE.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+from dataclasses import dataclass
+from typing import Any, Dict, Mapping, Optional
+
+
+@dataclass
+class Knobs:
+    # ---- dense GEMM dispatch (ops/gemm.py; profiles/wide_gemm.md)
+    # which decode-sized GEMMs gemm_wide serves: "auto" (the cutovers below), "all", "none", or a
+    # comma list of roles gate_up / down / proj
+    wide: str = "auto"
+    # gemm_wide variant for unsplit grids (33: LDS-DMA interleaved + asm fragment reads with one
+    # lgkmcnt per MFMA row) and for split-K grids (1); in-engine A/B 27,123 vs 27,014 / 26,896 tok/s
+    wide_variant: int = 33
+    wide_variant_split: int = 1
+    wide_gate_up_max_m: int = 256     # SwiGLU-fused gate|up on gemm_wide up to this M (then hipBLASLt)
+    wide_down_max_m: int = 512        # MLP down (K >= 8192, K > N) up to this M
+    wide_proj_max_m: int = 256        # qkv / o / LM head up to this M (K >= 8192: the down limit)
+    wide_target_wgs: int = 256        # split-K: about one workgroup per CU
+    wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
+    wide_small_bm_maxw: int = 4096 * 4096
+    # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
+    # from this M up to 256, unsplit grids only unless sq_split
+    sq: str = "all"
+    sq_min_m: int = 225
+    sq_split: bool = False
+    sq_variant: int = 4
+    # ---- attention (ops/__init__.py)
+    attn_target_waves: int = 1024     # decode split-KV: waves to aim for (profiles/attn_decode_sweep.txt)
+    prefill_attn: int = 4             # prefill kernel version 1..5 (4: LDS-shared K/V tiles)
+    # ---- model / engine
+    fused_rope: bool = True           # decode: RoPE + KV append fused into attention
+    defer_qkv: bool = False           # split-K qkv consumed by the attention kernel (measured -3 %: off)
+    defer_o: bool = True              # split-K o-proj reduce fused into the next add + RMSNorm
+    lookahead: bool = True            # single-GPU engine: issue step n+1 before step n's tokens land
+    pp_lookahead: bool = True         # pipeline driver: the same across stages
+    # ---- MoE (ops/moe.py)
+    moe_variant: int = 0
+    moe_wide_min_pairs: int = 8       # token-expert pairs per expert from which the tiled GEMM serves
+    moe_fused_router: bool = True
+    # ---- FP8 W8A8 (ops/quant.py)
+    fp8_bm128: bool = True
+    fp8_group_m: int = 4096
+    # ---- hipBLASLt (ops/tuning.py)
+    tunableop: bool = True            # load the shipped TunableOp solution table
+
+
+K = Knobs()
+
+
+def _coerce(name: str, value: Any) -> Any:
+    typ = type(getattr(Knobs(), name))
+    if typ is bool:
+        if isinstance(value, str):
+            return value.strip().lower() in ("1", "true", "yes", "on")
+        return bool(value)
+    return typ(value)
+
+
+def update(overrides: Optional[Mapping[str, Any]] = None, **kw) -> Knobs:
+    """Apply overrides (unknown names raise).  Returns the live knob object."""
+    items = dict(overrides or {})
+    items.update(kw)
+    names = {f.name for f in dataclasses.fields(Knobs)}
+    unknown = set(items) - names
+    if unknown:
+        raise ValueError(f"unknown kernel knobs: {sorted(unknown)} (known: {sorted(names)})")
+    for k, v in items.items():
+        setattr(K, k, _coerce(k, v))
+    return K
+
+
+def reset() -> Knobs:
+    """Back to the defaults (then the DLLM_KNOBS overrides)."""
+    for f in dataclasses.fields(Knobs):
+        setattr(K, f.name, f.default)
+    update(parse(os.environ.get("DLLM_KNOBS", "")))
+    return K
+
+
+def parse(spec: str) -> Dict[str, Any]:
+    """``"a=1,b=x"`` or a JSON object -> dict."""
+    spec = (spec or "").strip()
+    if not spec:
+        return {}
+    if spec.startswith("{"):
+        return dict(json.loads(spec))
+    out = {}
+    for part in spec.split(","):
+        if part.strip():
+            k, _, v = part.partition("=")
+            out[k.strip()] = v.strip()
+    return out
+
+
+def as_dict() -> Dict[str, Any]:
+    return dataclasses.asdict(K)
+
+
+def changed() -> Dict[str, Any]:
+    """The knobs that differ from the defaults (what a bench line records)."""
+    d = Knobs()
+    return {f.name: getattr(K, f.name) for f in dataclasses.fields(Knobs) if getattr(K, f.name) != getattr(d, f.name)}
+
+
+reset()

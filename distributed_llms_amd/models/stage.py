@@ -16,24 +16,20 @@ Stage I/O:
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
 import torch
 
-from .. import ops
+from .. import knobs, ops
 from ..config import ModelConfig
 from ..ops import reference as ref
 from . import weights as W
 
-# decode: RoPE + KV append fused into the attention kernel (one launch); DLLM_FUSED_ROPE=0 -> two launches
-FUSED_ROPE_DECODE = os.environ.get("DLLM_FUSED_ROPE", "1") != "0"
-# split-K partials handed to the consumer instead of reduced by a separate launch (A/B knobs):
-#   qkv -> the fused decode attention kernel sums them (every wave re-reads S f32 slabs on its
-#   critical path: -3 % at B=256, off by default); o -> the MLP half's add + RMSNorm (+1 %)
-DEFER_QKV = os.environ.get("DLLM_DEFER_QKV", "0") == "1"   # measured -3 %: off
-DEFER_O = os.environ.get("DLLM_DEFER_O", "1") != "0"
+# knobs.fused_rope: decode RoPE + KV append fused into the attention kernel (one launch).  Split-K
+# partials handed to the consumer instead of reduced by a separate launch: knobs.defer_qkv (the
+# fused decode attention kernel sums them: every wave re-reads S slabs on its critical path, -3 %
+# at B=256, off), knobs.defer_o (the MLP half's add + RMSNorm, +1 %).
 
 
 @dataclass
@@ -302,7 +298,7 @@ class ModelStage:
         decode kernel reduces itself (any other path materialises it)."""
         cfg = self.cfg
         k_cache, v_cache = self.kv.layer(li)
-        fused = not meta.is_prefill and FUSED_ROPE_DECODE and \
+        fused = not meta.is_prefill and knobs.K.fused_rope and \
             (isinstance(qkv, ops.gemm.SplitKPartial) or qkv.is_cuda)
         if not fused and isinstance(qkv, ops.gemm.SplitKPartial):
             qkv = qkv.materialize()
@@ -375,7 +371,7 @@ class ModelStage:
                     else:
                         x, residual = ops.fused_add_rms_norm(h, residual, lw["attn_norm"], eps, quant_out=q8)
                     h = None
-                    qkv = ops.linear(x, lw["wqkv"], defer=DEFER_QKV and self.has(l, 1))
+                    qkv = ops.linear(x, lw["wqkv"], defer=knobs.K.defer_qkv and self.has(l, 1))
                     if not self.has(l, 1):
                         out_aux = self._dense(qkv)
                         break
@@ -391,7 +387,7 @@ class ModelStage:
                     if self.tp.enabled:
                         h = self.tp.all_reduce_(ops.linear(a, lw["wo"]))
                     else:
-                        h = ops.linear(a, lw["wo"], defer=DEFER_O)
+                        h = ops.linear(a, lw["wo"], defer=knobs.K.defer_o)
             # ---- MLP half: atoms 3 / 4 (first / second half of the intermediate columns)
             if self.has(l, 3) or self.has(l, 4):
                 q8 = isinstance(lw.get("w_gate_up"), ops.quant.Fp8Weight)

@@ -13,11 +13,10 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
-import os
 
 import torch
 
-from .. import _ext
+from .. import _ext, knobs
 from . import gemm, quant
 from . import reference as ref
 
@@ -209,7 +208,6 @@ def rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, n
 
 
 # ---------------------------------------------------------- K6 / K7
-DECODE_TARGET_WAVES = int(os.environ.get("DLLM_ATTN_TARGET_WAVES", "1024"))  # sweep: profiles/attn_decode_sweep.txt
 
 
 def decode_split_plan(batch: int, num_kv_heads: int, max_ctx: int, block_size: int = 32,
@@ -223,7 +221,7 @@ def decode_split_plan(batch: int, num_kv_heads: int, max_ctx: int, block_size: i
     identically: the extra splits of the bucket are empty and add exact zeros, and the two
     paths produce bit-identical attention.
     """
-    target_waves = target_waves or DECODE_TARGET_WAVES
+    target_waves = target_waves or knobs.K.attn_target_waves     # sweep: profiles/attn_decode_sweep.txt
     max_blocks = max_blocks or -(-max_ctx // block_size)
     pairs = 1 << max(0, (max(1, batch * num_kv_heads) - 1).bit_length())
     target = max(1, min(64, target_waves // pairs))
@@ -332,7 +330,8 @@ def paged_attention_decode_rope(qkv, positions, cos_sin, k_cache, v_cache, slot_
 
 
 def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, scale: float,
-                            max_q_len: Optional[int] = None):
+                            max_q_len: Optional[int] = None, version: int = 0):
+    """``version``: prefill kernel 1..5 (0: knobs.prefill_attn)."""
     if not _gpu(q):
         return ref.paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, scale)
     _ck(q, "attn.q")
@@ -349,7 +348,7 @@ def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq
     _ext.kernels().paged_attention_prefill(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                            block_tables.data_ptr(), cu_seqlens_q.data_ptr(), seq_lens.data_ptr(),
                                            b, hq, k_cache.shape[1], d, k_cache.shape[2], block_tables.shape[1],
-                                           int(max_q_len), float(scale), _stream())
+                                           int(max_q_len), float(scale), version or knobs.K.prefill_attn, _stream())
     return out
 
 

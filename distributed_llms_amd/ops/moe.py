@@ -11,24 +11,21 @@ CPU path: the PyTorch reference (ops/reference.py).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
 
-from .. import _ext
+from .. import _ext, knobs
 from . import reference as ref
 
 GROUPED_MAX_TOKENS = 256      # beyond this the per-expert row count makes library GEMMs cheaper
-# 0 = pick by expected rows per expert; 1..6 force a kernel variant (bench/moe_bench.py sweeps them)
-GROUPED_VARIANT = int(os.environ.get("DLLM_MOE_VARIANT", "0"))
-# token-expert pairs (T x top_k) from which the MFMA-tiled grouped kernel (gemm_wide.hip
-# moe_wide_gemm) replaces the weight-streaming one (moe.hip); 0 disables it.  Mixtral-8x7B
-# end to end (scripts/gpu_moe_wide.sh, profiles/moe_wide.md): B=1 0.95x, B=4 1.10x, B=16 1.10x,
-# B=64 1.25x, B=128 1.52x, B=256 2.23x
-WIDE_MIN_PAIRS = int(os.environ.get("DLLM_MOE_WIDE_MIN_PAIRS", "8"))
-# decode router: fused GEMV + top-k + scatter kernels instead of library GEMM + route kernel
-FUSED_ROUTER = os.environ.get("DLLM_MOE_FUSED_ROUTER", "1") != "0"
+# knobs.moe_variant: 0 = pick by expected rows per expert; 1..6 force a kernel variant
+# (bench/moe_bench.py sweeps them).  knobs.moe_wide_min_pairs: token-expert pairs (T x top_k) from
+# which the MFMA-tiled grouped kernel (gemm_wide.hip moe_wide_gemm) replaces the weight-streaming
+# one (moe.hip); 0 disables it.  Mixtral-8x7B end to end (in-engine A/B,
+# profiles/moe_wide.md): B=1 0.95x, B=4 1.10x, B=16 1.10x, B=64 1.25x, B=128 1.52x, B=256 2.23x.
+# knobs.moe_fused_router: decode router as fused GEMV + top-k + scatter kernels instead of library
+# GEMM + route kernel.
 
 
 def route(router_logits: torch.Tensor, top_k: int):
@@ -74,7 +71,7 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     offsets = torch.empty(e + 1, dtype=torch.int32, device=dev)
     sorted_tok = torch.empty(t * top_k, dtype=torch.int32, device=dev)
     inv = torch.empty(t * top_k, dtype=torch.int32, device=dev)
-    if FUSED_ROUTER and t <= GROUPED_MAX_TOKENS and e in (8, 16) and h % 32 == 0 and x.dtype == w_router.dtype == torch.bfloat16 \
+    if knobs.K.moe_fused_router and t <= GROUPED_MAX_TOKENS and e in (8, 16) and h % 32 == 0 and x.dtype == w_router.dtype == torch.bfloat16 \
             and w_router.is_contiguous():
         # decode: router GEMV + softmax/top-k + scatter in two launches (no [T, E] logits round trip)
         k.moe_router_route(x.data_ptr(), w_router.data_ptr(), t, h, e, top_k, topk_w.data_ptr(), topk_ids.data_ptr(),
@@ -111,16 +108,16 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     elif t <= GROUPED_MAX_TOKENS:
         act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
         rows = -(-t * top_k // e)        # expected rows per expert picks the kernel's row tile
-        if 0 < WIDE_MIN_PAIRS <= t * top_k and x.dtype == torch.bfloat16 and two_i % 128 == 0 and h % 128 == 0 \
+        if 0 < knobs.K.moe_wide_min_pairs <= t * top_k and x.dtype == torch.bfloat16 and two_i % 128 == 0 and h % 128 == 0 \
                 and h % 64 == 0 and inter % 64 == 0:
             k.moe_wide_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
                             cnt_p, off_p, e_loc, two_i, h, 1, st)
             k.moe_wide_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, 0, st)
         else:
             k.moe_grouped_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
-                               cnt_p, off_p, e_loc, two_i, h, 1, rows, GROUPED_VARIANT, st)
+                               cnt_p, off_p, e_loc, two_i, h, 1, rows, knobs.K.moe_variant, st)
             k.moe_grouped_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, 0,
-                               rows, GROUPED_VARIANT, st)
+                               rows, knobs.K.moe_variant, st)
     else:
         xs = x.index_select(0, sorted_tok.long())
         off = offsets.cpu().tolist()          # prefill only: eager, host sync is fine here

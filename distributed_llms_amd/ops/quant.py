@@ -22,12 +22,11 @@ quantization, f32 math), which is also the numerics oracle of the GPU tests.
 """
 from __future__ import annotations
 
-import os
 from typing import Tuple
 
 import torch
 
-from .. import _ext
+from .. import _ext, knobs
 
 FP8 = torch.float8_e4m3fn
 FP8_MAX = 448.0
@@ -194,11 +193,11 @@ def linear_ref(x, w: Fp8Weight, swiglu: bool = False) -> torch.Tensor:
 # instead of one 256-row tile -- a third fewer staged bytes per workgroup per K-tile (the loop is
 # bound by its LDS-DMA staging).  bench/fp8_bench.py --sweep at M = 256 (us, default 1-tile plan ->
 # this): o_8b 21.4 -> 18.0, qkv_8b 20.3 -> 19.1 (2 slices; 3 slices: 26.0), down_8b 29.3 = 29.3
-FP8_BM128 = os.environ.get("DLLM_FP8_BM128", "1") != "0"
+# (knobs.fp8_bm128)
 # prefill-sized M (no K split): grouped row-tile order (gemm_wide_fp8 variant bit 64) from this M:
 # at M = 32768 qkv 1018 -> 889 us, o 660 -> 599, gate|up 4509 -> 3924, down 2083 -> 1873 (1.8-2.0
 # PFLOP/s); at M = 2048 it is 1-6 % slower
-FP8_GROUP_M = int(os.environ.get("DLLM_FP8_GROUP_M", "4096"))
+# PFLOP/s); at M = 2048 it is 1-6 % slower (knobs.fp8_group_m)
 
 
 def fp8_plan(m: int, n: int, k: int, swiglu: bool = False) -> Tuple[int, int]:
@@ -206,7 +205,7 @@ def fp8_plan(m: int, n: int, k: int, swiglu: bool = False) -> Tuple[int, int]:
     kernel's rule on the 128-K tiles (a K-tile of fp8 holds the bytes of a 64-K bf16 tile)."""
     from .gemm import wide_splits
     s = wide_splits(m, n, k // 2, swiglu)
-    if FP8_BM128 and not swiglu and s > 1 and 128 < m <= 256:
+    if knobs.K.fp8_bm128 and not swiglu and s > 1 and 128 < m <= 256:
         tiles = (n // 128) * 2
         return max(1, min(256 // tiles, (k // 128) // 4, 16)), 128
     return s, 0
@@ -245,7 +244,7 @@ def linear_fp8(x: torch.Tensor, w: Fp8Weight, swiglu: bool = False, defer: bool 
     if s > 1 and s * m * n > ws.numel():
         s = max(1, ws.numel() // (m * n))
     # weights streamed non-temporal only where one row tile covers M (each weight byte read once)
-    variant = (1 if m <= 256 else (4 | (64 if 0 < FP8_GROUP_M <= m else 0))) | (bm << 8)
+    variant = (1 if m <= 256 else (4 | (64 if 0 < knobs.K.fp8_group_m <= m else 0))) | (bm << 8)
     stream = torch.cuda.current_stream().cuda_stream
     kern = _ext.kernels()
     if defer and not swiglu and s > 1:

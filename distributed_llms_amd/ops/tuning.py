@@ -7,7 +7,7 @@ and a shape that is not in the file simply uses the library heuristic), so the c
 before any HIP graph is captured.  The file carries TunableOp validators (torch, HIP,
 hipBLASLt, rocBLAS versions, gfx arch); on a mismatching stack TunableOp ignores it.
 
-Disable with ``DLLM_TUNABLEOP=0``.
+Disable with the ``tunableop`` kernel knob (distributed_llms_amd/knobs.py).
 """
 from __future__ import annotations
 
@@ -29,7 +29,8 @@ def enable_tuned_gemms(path: str = TUNED_CSV) -> bool:
     if _state["done"]:
         return _state["ok"]
     _state["done"] = True
-    if os.environ.get("DLLM_TUNABLEOP", "1") == "0" or not torch.cuda.is_available() or not os.path.exists(path):
+    from .. import knobs
+    if not knobs.K.tunableop or not torch.cuda.is_available() or not os.path.exists(path):
         return False
     tun = torch.cuda.tunable
     try:

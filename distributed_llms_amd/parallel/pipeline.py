@@ -17,7 +17,7 @@ step later, for bookkeeping only, so neither the host nor the control plane is o
 critical path: a slot's round trip is the stages' GPU time plus the hops, against ``num_slots``
 microbatches of stage-0 work.  Steps that need the host first (prefill admission, preemption,
 sampled sequences' stop checks after a prefill) fall back to completing the slot's step before
-scheduling (DLLM_PP_LOOKAHEAD=0: always).
+scheduling (knobs.pp_lookahead off: always).
 """
 from __future__ import annotations
 
@@ -30,6 +30,7 @@ from typing import Deque, List, Optional
 import numpy as np
 import torch
 
+from .. import knobs
 from ..config import EngineConfig, pipeline_slots, resolve_device  # noqa: F401  (pipeline_slots re-exported)
 from ..engine.batch import HostBatch, build_host_batch
 from ..engine.runner import StageRunner
@@ -43,7 +44,6 @@ log = logging.getLogger("dllm.pipeline")
 
 ROUND_END = -2     # control marker: followers return to their caller (bench round barrier)
 _MARKERS = (STOP, ROUND_END)
-LOOKAHEAD = os.environ.get("DLLM_PP_LOOKAHEAD", "1") != "0"
 
 
 def _marker(code: int) -> np.ndarray:
@@ -116,7 +116,7 @@ class PipelineDriver:
         self.device = runner.stage.device
         self.inflight: Deque[_Issued] = collections.deque()           # issue order
         self.per_slot: List[Deque[_Issued]] = [collections.deque() for _ in range(self.num_slots)]
-        self.lookahead = LOOKAHEAD
+        self.lookahead = knobs.K.pp_lookahead
         # pp x tp: the stage-0 TP peers replay every issue on their own lanes
         self.tp = runner.stage.tp if runner.stage.tp.enabled else None
         self.step_id = 0

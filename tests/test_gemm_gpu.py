@@ -1,4 +1,5 @@
-"""Skinny-M MFMA GEMM (decode) vs a plain fp32 PyTorch GEMM of the same operands."""
+"""Decode / prefill GEMM kernels (gemm_wide, gemm_sq, gemm_pp, split-K reducers) vs a plain fp32
+PyTorch GEMM of the same operands."""
 import os
 import pytest
 import torch
@@ -16,25 +17,27 @@ def _bf(*s, scale=1.0):
 
 @pytest.mark.parametrize("m", [1, 5, 32, 33, 64])
 @pytest.mark.parametrize("n,k", [(6144, 4096), (4096, 4096), (4096, 14336), (128, 768), (2304, 768)])
-def test_skinny_linear(cuda, m, n, k):
+def test_small_m_linear_dispatch(cuda, m, n, k):
+    """Decode batches 1..64 take the wide kernel's 64-row tile through the default dispatch."""
     x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    y = gemm.linear(x, w, force_skinny=True)
+    assert gemm._use_wide(m, n, k, x, w)
+    y = gemm.linear(x, w)
     ref = x.float() @ w.float().t()
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
-def test_skinny_bias(cuda):
+def test_bias_uses_library_gemm(cuda):
     x, w, b = _bf(9, 768), _bf(2304, 768, scale=0.05), _bf(2304)
-    y = gemm.linear(x, w, b, force_skinny=True)
+    y = gemm.linear(x, w, b)
     ref = x.float() @ w.float().t() + b.float()
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("m", [1, 16, 64])
 @pytest.mark.parametrize("inter,k", [(14336, 4096), (512, 256), (1024, 512)])
-def test_skinny_swiglu(cuda, m, inter, k):
+def test_small_m_swiglu(cuda, m, inter, k):
     x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
-    y = gemm.linear_swiglu(x, w, force_skinny=True)
+    y = gemm.linear_swiglu(x, w)
     gu = x.float() @ w.float().t()
     ref = F.silu(gu[:, :inter]) * gu[:, inter:]
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
@@ -42,43 +45,25 @@ def test_skinny_swiglu(cuda, m, inter, k):
 
 def test_large_m_uses_library_gemm(cuda):
     x, w = _bf(300, 512), _bf(256, 512, scale=0.05)
+    assert not gemm._use_wide(300, 256, 512, x, w)
     y = ops.linear(x, w)
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
 
 
-def test_skinny_graph_replay(cuda):
+def test_small_m_graph_replay(cuda):
     x, w = _bf(64, 4096), _bf(4096, 4096, scale=0.05)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        gemm.linear(x, w, force_skinny=True)
+        gemm.linear(x, w)
     torch.cuda.current_stream().wait_stream(s)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
-        y = gemm.linear(x, w, force_skinny=True)
+        y = gemm.linear(x, w)
     for _ in range(3):
         x.copy_(_bf(64, 4096))
         g.replay()
         torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
-
-
-@pytest.mark.parametrize("m", [1, 50, 128, 256, 300])
-@pytest.mark.parametrize("n,k,splits", [(6144, 4096, 0), (4096, 14336, 0), (256, 512, 1), (384, 1024, 3)])
-def test_tiled_linear(cuda, m, n, k, splits):
-    x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    y = gemm.linear_tiled(x, w, splits=splits)
-    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
-
-
-@pytest.mark.parametrize("m", [7, 256])
-def test_tiled_swiglu_and_bias(cuda, m):
-    x, w = _bf(m, 1024), _bf(2 * 512, 1024, scale=0.05)
-    gu = x.float() @ w.float().t()
-    y = gemm.linear_tiled(x, w, swiglu=True, splits=2)
-    torch.testing.assert_close(y.float(), F.silu(gu[:, :512]) * gu[:, 512:], atol=3e-2, rtol=3e-2)
-    b = _bf(1024)
-    y2 = gemm.linear_tiled(x, w, bias=b, splits=2)
-    torch.testing.assert_close(y2.float(), gu + b.float(), atol=3e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("m,n,k", [(256, 4096, 14336), (96, 1024, 8192)])
@@ -209,7 +194,7 @@ def test_wide_deferred_splitk_matches_materialized(cuda):
 @pytest.mark.parametrize("bm", [64, 128, 192])
 @pytest.mark.parametrize("m", [100, 256, 384])
 def test_wide_row_tile_override(cuda, bm, m):
-    """gemm_wide with a forced smaller row tile (variant bits 8.., what DLLM_WIDE_SMALL_BM selects):
+    """gemm_wide with a forced smaller row tile (variant bits 8.., what knobs.wide_small_bm selects):
     several M tiles per N tile, plain and deferred split-K."""
     from distributed_llms_amd import _ext
     x, w = _bf(m, 4096), _bf(4096, 4096, scale=0.05)
@@ -228,7 +213,7 @@ def test_wide_row_tile_override(cuda, bm, m):
 
 @pytest.mark.parametrize("m", [640, 768])
 def test_wide_linear_past_512_rows(cuda, m):
-    """DLLM_WIDE_DOWN_MAX_M > 512 routes M > 512 down projections to gemm_wide: three 256-row
+    """knobs.wide_down_max_m > 512 routes M > 512 down projections to gemm_wide: three 256-row
     tiles (the 192-row tile is only used up to 384) with an 8-way K split."""
     x, w = _bf(m, 14336), _bf(4096, 14336, scale=0.05)
     y = gemm.linear_wide(x, w, splits=8)
@@ -239,9 +224,9 @@ def test_deferred_down_at_768_rows_into_fused_norm(cuda, monkeypatch):
     """ops.linear(defer=True) at M = 768 with the down cutover raised: the deferred split-K partial
     feeds fused_add_rms_norm and matches the fp32 reference."""
     from distributed_llms_amd.ops import reference as ref
-    monkeypatch.setattr(gemm, "WIDE", {"auto"})
-    monkeypatch.setattr(gemm, "GEMM_MODE", "auto")
-    monkeypatch.setattr(gemm, "WIDE_DOWN_MAX_M", 768)
+    from distributed_llms_amd import knobs
+    monkeypatch.setattr(knobs.K, "wide", "auto")
+    monkeypatch.setattr(knobs.K, "wide_down_max_m", 768)
     torch.manual_seed(1)
     m, n, k = 768, 4096, 14336
     x = (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16)
@@ -258,42 +243,6 @@ def test_deferred_down_at_768_rows_into_fused_norm(cuda, monkeypatch):
     torch.testing.assert_close(y.float(), yr, atol=6e-2, rtol=3e-2)
 
 
-_SKN_CHILD = r"""
-import torch
-from distributed_llms_amd import ops
-from distributed_llms_amd.ops import gemm, reference as ref
-torch.manual_seed(2)
-m, n, k = 256, 4096, 14336
-x = (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16)
-w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
-g = (1 + 0.1 * torch.randn(n, device="cuda")).to(torch.bfloat16)
-res0 = torch.randn(m, n, device="cuda").to(torch.bfloat16)
-p = gemm.linear_wide(x, w, splits=8, defer=True)
-assert isinstance(p, gemm.SplitKPartial) and p.splits == 8
-r = res0.clone()
-y, _ = ops.fused_add_rms_norm(p, r, g, 1e-5)
-h = gemm.linear_wide(x, w, splits=8, defer=True).materialize()
-yr, rr = ref.fused_add_rms_norm(h.float(), res0.float(), g.float(), 1e-5)
-torch.testing.assert_close(r.float(), rr, atol=3e-2, rtol=3e-2)
-torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
-print("SKN512_OK")
-"""
-
-
-def test_skn_512_threads(cuda):
-    """The opt-in 512-thread splitk_add_rms_norm (DLLM_SKN_THREADS=512, read once per process, S == 8
-    and hidden 4096 only) against the fp32 reference, in a fresh process that sets the knob before
-    its first GPU call."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, DLLM_SKN_THREADS="512", PYTHONPATH=root)
-    out = subprocess.run([sys.executable, "-c", _SKN_CHILD], env=env, cwd=root, capture_output=True, text=True,
-                         timeout=300)
-    assert out.returncode == 0 and "SKN512_OK" in out.stdout, out.stdout[-2000:] + out.stderr[-4000:]
-
-
-@pytest.mark.parametrize("m", [129, 200, 256])
 @pytest.mark.parametrize("n,k,splits", [(6144, 4096, 0), (4096, 14336, 0), (4096, 4096, 16), (1024, 512, 1),
                                         (512, 1024, 3)])
 def test_sq_linear(cuda, m, n, k, splits):
@@ -328,22 +277,6 @@ def test_sq_deferred_into_fused_norm(cuda):
     yr, rr = ref.fused_add_rms_norm(ref.linear(x.float(), w.float()), res0.float(), g.float(), 1e-5)
     torch.testing.assert_close(r.float(), rr, atol=6e-2, rtol=3e-2)
     torch.testing.assert_close(y.float(), yr, atol=6e-2, rtol=3e-2)
-
-
-@pytest.mark.parametrize("m,n,k,splits,swiglu", [(256, 28672, 4096, 2, True), (256, 4096, 14336, 8, False),
-                                                (256, 6144, 4096, 5, False), (200, 1024, 512, 1, False),
-                                                (100, 2048, 1024, 3, False), (256, 512, 64, 2, True),
-                                                (300, 1024, 256, 1, False)])
-def test_big_linear(cuda, m, n, k, splits, swiglu):
-    """gemm_big (256 x 256 x 32 tile, one wave per SIMD): against the fp32 product, SwiGLU through
-    the split-K reduce, rows past M masked, short K (fewer tiles than the three in flight)."""
-    x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    y = gemm.linear_big(x, w, splits=splits, swiglu=swiglu)
-    ref = x.float() @ w.float().t()
-    if swiglu:
-        g, u = ref.chunk(2, -1)
-        ref = F.silu(g) * u
-    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
 # ---- gemm_pp: ping-pong 256-row-tile kernel (decode split-K, prefill grouped + SwiGLU)

@@ -134,8 +134,7 @@ def test_paged_attention_decode_fused_rope(cuda, hq, hkv, d, lens, rope):
 
 @pytest.mark.parametrize("version", ["1", "2", "3", "4", "5"])
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 64)])
-def test_paged_attention_prefill(cuda, monkeypatch, hq, hkv, d, version):
-    monkeypatch.setenv("DLLM_PREFILL_ATTN", version)
+def test_paged_attention_prefill(cuda, hq, hkv, d, version):
     ctx = [37, 128, 300, 5]
     qlen = [37, 64, 1, 5]       # second/third: chunked prefill with prior context
     k, v, bt = _fill_paged(ctx, hkv, d)
@@ -143,16 +142,15 @@ def test_paged_attention_prefill(cuda, monkeypatch, hq, hkv, d, version):
     sl = torch.tensor(ctx, dtype=torch.int32, device="cuda")
     q = _bf(sum(qlen), hq, d)
     scale = 1 / math.sqrt(d)
-    out = ops.paged_attention_prefill(q, k, v, bt, cu, sl, scale)
+    out = ops.paged_attention_prefill(q, k, v, bt, cu, sl, scale, version=int(version))
     expect = ref.paged_attention_prefill(q.float(), k.float(), v.float(), bt, cu, sl, scale)
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("version", ["3", "4", "5"])
-def test_paged_attention_prefill_long(cuda, monkeypatch, version):
+def test_paged_attention_prefill_long(cuda, version):
     """Long prompts: > 64 KV chunks per sequence (block-id reloads), many workgroups per
     (sequence, kv head), a chunked prefill that starts mid-block."""
-    monkeypatch.setenv("DLLM_PREFILL_ATTN", version)
     hq, hkv, d = 32, 8, 128
     ctx = [2300, 777, 64]
     qlen = [900, 777, 33]
@@ -161,7 +159,7 @@ def test_paged_attention_prefill_long(cuda, monkeypatch, version):
     sl = torch.tensor(ctx, dtype=torch.int32, device="cuda")
     q = _bf(sum(qlen), hq, d)
     scale = 1 / math.sqrt(d)
-    out = ops.paged_attention_prefill(q, k, v, bt, cu, sl, scale)
+    out = ops.paged_attention_prefill(q, k, v, bt, cu, sl, scale, version=int(version))
     expect = ref.paged_attention_prefill(q.float(), k.float(), v.float(), bt, cu, sl, scale)
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
 

@@ -41,7 +41,7 @@ def _oracle(x, w, swiglu=False):
     (256, 2048, 4096, True, 4),          # split-K SwiGLU (splitk_reduce_swiglu)
     (256, 4096, 14336, False, 0),        # down_8b
     (1000, 1024, 1024, False, 1),        # prefill-sized M, several row tiles
-    (5000, 1024, 512, True, 0),          # grouped row-tile order (M >= DLLM_FP8_GROUP_M), SwiGLU
+    (5000, 1024, 512, True, 0),          # grouped row-tile order (M >= knobs.fp8_group_m), SwiGLU
     (4500, 2048, 1024, False, 0),        # grouped, partial last row tile and group
 ])
 def test_gemm_wide_fp8_matches_reference(m, n, k, swiglu, splits):

@@ -1,8 +1,8 @@
 """Decode GEMM routing between the wide-M HIP kernel (csrc/kernels/gemm_wide.hip) and hipBLASLt.
 
 The cutovers are measured in-engine (profiles/wide_gemm.md): gate|up (SwiGLU) and qkv / o on the
-wide kernel up to M = 256, the K >= 8192 down projection up to M = 512.  CPU-only: `_use_wide` is
-pure shape / dtype logic."""
+wide kernel up to M = 256, the K >= 8192 down projection up to M = 512 (distributed_llms_amd/knobs.py).
+CPU-only: `_use_wide` is pure shape / dtype logic."""
 import pytest
 import torch
 
@@ -14,15 +14,14 @@ def _xw(m, n, k):
 
 
 @pytest.fixture(autouse=True)
-def _defaults(monkeypatch):
-    monkeypatch.setattr(gemm, "WIDE", {"auto"})
-    monkeypatch.setattr(gemm, "GEMM_MODE", "auto")
-    monkeypatch.setattr(gemm, "WIDE_MIN_M", 1)
-    # the cutovers are read from the environment at import time: pin the shipped defaults so an
-    # exported A/B knob (e.g. DLLM_WIDE_DOWN_MAX_M=768) cannot move the boundary cases below
-    monkeypatch.setattr(gemm, "WIDE_GATE_UP_MAX_M", 256)
-    monkeypatch.setattr(gemm, "WIDE_DOWN_MAX_M", 512)
-    monkeypatch.setattr(gemm, "WIDE_PROJ_MAX_M", 256)
+def _defaults():
+    # pin the shipped defaults (a DLLM_KNOBS override in the environment cannot move the boundaries)
+    from distributed_llms_amd import knobs
+    saved = knobs.as_dict()
+    for f, v in knobs.Knobs().__dict__.items():
+        setattr(knobs.K, f, v)
+    yield
+    knobs.update(saved)
 
 
 @pytest.mark.parametrize("m,expect", [(1, True), (64, True), (256, True), (257, False), (384, False), (512, False)])
@@ -61,33 +60,48 @@ def test_down_role_rule():
     assert not gemm.is_down_proj(4096, 4096) and not gemm.is_down_proj(128256, 4096)
 
 
-def test_down_cap_can_exceed_512(monkeypatch):
-    monkeypatch.setattr(gemm, "WIDE_DOWN_MAX_M", 768)
+def test_down_cap_can_exceed_512():
+    from distributed_llms_amd import knobs
+    knobs.update(wide_down_max_m=768)
     x, w = _xw(768, 4096, 14336)
     assert gemm._use_wide(768, 4096, 14336, x, w)
     xg, wg = _xw(768, 2 * 14336, 4096)
     assert not gemm._use_wide(768, wg.shape[0], 4096, xg, wg, swiglu=True)
 
 
-def test_blas_mode_and_dtype_disable_wide(monkeypatch):
+def test_wide_off_and_dtype_disable_wide():
+    from distributed_llms_amd import knobs
     x, w = _xw(128, 4096, 4096)
     assert not gemm._use_wide(128, 4096, 4096, x.float(), w.float())
-    monkeypatch.setattr(gemm, "GEMM_MODE", "blas")
+    knobs.update(wide="none")
     assert not gemm._use_wide(128, 4096, 4096, x, w)
 
 
-def test_sq_only_on_unsplit_grids(monkeypatch):
+def test_sq_only_on_unsplit_grids():
     """gemm_sq (256 x 256 tiles) serves 225 <= M <= 256 only where its grid needs no K split: the
     LM head and the 70B gate|up (profiles/wide_gemm.md)."""
-    monkeypatch.setattr(gemm, "SQ", {"all"})
-    monkeypatch.setattr(gemm, "SQ_MIN_M", 225)
-    monkeypatch.setattr(gemm, "SQ_SPLIT", False)
+    from distributed_llms_amd import knobs
     assert gemm.use_sq(256, 128256, 4096) and not gemm.use_sq(192, 128256, 4096)
     assert gemm.use_sq(256, 57344, 8192, swiglu=True)
     assert not gemm.use_sq(128, 128256, 4096)                      # 128-row tile of the wide kernel
     for n, k, sw in ((6144, 4096, False), (4096, 4096, False), (28672, 4096, True), (4096, 14336, False),
                      (10240, 8192, False), (8192, 28672, False), (32000, 4096, False)):
         assert not gemm.use_sq(256, n, k, swiglu=sw), (n, k)
-    monkeypatch.setattr(gemm, "SQ_SPLIT", True)
+    knobs.update(sq_split=True)
     assert gemm.use_sq(256, 4096, 14336)
     assert gemm.sq_splits(256, 4096, 14336) == 16 and gemm.sq_splits(256, 6144, 4096) == 10
+
+
+def test_knobs_move_the_cutovers_and_reject_unknown_names():
+    from distributed_llms_amd import knobs
+    x, w = _xw(384, 6144, 4096)
+    assert not gemm._use_wide(384, 6144, 4096, x, w)
+    knobs.update(wide_proj_max_m=512)
+    assert gemm._use_wide(384, 6144, 4096, x, w)
+    knobs.update({"wide": "none"})
+    assert not gemm._use_wide(16, 6144, 4096, x, w)
+    with pytest.raises(ValueError):
+        knobs.update(no_such_knob=1)
+    assert knobs.parse("wide_variant=1, defer_qkv=1") == {"wide_variant": "1", "defer_qkv": "1"}
+    knobs.update(knobs.parse('{"defer_qkv": "true"}'))
+    assert knobs.K.defer_qkv is True and "defer_qkv" in knobs.changed()
