@@ -2,7 +2,7 @@
 
 Times N back-to-back launches between two events (the GPU never idles, so host launch
 overhead is excluded) and reports us/call and KV bytes streamed per second, sweeping the
-split-plan target (``ops.DECODE_TARGET_WAVES``).
+split-plan target (``knobs.attn_target_waves``).
 
     python bench/attn_bench.py [--batch 64 256] [--ctx 192 1024 4096]
 """
@@ -15,6 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 import distributed_llms_amd.ops as ops
+from distributed_llms_amd import knobs
 
 
 def main():
@@ -48,7 +49,7 @@ def main():
             kv_bytes = b * ctx * a.hkv * a.d * 2 * 2
             cells = []
             for t in a.targets:
-                ops.DECODE_TARGET_WAVES = t
+                knobs.K.attn_target_waves = t
                 f = lambda: ops.paged_attention_decode(q, kc, vc, bt, sl, 0.088, max_ctx=ctx)   # noqa: E731
                 f()
                 torch.cuda.synchronize()
@@ -63,7 +64,7 @@ def main():
                 cells.append(f"{us:7.1f}us/{kv_bytes / us / 1e6:4.2f}TB s{sp:<2d}")
             print(f"{b:4d} {ctx:5d} " + " ".join(f"{c:>16s}" for c in cells), flush=True)
             del kc, vc
-    ops.DECODE_TARGET_WAVES = 1024
+    knobs.K.attn_target_waves = 1024
 
 
 def cold(a):

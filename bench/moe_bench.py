@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import torch.nn.functional as F
 
-from distributed_llms_amd import _ext, ops
+from distributed_llms_amd import _ext, knobs, ops
 from distributed_llms_amd.ops import moe
 
 
@@ -86,12 +86,12 @@ def main():
         if t <= moe.GROUPED_MAX_TOKENS and a.variants:
             row = []
             for v in a.variants:
-                moe.GROUPED_VARIANT = v
+                knobs.K.moe_variant = v
                 f_hip()
                 tv = timeit(f_hip, a.iters)
                 e2 = (f_hip().float() - f_blas().float()).abs().max().item()
                 row.append(f"v{v}={tv * 1e6:.0f}us({nbytes / tv / 1e12:.2f}TB/s{'' if e2 < 0.1 else ' BAD'})")
-            moe.GROUPED_VARIANT = 0
+            knobs.K.moe_variant = 0
             print("      variants: " + "  ".join(row), flush=True)
 
 

@@ -18,12 +18,13 @@ import torch
 
 from distributed_llms_amd.ops import gemm
 
-CASES = [  # name, M, N, K, swiglu, splits, variant
-    ("gate_up dec", 256, 28672, 4096, True, 1, 1), ("gate_up dec", 256, 28672, 4096, True, 2, 0),
-    ("gate_up dec", 256, 28672, 4096, True, 1, 0),
-    ("down dec", 256, 4096, 14336, False, 8, 1), ("down dec", 256, 4096, 14336, False, 16, 0),
-    ("qkv dec", 256, 6144, 4096, False, 5, 1), ("qkv dec", 256, 6144, 4096, False, 10, 0),
+CASES = [  # name, M, N, K, swiglu, splits, variant (| 16: no LDS-DMA in the loop, | 32: no fragment reads)
+    ("gate_up dec", 256, 28672, 4096, True, 1, 1), ("gate_up noload", 256, 28672, 4096, True, 1, 1 | 16),
+    ("gate_up noread", 256, 28672, 4096, True, 1, 1 | 32),
+    ("gate_up dec", 256, 28672, 4096, True, 2, 0), ("gate_up noload", 256, 28672, 4096, True, 2, 16),
+    ("down dec", 256, 4096, 14336, False, 8, 1), ("down noload", 256, 4096, 14336, False, 8, 1 | 16),
     ("gate pf", 8192, 14336, 4096, False, 1, 4), ("gate pf", 8192, 14336, 4096, False, 1, 5),
+    ("gate pf noload", 8192, 14336, 4096, False, 1, 1 | 16), ("gate pf noread", 8192, 14336, 4096, False, 1, 1 | 32),
 ]
 
 
@@ -51,9 +52,10 @@ def main():
         def run(var):
             return gemm.linear_pp(x, ws_[next(it) % copies], splits=s, swiglu=sw, variant=var)
         for _ in range(10):
-            run(v | 8)
+            run((v & 7) | 8 | (v & 48))
         torch.cuda.synchronize()
         bn = 128 if v & 1 else 256
+        # ablations time the diagnostic build itself (their output is garbage)
         grid = (n // bn) * (-(-m // 256)) * s
         rec = gemm._workspace(dev)[-grid * 512:].view(grid * 4, 128)[:, :4].cpu()
         tot, bt, nt, rt = rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3]
@@ -62,7 +64,7 @@ def main():
         ideal = 2 * 8 * (bn // 32) * 16
         per = (tot / nt).tolist()
         frac = (bt / tot).tolist()
-        t_real = timed(lambda: run(v))
+        t_real = timed(lambda: run((v & 7) | (8 | (v & 48) if v & 48 else 0)))
         wg_us = (rt_ns / 1e3).view(-1, 4).max(dim=1).values
         print(f"{name:12s} M={m:5d} N={n:5d} K={k:5d} S={s:2d} BN={bn} var={v}: kernel {t_real:7.1f} us "
               f"({2.0 * m * n * k / t_real / 1e6:5.0f} TF) | WG loop median {statistics.median(wg_us.tolist()):6.1f} us, "

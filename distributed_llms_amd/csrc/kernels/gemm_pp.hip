@@ -152,6 +152,8 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   constexpr int G = GA + GB;
   constexpr bool NT = (VAR & 1) != 0, GROUPED = (VAR & 2) != 0;
   constexpr bool PROF = (VAR & 4) != 0;                // diagnostic build: cycle stamps around B_t
+  // diagnostic ablations (wrong results, timing only): no LDS-DMA pieces / no fragment reads in the loop
+  constexpr bool NOLOAD = (VAR & 8) != 0, NOREAD = (VAR & 16) != 0;
   constexpr bool SWIGLU = MODE == 2;
   constexpr int OUTW = SWIGLU ? BN / 2 : BN;           // output tile width (elements)
   constexpr int OPITCH = OUTW + 8;                     // LDS output row pitch (elements): +16 B
@@ -296,10 +298,10 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
           acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[c], fa0[r], acc[r][c], 0, 0, 0);
 #pragma unroll
           for (int a = 0; a < RT; ++a)
-            if (SC::pos(0, 0, a) == i) fa1[a] = pp_frag_dyn(base + a_off + a * 16 * 128);
+            if (!NOREAD && SC::pos(0, 0, a) == i) fa1[a] = pp_frag_dyn(base + a_off + a * 16 * 128);
 #pragma unroll
           for (int b = 0; b < CT; ++b)
-            if (SC::pos(0, 1, b) == i) fb1[b] = pp_frag_dyn(base + b_off + b * 16 * 128);
+            if (!NOREAD && SC::pos(0, 1, b) == i) fb1[b] = pp_frag_dyn(base + b_off + b * 16 * 128);
           __builtin_amdgcn_sched_barrier(0);
         });
       }
@@ -331,13 +333,13 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
             }
           }
           if constexpr (i >= SC::EB - 1 && (i - SC::EB + 1) % GE == 0 && (i - SC::EB + 1) / GE < G)
-            piece(slot, t + NB, (i - SC::EB + 1) / GE);
+            if constexpr (!NOLOAD) piece(slot, t + NB, (i - SC::EB + 1) / GE);
 #pragma unroll
           for (int a = 0; a < RT; ++a)
-            if (SC::pos(1, 0, a) == i) fa0[a] = pp_frag_dyn(base + a_off + a * 16 * 128);
+            if (!NOREAD && SC::pos(1, 0, a) == i) fa0[a] = pp_frag_dyn(base + a_off + a * 16 * 128);
 #pragma unroll
           for (int b = 0; b < CT; ++b)
-            if (SC::pos(1, 1, b) == i) fb0[b] = pp_frag_dyn(base + b_off + b * 16 * 128);
+            if (!NOREAD && SC::pos(1, 1, b) == i) fb0[b] = pp_frag_dyn(base + b_off + b * 16 * 128);
           __builtin_amdgcn_sched_barrier(0);
         });
       }
@@ -438,7 +440,8 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
   hipLaunchKernelGGL((gemm_pp_kernel<BN_, MODE_, VAR_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, \
                      (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kps, S, dbg)
   // variant bit 3: diagnostic build -- per-wave cycle stamps (loop, B_t waits) into the LAST
-  // grid x 512 floats of ws (after the slabs); output as usual
+  // grid x 512 floats of ws (after the slabs); output as usual.  With it, bit 4: no LDS-DMA pieces
+  // in the loop, bit 5: no fragment reads in the loop (ablations: wrong results, timing only)
   const bool prof = (variant & 8) != 0;
   float* dbg = nullptr;
   if (prof) {
@@ -447,7 +450,12 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
   }
 #define DLLM_PP_V(BN_, MODE_)                                        \
   do {                                                               \
-    if (prof) { if (grp) DLLM_PP_GO(BN_, MODE_, 6); else DLLM_PP_GO(BN_, MODE_, 4); } \
+    if (prof) {                                                      \
+      if (grp) DLLM_PP_GO(BN_, MODE_, 6);                            \
+      else if (variant & 16) DLLM_PP_GO(BN_, MODE_, 12);             \
+      else if (variant & 32) DLLM_PP_GO(BN_, MODE_, 20);             \
+      else DLLM_PP_GO(BN_, MODE_, 4);                                \
+    }                                                                \
     else if (grp) { if (nt) DLLM_PP_GO(BN_, MODE_, 3); else DLLM_PP_GO(BN_, MODE_, 2); } \
     else { if (nt) DLLM_PP_GO(BN_, MODE_, 1); else DLLM_PP_GO(BN_, MODE_, 0); }     \
   } while (0)

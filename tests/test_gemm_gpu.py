@@ -243,6 +243,7 @@ def test_deferred_down_at_768_rows_into_fused_norm(cuda, monkeypatch):
     torch.testing.assert_close(y.float(), yr, atol=6e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("m", [129, 200, 256])
 @pytest.mark.parametrize("n,k,splits", [(6144, 4096, 0), (4096, 14336, 0), (4096, 4096, 16), (1024, 512, 1),
                                         (512, 1024, 3)])
 def test_sq_linear(cuda, m, n, k, splits):

@@ -72,7 +72,8 @@ def test_moe_graph_capturable(cuda):
 def test_moe_wide_grouped_kernel(cuda, monkeypatch, t, skew):
     """The MFMA-tiled grouped expert GEMM (gemm_wide.hip moe_wide_gemm) forced for every token
     count: 64-row tiles, 128-row chunks, multi-chunk experts (skewed routing) and empty experts."""
-    monkeypatch.setattr(moe, "WIDE_MIN_PAIRS", 1)
+    from distributed_llms_amd import knobs
+    monkeypatch.setattr(knobs.K, "moe_wide_min_pairs", 1)
     e, k, h, i = 8, 2, 512, 384
     x = _bf(t, h)
     if skew:
