@@ -165,16 +165,19 @@ def run_single(args):
     if eng.runner is not None:
         eng.runner.meter(True)
     tr = start_trace(args)
-    lat = []
+    lat, done = [], []
     t0 = time.perf_counter()
     for r in range(args.steps):
         seqs = round_(r)
         lat.extend(s.latency() for s in seqs)
+        done.extend(seqs)
     sync()
     elapsed = time.perf_counter() - t0
     assert all(len(s.output) == args.gen_len for s in seqs)
+    from distributed_llms_amd.utils.metrics import request_timing, seq_timing
     extra = {"load_s": round(load_s, 1), "transport": "none",
-             "stage_busy_frac": [round(eng.runner.busy_seconds() / elapsed, 4) if eng.runner else None]}
+             "stage_busy_frac": [round(eng.runner.busy_seconds() / elapsed, 4) if eng.runner else None],
+             **request_timing(*seq_timing(done))}
     if tr is not None:
         finish_trace(args, tr, elapsed, 0)
     emit(args, 1, elapsed, lat, extra)

@@ -9,6 +9,7 @@ import torch.distributed as dist
 
 from ..config import EngineConfig
 from ..engine.sequence import SamplingParams
+from ..utils.metrics import request_timing, seq_timing
 from .dist_engine import RankRole, agree_max, init_distributed
 
 
@@ -59,25 +60,34 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
     if runner is not None:
         runner.meter(True)
     tr = start_trace(args) if start_trace else None
-    lat = []
+    tp_ = getattr(role, "transport", None)
+    hop0 = tp_.hop_stats() if tp_ is not None else {}
+    lat, done = [], []
     t0 = time.perf_counter()
     for r in range(args.steps):
         seqs = one_round(r)
         lat.extend(s.latency() for s in seqs)
+        done.extend(seqs)
     _sync(ctx)
     elapsed = agree_max(ctx, time.perf_counter() - t0)
+    hop1 = tp_.hop_stats() if tp_ is not None else {}
     if role.is_driver:
         assert all(len(s.output) == args.gen_len for s in seqs), "incomplete generations"
     # gather latencies to rank 0
     obj = [None] * world
-    dist.all_gather_object(obj, lat, group=ctx.ctrl_group)
-    all_lat = [x for part in obj for x in part]
+    dist.all_gather_object(obj, (lat, seq_timing(done)), group=ctx.ctrl_group)
+    all_lat = [x for part in obj for x in part[0]]
+    all_ttft = [x for part in obj for x in part[1][0]]
+    all_itl = [x for part in obj for x in part[1][1]]
     if tr is not None:
         finish_trace(args, tr, elapsed, ctx.rank)
     # per-rank device busy fraction over the timed rounds, and what the data plane ran on
     mine = {"busy": round(runner.busy_seconds() / elapsed, 4) if runner is not None else None}
-    tp_ = getattr(role, "transport", None)
     mine["transport"] = getattr(tp_, "kind", "none") if tp_ is not None else "none"
+    d = {k: hop1.get(k, 0) - hop0.get(k, 0) for k in hop1}
+    mine["hop_tx"] = (d.get("hidden_tx", 0) + d.get("ids_tx", 0)) / elapsed   # device-plane bytes / s out
+    mine["hop_rx"] = (d.get("hidden_rx", 0) + d.get("ids_rx", 0)) / elapsed
+    mine["meta"] = (d.get("meta_tx", 0) + d.get("meta_rx", 0)) / elapsed
     mine["rccl_comm_ranks"] = list(getattr(tp_, "comm_ranks", []) or [])
     info = [None] * world
     dist.all_gather_object(info, mine, group=ctx.ctrl_group)
@@ -97,6 +107,11 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
         extra["rccl_comms"] = sum(len(i["rccl_comm_ranks"]) for i in info) // 2
         extra["rccl_ranks"] = sum(1 for i in info if i["rccl_comm_ranks"])
         extra["rccl_comm_nranks"] = sorted({n for i in info for n in i["rccl_comm_ranks"]})
+        # per-rank activation / ids traffic over the timed rounds (xGMI hops), MB/s
+        extra["hop_tx_MBps"] = [round(i["hop_tx"] / 1e6, 3) for i in info]
+        extra["hop_rx_MBps"] = [round(i["hop_rx"] / 1e6, 3) for i in info]
+        extra["meta_MBps"] = [round(i["meta"] / 1e6, 3) for i in info]
+        extra.update(request_timing(all_ttft, all_itl))
         emit(args, world, elapsed, all_lat, extra, global_batch=per_pipe * ctx.dp)
     role.shutdown()
     _sync(ctx)

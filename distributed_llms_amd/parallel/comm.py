@@ -21,7 +21,9 @@ how the pipeline schedule is exercised on the single-GPU test box.
 """
 from __future__ import annotations
 
+import functools
 import queue
+import threading
 from typing import Optional
 
 import numpy as np
@@ -99,9 +101,56 @@ class PendingIds:
         return t.numpy()
 
 
+def _elem_bytes(dtype) -> int:
+    return torch.empty(0, dtype=dtype).element_size()
+
+
+# per-hop traffic accounting (bytes per stage edge; bench JSON and /metrics): method ->
+# (counter, bytes of one call from its arguments / result)
+_COUNTED = {
+    "send_hidden": ("hidden_tx", lambda a, r: a[0].numel() * a[0].element_size()),
+    "recv_hidden": ("hidden_rx", lambda a, r: int(a[0]) * int(a[1]) * _elem_bytes(a[2])),
+    "send_ids": ("ids_tx", lambda a, r: a[0].numel() * 4),
+    "recv_ids": ("ids_rx", lambda a, r: int(a[0]) * 4),
+    "send_meta": ("meta_tx", lambda a, r: 8 + 4 * len(a[0])),
+    "recv_meta": ("meta_rx", lambda a, r: 8 + 4 * len(r)),
+}
+_hop_depth = threading.local()
+
+
+def _counting(fn, key, size):
+    @functools.wraps(fn)
+    def wrapper(self, *a, **kw):
+        depth = getattr(_hop_depth, "d", 0)
+        _hop_depth.d = depth + 1
+        try:
+            r = fn(self, *a, **kw)
+        finally:
+            _hop_depth.d = depth
+        if depth == 0:                    # outermost call only (a subclass may call super())
+            h = self.__dict__.setdefault("_hop_bytes", {})
+            h[key] = h.get(key, 0) + int(size(a, r))
+        return r
+    wrapper._counted = True
+    return wrapper
+
+
 class Transport:
+    """Every subclass's send/recv methods are wrapped to count the bytes they move
+    (:meth:`hop_stats`)."""
     stage: int
     num_stages: int
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        for name, (key, size) in _COUNTED.items():
+            fn = cls.__dict__.get(name)
+            if fn is not None and not getattr(fn, "_counted", False):
+                setattr(cls, name, _counting(fn, key, size))
+
+    def hop_stats(self) -> dict:
+        """Bytes moved so far by this stage's transport: hidden / ids / meta, tx and rx."""
+        return dict(self.__dict__.get("_hop_bytes", {}))
 
     def send_meta(self, arr: np.ndarray) -> None: ...
     def recv_meta(self) -> np.ndarray: ...

@@ -57,6 +57,20 @@ class RequestMetrics:
             }
 
 
+def request_timing(ttfts: List[float], itls: List[float]) -> Dict[str, Optional[float]]:
+    """Bench-line fields: time to first token and inter-token latency percentiles, in ms."""
+    ms = lambda v: None if v is None else round(1000.0 * v, 3)
+    return {"ttft_p50_ms": ms(percentile(ttfts, 50)), "ttft_p99_ms": ms(percentile(ttfts, 99)),
+            "itl_p50_ms": ms(percentile(itls, 50)), "itl_p99_ms": ms(percentile(itls, 99))}
+
+
+def seq_timing(seqs):
+    """(ttfts, itls) in seconds of finished sequences."""
+    ttfts = [t for t in (s.ttft() for s in seqs) if t is not None]
+    itls = [d for s in seqs for d in s.itl()]
+    return ttfts, itls
+
+
 def itl_stats(seqs) -> Dict[str, Optional[float]]:
     xs = [d for s in seqs for d in s.itl()]
     return {"itl_p50_s": percentile(xs, 50), "itl_p99_s": percentile(xs, 99)}
@@ -73,7 +87,8 @@ def prometheus_text(summary: Dict[str, Optional[float]], prefix: str = "dllm") -
 
 
 # per-worker gauges of the master's STATUS fan-out (HBM used, KV blocks, queue depth)
-_WORKER_GAUGES = ("hbm_used_bytes", "hbm_total_bytes", "kv_free_blocks", "running", "waiting", "steps")
+_WORKER_GAUGES = ("hbm_used_bytes", "hbm_total_bytes", "kv_free_blocks", "running", "waiting", "steps",
+                  "hop_tx_bytes", "hop_rx_bytes", "hop_tx_bytes_per_s", "hop_rx_bytes_per_s")
 
 
 def _label(v) -> str:

@@ -616,6 +616,19 @@ class WorkerNode:
             free, total = torch.cuda.mem_get_info(torch.device(self.device))
             st["hbm_used_bytes"] = int(total - free)
             st["hbm_total_bytes"] = int(total)
+        tp = getattr(self, "_transport", None)
+        if tp is not None:                   # this stage's activation / ids hops
+            hs = tp.hop_stats()
+            tx = sum(v for k, v in hs.items() if k.endswith("_tx"))
+            rx = sum(v for k, v in hs.items() if k.endswith("_rx"))
+            now = time.monotonic()
+            prev = getattr(self, "_hop_prev", None)
+            if prev is not None and now > prev[0]:
+                st["hop_tx_bytes_per_s"] = (tx - prev[1]) / (now - prev[0])
+                st["hop_rx_bytes_per_s"] = (rx - prev[2]) / (now - prev[0])
+            self._hop_prev = (now, tx, rx)
+            st["hop_tx_bytes"], st["hop_rx_bytes"] = tx, rx
+            st["transport"] = getattr(tp, "kind", "")
         t = self.driver or self.engine
         if t is not None:
             st["running"] = t.scheduler.num_running()

@@ -46,6 +46,10 @@ def test_torchrun_bench_cpu(n, par, trace, tmp_path):
     if par == "pp":                 # CPU stages run one slot per stage (config.pipeline_slots)
         assert rec["microbatch_slots"] == n
         assert rec["config"]["global_batch"] == 3 * n
+        # every stage but the last sends activations; the last sends the ids back to stage 0
+        assert len(rec["hop_tx_MBps"]) == n and all(v > 0 for v in rec["hop_tx_MBps"])
+        assert rec["transport"] == "torch" and all(v > 0 for v in rec["meta_MBps"][:-1])
+    assert rec["ttft_p50_ms"] > 0 and rec["itl_p50_ms"] > 0 and rec["ttft_p99_ms"] >= rec["ttft_p50_ms"]
     if par == "tp":                 # one TP group: one engine's batch
         assert rec["config"]["global_batch"] == 3
     if trace:   # every rank wrote a timeline; every stage reports its busy fraction
@@ -65,6 +69,7 @@ def test_single_process_bench_json_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_lines(r.stdout)[0]
     assert KEYS <= set(rec) and rec["n_gpus"] == 1
+    assert rec["ttft_p50_ms"] > 0 and rec["itl_p50_ms"] > 0 and rec["kernel_knobs"] == {}
 
 
 @pytest.mark.slow

@@ -321,3 +321,37 @@ def test_transport_resolution(monkeypatch):
     assert resolve_transport("auto", "cpu", False) == "torch"
     monkeypatch.setenv("DLLM_TRANSPORT", "torch")
     assert resolve_transport("rccl", "cuda:1", False) == "torch"
+
+
+def test_transport_hop_accounting():
+    """Every transport counts the bytes its hops move (activations, ids, metadata), once per call
+    even where a subclass method calls its parent's."""
+    import numpy as np
+    from distributed_llms_amd.parallel.comm import LoopbackHub
+    hub = LoopbackHub(2)
+    t0, t1 = hub.transport(0), hub.transport(1)
+    t0.send_meta(np.arange(10, dtype=np.int32))
+    t1.recv_meta()
+    t0.send_hidden(torch.randn(3, 8))
+    t1.recv_hidden(3, 8, torch.float32, "cpu")
+    t1.send_ids(torch.tensor([1, 2, 3], dtype=torch.int32))
+    t0.recv_ids(3, "cpu")
+    assert t0.hop_stats() == {"meta_tx": 48, "hidden_tx": 96, "ids_rx": 12}
+    assert t1.hop_stats() == {"meta_rx": 48, "hidden_rx": 96, "ids_tx": 12}
+
+    from distributed_llms_amd.parallel.comm import LoopbackTransport
+
+    class Sub(LoopbackTransport):
+        def send_hidden(self, t):
+            return super().send_hidden(t)
+    t2 = Sub(hub, 0)
+    t2.send_hidden(torch.zeros(2, 8))
+    assert t2.hop_stats() == {"hidden_tx": 64}
+
+
+def test_cluster_metrics_render_hop_gauges():
+    from distributed_llms_amd.utils.metrics import cluster_prometheus_text
+    txt = cluster_prometheus_text({"metrics": {}, "stage_workers": ["w0"], "workers": {
+        "w0": {"remote": {"role": "driver", "hop_tx_bytes": 1024, "hop_tx_bytes_per_s": 2.5e9}}}})
+    assert 'dllm_worker_hop_tx_bytes{worker="w0",stage="0",role="driver"} 1024' in txt
+    assert "dllm_worker_hop_tx_bytes_per_s" in txt
