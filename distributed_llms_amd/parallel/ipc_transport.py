@@ -43,6 +43,8 @@ from .comm import DistTransport
 
 
 class IpcTransport(DistTransport):
+    kind = "ipc"
+
     def __init__(self, ranks, stage: int, ctrl_group, device, max_rows: int, hidden: int, dtype=torch.bfloat16,
                  ring_group=None, window: int = 2):
         """``window``: the most microbatches in flight in the pipeline; the ring gets window + 1 slots."""
