@@ -70,12 +70,12 @@ def decode_impls(x, n, k, sw, role):
             continue
         base = gemm.pp_splits(m, n, k, bn)
         for s in sorted({max(1, base // 2), base} | ({1, 2} if sw else set())):
-            for nt in (0, 2):
+            for nt in (0, 2, 64):              # 64: schedule 2 (staging spread over the K-tile)
                 v = vb | nt
 
                 def f(w, s=s, v=v):
                     return gemm.linear_pp(x, w, splits=s, swiglu=sw, defer=defer, variant=v)
-                impls[f"pp{bn}s{s}{'nt' if nt else ''}"] = f
+                impls[f"pp{bn}s{s}{ {0: '', 2: 'nt', 64: 'S2'}[nt] }"] = f
     return impls
 
 
@@ -118,10 +118,10 @@ def main():
             x = torch.randn(T, k, device="cuda").to(torch.bfloat16)
             impls = {"blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w))}
             for bn, vb in ((256, 0), (128, 1)):
-                for grp in (0, 4):
+                for grp in (4, 68):                    # grouped order; 68 = grouped + schedule 2
                     v = vb | grp
-                    impls[f"pp{bn}{'g' if grp else ''}"] = (lambda w, v=v: gemm.linear_pp(x, w, splits=1, swiglu=sw,
-                                                                                           variant=v))
+                    impls[f"pp{bn}g{'S2' if grp & 64 else ''}"] = (lambda w, v=v: gemm.linear_pp(
+                        x, w, splits=1, swiglu=sw, variant=v))
             graphs = {key: graph_of(f, [w], 2) for key, f in impls.items()}
             res = {key: [] for key in graphs}
             for _ in range(a.rounds):

@@ -68,6 +68,13 @@ __device__ __forceinline__ void pp_wait_n(int younger) {   // younger: compile-t
 }
 #undef PP_VM
 
+// s_waitcnt vmcnt(N) for a compile-time N
+template <int N>
+__device__ __forceinline__ void pp_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
 // f(integral_constant<int, i>) for i = 0 .. N-1, each i a constant expression
 template <int... I, class F>
 __device__ __forceinline__ void pp_static_for_impl(std::integer_sequence<int, I...>, F&& f) {
@@ -154,13 +161,24 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   constexpr bool PROF = (VAR & 4) != 0;                // diagnostic build: cycle stamps around B_t
   // diagnostic ablations (wrong results, timing only): no LDS-DMA pieces / no fragment reads in the loop
   constexpr bool NOLOAD = (VAR & 8) != 0, NOREAD = (VAR & 16) != 0;
+  // schedule 2 (VAR 32): a K-tile's fragments are all read into registers early in its first K-half,
+  // so its slot is re-staged from then on -- LDS-DMA pieces spread over ~60 % of the K-tile instead
+  // of bunched into half of K-half 1 (see the loop)
+  constexpr bool SCHED2 = (VAR & 32) != 0;
   constexpr bool SWIGLU = MODE == 2;
   constexpr int OUTW = SWIGLU ? BN / 2 : BN;           // output tile width (elements)
-  constexpr int OPITCH = OUTW + 8;                     // LDS output row pitch (elements): +16 B
+  // schedule 2 + SwiGLU: the epilogue stages gate and up as bf16 (the image is the full BN wide)
+  // and applies silu(g) * u while storing -- the fused fp32 form kept the accumulators live
+  // longer and made hipcc shuffle them through VGPRs inside the main loop
+  constexpr bool SWI2 = SWIGLU && SCHED2;
+  constexpr int IMGW = SWI2 ? BN : OUTW;               // LDS image width (elements)
+  constexpr int OPITCH = IMGW + 8;                     // LDS output row pitch (elements): +16 B
   constexpr int SMEM = NB * SLOT > BM * OPITCH ? NB * SLOT : BM * OPITCH;   // ring, then output image
   static_assert(SMEM * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) bf16 smem[SMEM];
 
+  [[maybe_unused]] unsigned long long rt_entry = 0, rt_loop0 = 0, rt_loop1 = 0;
+  if constexpr (PROF) rt_entry = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv >> 1, wn = wv & 1;
@@ -212,9 +230,28 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   // a DUMMY piece -- K-tile nt - 1 again (L2-resident), into a slot nobody reads again -- so that
   // every K-tile of the loop issues exactly G pieces: straight-line MFMA streams and static vmcnt
   // counts
+  // schedule 2 stages through buffer loads: a 32-bit per-lane offset + an SGPR offset per piece
+  // (K-tile, B row group), so no 64-bit VGPR address math in the MFMA stream (register pressure)
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t rsA, rsB;
+  if constexpr (SCHED2) {
+    rsA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)((long)M * K * 2 - (long)ks0 * 128), 0x00020000);
+    rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, (int)((long)N * K * 2 - (long)ks0 * 128), 0x00020000);
+  }
   auto piece = [&](int slot, int ks, int p) {
     bf16* base = smem + slot * SLOT;
     ks = min(ks, nt - 1);                              // wave-uniform: SALU, no per-lane select
+    if constexpr (SCHED2) {
+      if (p < GA) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_vptr_p)(base + (wv * GA + p) * 512), 16, (int)offA[p],
+                                                 ks * PBK * 2, 0, 0);
+      } else {
+        const int q = wv * GB + p - GA;
+        const int brow = pp_b_row<BN, SWIGLU>(8 * q, n_t, N / 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_vptr_p)(base + BM * PBK + q * 512), 16, (int)offB[q & 1],
+                                                 brow * K * 2 + ks * PBK * 2, 0, NT ? 2 : 0);
+      }
+      return;
+    }
     if (p < GA) {
       __builtin_amdgcn_global_load_lds((glb_vptr_p)(Ab + offA[p] + ks * PBK * 2),
                                        (lds_vptr_p)(base + (wv * GA + p) * 512), 16, 0, 0);
@@ -245,7 +282,101 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   // the next K-half's reads are in flight under this one's MFMAs (software pipeline)
   bf16x8 fa0[RT], fb0[CT], fa1[RT], fb1[CT];
 
-  if (nt > 0) {
+  if (nt > 0 && SCHED2) {
+    // ---- schedule 2.  Per K-tile t (slot cur = t % NB), MFMA i = 0 .. 2 NMF - 1 (K-half h = i / NMF):
+    //  * set 0 (fa0, fb0) = K-half 0 fragments, read at the end of the previous K-tile; the first
+    //    MFMA of each row waits with a COUNTED lgkmcnt for exactly its A fragment (row 0: all B);
+    //  * the K-half 1 fragments (set 1) are read from cur one every 2 MFMAs from the start; after
+    //    MFMA IB1 (< NMF): lgkmcnt(0) + barrier -> every wave holds the whole K-tile in registers,
+    //    slot cur is free, and the G pieces of K-tile t + NB are staged into it one every GE MFMAs;
+    //  * after MFMA IB3 (>= NMF, set 0 no longer in use): vmcnt(pieces younger than K-tile t + 1's)
+    //    + barrier -> K-tile t + 1 has landed for every wave; its K-half 0 fragments are read into
+    //    set 0 one every 2 MFMAs.
+    constexpr int NMF = RT * CT, NR = RT + CT;
+    constexpr int IB1 = 2 * NR + 8 < NMF - 1 ? 2 * NR + 8 : NMF - 1;
+    constexpr int GE = (2 * NMF - 4 - IB1 - 1) / G > 1 ? (2 * NMF - 4 - IB1 - 1) / G : 1;
+    constexpr int IB3 = 2 * NMF - 8 - 2 * NR > NMF ? 2 * NMF - 8 - 2 * NR : NMF;
+    constexpr int PB3 = (IB3 - IB1 - 1) / GE + 1 < G ? (IB3 - IB1 - 1) / GE + 1 : G;   // pieces issued by IB3
+    constexpr int VC = (NB - 2) * G + PB3;
+    static_assert(IB1 + 1 + GE * (G - 1) < 2 * NMF && IB3 + 1 + 2 * (NR - 1) < 2 * NMF, "schedule 2 fits a K-tile");
+    static_assert(VC <= 63, "vmcnt");
+    // fragment reads off two base registers per set (A rows, B rows of the slot) with the
+    // fragment's offset in the instruction's immediate field: no address math per read
+    auto rd0 = [&](uint32_t base, auto mc) {           // set-0 read m: B fragments first, then A rows
+      constexpr int m = decltype(mc)::value;
+      if constexpr (m < CT) fb0[m] = pp_frag<m * 16 * 128>(base + b_off);
+      else fa0[m - CT] = pp_frag<(m - CT) * 16 * 128>(base + a_off);
+    };
+    auto rd1 = [&](uint32_t base, auto mc) {
+      constexpr int m = decltype(mc)::value;
+      if constexpr (m < CT) fb1[m] = pp_frag<m * 16 * 128>(base + b_off);
+      else fa1[m - CT] = pp_frag<(m - CT) * 16 * 128>(base + a_off);
+    };
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int p = 0; p < G; ++p) piece(j, j, p);
+    pp_wait_n<G>(NB - 1);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    [[maybe_unused]] unsigned long long st0 = 0, rt0 = 0;
+    if constexpr (PROF) {   // stamped before the counted reads (an s_memtime counts on lgkmcnt)
+      rt0 = __builtin_amdgcn_s_memrealtime();
+      rt_loop0 = rt0;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0) :: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    pp_static_for<NR>([&](auto mc) { rd0(lds_base + lane_off[0], mc); });
+    __builtin_amdgcn_sched_barrier(0);
+    int slot = 0;
+    for (int t = 0; t < nt; ++t) {
+      const int nslot = slot == NB - 1 ? 0 : slot + 1;
+      const uint32_t base1 = lds_base + (uint32_t)(slot * SLOT * 2) + lane_off[1];
+      const uint32_t base0 = lds_base + (uint32_t)(nslot * SLOT * 2) + lane_off[0];
+      pp_static_for<2 * NMF>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, h = i / NMF, j = i % NMF, r = j / CT, c = j % CT;
+        if constexpr (h == 0 && c == 0) {
+          constexpr int w0 = (RT - 1 - r) + (j / 2 < NR ? j / 2 : NR);
+          pp_lgkm<(w0 > 15 ? 15 : w0)>();
+        }
+        if constexpr (h == 0)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[c], fa0[r], acc[r][c], 0, 0, 0);
+        else
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[c], fa1[r], acc[r][c], 0, 0, 0);
+        if constexpr (i % 2 == 1 && i / 2 < NR) {
+          if constexpr (!NOREAD) rd1(base1, std::integral_constant<int, i / 2>{});
+        }
+        if constexpr (i == IB1) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (i > IB1 && (i - IB1 - 1) % GE == 0 && (i - IB1 - 1) / GE < G) {
+          if constexpr (!NOLOAD) piece(slot, t + NB, (i - IB1 - 1) / GE);
+        }
+        if constexpr (i == IB3) {
+          pp_vm<VC>();
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (i > IB3 && (i - IB3 - 1) % 2 == 0 && (i - IB3 - 1) / 2 < NR) {
+          if constexpr (!NOREAD) rd0(base0, std::integral_constant<int, (i - IB3 - 1) / 2>{});
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      slot = nslot;
+    }
+    if constexpr (PROF) {
+      unsigned long long st1;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1) :: "memory");
+      const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      rt_loop1 = rt1;
+      const float vals[4] = {(float)(st1 - st0), 0.f, (float)nt, (float)(rt1 - rt0)};
+      float* rec = D + ((size_t)blockIdx.x * 4 + wv) * 128;
+      if (lane < 4) rec[lane] = vals[lane & 3];
+    }
+  } else if (nt > 0) {
     using SC = PpSched<RT, CT>;
     constexpr int NMF = RT * CT;                       // 64 or 32 MFMAs per K-half
     // prologue: K-tiles 0 .. NB-1 in flight; wait for K-tile 0; read K-half 0 of it in the
@@ -363,7 +494,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const int row = wm * TM + rt * 16 + lr;
-    if constexpr (SWIGLU) {
+    if constexpr (SWIGLU && !SWI2) {
 #pragma unroll
       for (int cp = 0; cp < CT / 2; ++cp) {
         const f32x4 g = acc[rt][2 * cp], u = acc[rt][2 * cp + 1];
@@ -398,17 +529,37 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   const int ch = tid % CPR, r0 = tid / CPR;
   const int ldc = SWIGLU ? N / 2 : N;
   const int col0 = n_t * OUTW + ch * 8;
+  // SWI2: output columns 8 ch .. 8 ch + 7 sit in 16-column group ch / 2 -> gate at image column
+  // 32 (ch / 2) + 8 (ch % 2), up 16 further
+  const int icol = SWI2 ? 32 * (ch >> 1) + 8 * (ch & 1) : ch * 8;
 #pragma unroll 4
   for (int r = r0; r < BM; r += RPI) {
     const int m = m0 + r;
     if (m >= M) break;
-    const int4 v = *reinterpret_cast<const int4*>(smem + r * OPITCH + ch * 8);
+    int4 v = *reinterpret_cast<const int4*>(smem + r * OPITCH + icol);
+    if constexpr (SWI2) {
+      const bf16x8 g = *reinterpret_cast<const bf16x8*>(&v);
+      const bf16x8 u = *reinterpret_cast<const bf16x8*>(smem + r * OPITCH + icol + 16);
+      bf16x8 h;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) h[e] = f2bf(silu_f(bf2f(g[e])) * bf2f(u[e]));
+      v = *reinterpret_cast<const int4*>(&h);
+    }
     if constexpr (MODE == 1) {
       _Float16* Ph = reinterpret_cast<_Float16*>(P);
       *reinterpret_cast<int4*>(Ph + ((size_t)split * M + m) * N + col0) = v;
     } else {
       *reinterpret_cast<int4*>(C + (size_t)m * ldc + col0) = v;
     }
+  }
+  if constexpr (PROF && SCHED2) {   // timeline of this wave (100 MHz ticks) + where it ran
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(hw), "=s"(xcc));
+    const double v8[6] = {(double)rt_entry, (double)rt_loop0, (double)rt_loop1, (double)rt_end, (double)hw, (double)xcc};
+    double* rec = reinterpret_cast<double*>(D + ((size_t)blockIdx.x * 4 + wv) * 128 + 8);
+    if (lane < 6) rec[lane] = v8[lane < 6 ? lane : 0];
   }
 }
 
@@ -439,9 +590,12 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
 #define DLLM_PP_GO(BN_, MODE_, VAR_)                                                                     \
   hipLaunchKernelGGL((gemm_pp_kernel<BN_, MODE_, VAR_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, \
                      (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kps, S, dbg)
-  // variant bit 3: diagnostic build -- per-wave cycle stamps (loop, B_t waits) into the LAST
-  // grid x 512 floats of ws (after the slabs); output as usual.  With it, bit 4: no LDS-DMA pieces
-  // in the loop, bit 5: no fragment reads in the loop (ablations: wrong results, timing only)
+  // variant bit 6: schedule 2 (the K-tile's fragments read early, staging spread; weights never
+  // nontemporal).  Bit 3: diagnostic build -- per-wave cycle stamps (loop, B_t waits) into the LAST
+  // grid x 512 floats of ws (after the slabs); output as usual.  With it (schedule 1 only), bit 4:
+  // no LDS-DMA pieces in the loop, bit 5: no fragment reads in the loop (ablations: wrong results,
+  // timing only)
+  const bool sched2 = (variant & 64) != 0;
   const bool prof = (variant & 8) != 0;
   float* dbg = nullptr;
   if (prof) {
@@ -450,7 +604,11 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
   }
 #define DLLM_PP_V(BN_, MODE_)                                        \
   do {                                                               \
-    if (prof) {                                                      \
+    if (sched2) {                                                    \
+      if (prof) { if (grp) DLLM_PP_GO(BN_, MODE_, 38); else DLLM_PP_GO(BN_, MODE_, 36); } \
+      else if (grp) DLLM_PP_GO(BN_, MODE_, 34);                      \
+      else DLLM_PP_GO(BN_, MODE_, 32);                               \
+    } else if (prof) {                                               \
       if (grp) DLLM_PP_GO(BN_, MODE_, 6);                            \
       else if (variant & 16) DLLM_PP_GO(BN_, MODE_, 12);             \
       else if (variant & 32) DLLM_PP_GO(BN_, MODE_, 20);             \

@@ -284,7 +284,7 @@ def test_sq_deferred_into_fused_norm(cuda):
 @pytest.mark.parametrize("m", [1, 77, 200, 256, 300, 777])
 @pytest.mark.parametrize("n,k,splits", [(6144, 4096, 1), (6144, 4096, 10), (4096, 14336, 16), (512, 192, 3),
                                         (512, 128, 2), (256, 320, 1)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 64, 65, 68, 69])
 def test_pp_linear(cuda, m, n, k, splits, variant):
     x, w = _bf(m, k), _bf(n, k, scale=0.05)
     y = gemm.linear_pp(x, w, splits=splits, variant=variant)
@@ -294,7 +294,7 @@ def test_pp_linear(cuda, m, n, k, splits, variant):
 
 @pytest.mark.parametrize("m", [64, 256, 1000])
 @pytest.mark.parametrize("inter,k,splits", [(14336, 4096, 1), (14336, 4096, 2), (384, 256, 1)])
-@pytest.mark.parametrize("variant", [0, 1, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 4, 5, 6, 64, 65, 68])
 def test_pp_swiglu(cuda, m, inter, k, splits, variant):
     if variant & 1 == 0 and (2 * inter) % 256:
         pytest.skip("256-column tile needs 2I % 256 == 0")
