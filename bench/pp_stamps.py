@@ -18,13 +18,10 @@ import torch
 
 from distributed_llms_amd.ops import gemm
 
-CASES = [  # name, M, N, K, swiglu, splits, variant (| 16: no LDS-DMA in the loop, | 32: no fragment reads)
-    ("gate_up dec", 256, 28672, 4096, True, 1, 1), ("gate_up noload", 256, 28672, 4096, True, 1, 1 | 16),
-    ("gate_up noread", 256, 28672, 4096, True, 1, 1 | 32),
-    ("gate_up dec", 256, 28672, 4096, True, 2, 0), ("gate_up noload", 256, 28672, 4096, True, 2, 16),
-    ("down dec", 256, 4096, 14336, False, 8, 1), ("down noload", 256, 4096, 14336, False, 8, 1 | 16),
-    ("gate pf", 8192, 14336, 4096, False, 1, 4), ("gate pf", 8192, 14336, 4096, False, 1, 5),
-    ("gate pf noload", 8192, 14336, 4096, False, 1, 1 | 16), ("gate pf noread", 8192, 14336, 4096, False, 1, 1 | 32),
+CASES = [  # name, M, N, K, swiglu, splits, variant (| 64: schedule 2, | 16 / 32: schedule-1 ablations)
+    ("gate_up dec S2", 256, 28672, 4096, True, 2, 64), ("gate_up dec", 256, 28672, 4096, True, 1, 1),
+    ("gate pf S2", 8192, 14336, 4096, False, 1, 68), ("gate pf", 8192, 14336, 4096, False, 1, 4),
+    ("gate pf S2 BN128", 8192, 14336, 4096, False, 1, 69),
 ]
 
 
@@ -52,25 +49,29 @@ def main():
         def run(var):
             return gemm.linear_pp(x, ws_[next(it) % copies], splits=s, swiglu=sw, variant=var)
         for _ in range(10):
-            run((v & 7) | 8 | (v & 48))
+            run((v & 7) | 8 | (v & 112))
         torch.cuda.synchronize()
         bn = 128 if v & 1 else 256
         # ablations time the diagnostic build itself (their output is garbage)
         grid = (n // bn) * (-(-m // 256)) * s
-        rec = gemm._workspace(dev)[-grid * 512:].view(grid * 4, 128)[:, :4].cpu()
+        full = gemm._workspace(dev)[-grid * 512:].view(grid * 4, 128).cpu()
+        rec = full[:, :4]
         tot, bt, nt, rt = rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3]
+        b1, b3 = (full[:, 20] / tot).tolist(), (full[:, 21] / tot).tolist()
         rt_ns = rt * 10.0
         ghz = statistics.median((tot / rt_ns).tolist())
         ideal = 2 * 8 * (bn // 32) * 16
         per = (tot / nt).tolist()
         frac = (bt / tot).tolist()
-        t_real = timed(lambda: run((v & 7) | (8 | (v & 48) if v & 48 else 0)))
+        t_real = timed(lambda: run((v & 7) | (v & 64) | (8 | (v & 48) if v & 48 else 0)))
         wg_us = (rt_ns / 1e3).view(-1, 4).max(dim=1).values
         print(f"{name:12s} M={m:5d} N={n:5d} K={k:5d} S={s:2d} BN={bn} var={v}: kernel {t_real:7.1f} us "
               f"({2.0 * m * n * k / t_real / 1e6:5.0f} TF) | WG loop median {statistics.median(wg_us.tolist()):6.1f} us, "
               f"sum/256 {wg_us.sum().item() / 256:7.1f} us | clock {ghz:.2f} GHz | cycles/K-tile "
               f"{statistics.median(per):6.0f} (ideal {ideal}, {ideal / statistics.median(per) * 100:3.0f} %) | "
-              f"B_t share {statistics.median(frac) * 100:4.1f} %", flush=True)
+              f"barrier share {statistics.median(frac) * 100:4.1f} %"
+              + (f" (IB1 {statistics.median(b1) * 100:.1f} %, IB3 {statistics.median(b3) * 100:.1f} %)" if v & 64 else ""),
+              flush=True)
         del ws_, x
         torch.cuda.empty_cache()
 

@@ -1,7 +1,7 @@
 // 4-wave software-pipelined MFMA GEMM for 256-row tiles: C[M,N] = A[M,K] . B[N,K]^T, bf16 in, f32
-// accumulate.  Serves the decode projections at batch 129..256 (one row tile, split-K over
-// workgroups) and the prefill projections (M = tokens, grouped row-tile order, SwiGLU fused into
-// the epilogue).
+// accumulate.  The engine runs the prefill MLP gate|up through it (schedule 2, 256-column tiles,
+// grouped row-tile order, SwiGLU fused into the epilogue: faster than hipBLASLt + silu_mul,
+// profiles/round3_gemm_experiments.md); decode-M split-K forms are kept for experiments.
 //
 // Why this shape (profiles/round3_gemm_counters.md): hipBLASLt's 256 x 256 kernel keeps the MFMA
 // pipe ~82 % busy with ONE wave per SIMD and a 128 x 128 wave tile, while 8-wave designs that
@@ -151,11 +151,12 @@ template <int BN, int MODE, int VAR>
 __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                          bf16* __restrict__ C, float* __restrict__ P, int M, int N,
                                                          int K, int ks_per_split, int nsplit, float* __restrict__ D) {
-  constexpr int BM = 256, TM = 128, TN = BN / 2;       // 4 waves as 2 (M) x 2 (N)
+  constexpr int NW = 4, NWN = 2;
+  constexpr int BM = 256, TM = 128, TN = BN / NWN;     // waves as 2 (M) x NWN (N)
   constexpr int RT = TM / 16, CT = TN / 16;            // 16 x 16 fragments per wave: 8 x 8 or 8 x 4
   constexpr int SLOT = (BM + BN) * PBK;                // bf16 elements per ring slot (one K-tile)
   constexpr int NB = BN == 256 ? 2 : 3;                // K-tiles held in LDS
-  constexpr int GA = BM * PBK * 2 / 1024 / 4, GB = BN * PBK * 2 / 1024 / 4;   // glds per wave per K-tile
+  constexpr int GA = BM * PBK * 2 / 1024 / NW, GB = BN * PBK * 2 / 1024 / NW;  // glds per wave per K-tile
   constexpr int G = GA + GB;
   constexpr bool NT = (VAR & 1) != 0, GROUPED = (VAR & 2) != 0;
   constexpr bool PROF = (VAR & 4) != 0;                // diagnostic build: cycle stamps around B_t
@@ -181,7 +182,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   if constexpr (PROF) rt_entry = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wv >> 1, wn = wv & 1;
+  const int wm = wv / NWN, wn = wv % NWN;
   const int mtiles = (M + BM - 1) / BM;
   const int ntiles = N / BN;
   const int total = gridDim.x;
@@ -282,7 +283,8 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   // the next K-half's reads are in flight under this one's MFMAs (software pipeline)
   bf16x8 fa0[RT], fb0[CT], fa1[RT], fb1[CT];
 
-  if (nt > 0 && SCHED2) {
+  if constexpr (SCHED2) {
+  if (nt > 0) {
     // ---- schedule 2.  Per K-tile t (slot cur = t % NB), MFMA i = 0 .. 2 NMF - 1 (K-half h = i / NMF):
     //  * set 0 (fa0, fb0) = K-half 0 fragments, read at the end of the previous K-tile; the first
     //    MFMA of each row waits with a COUNTED lgkmcnt for exactly its A fragment (row 0: all B);
@@ -316,10 +318,10 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
     for (int j = 0; j < NB; ++j)
 #pragma unroll
       for (int p = 0; p < G; ++p) piece(j, j, p);
-    pp_wait_n<G>(NB - 1);
+    pp_vm<(NB - 1) * G>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    [[maybe_unused]] unsigned long long st0 = 0, rt0 = 0;
+    [[maybe_unused]] unsigned long long st0 = 0, rt0 = 0, sb0 = 0, sb1 = 0, sb3 = 0;
     if constexpr (PROF) {   // stamped before the counted reads (an s_memtime counts on lgkmcnt)
       rt0 = __builtin_amdgcn_s_memrealtime();
       rt_loop0 = rt0;
@@ -347,17 +349,33 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
           if constexpr (!NOREAD) rd1(base1, std::integral_constant<int, i / 2>{});
         }
         if constexpr (i == IB1) {
+          if constexpr (PROF) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sb0) :: "memory");
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
+          if constexpr (PROF) {
+            __builtin_amdgcn_sched_barrier(0);
+            unsigned long long s1;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(s1) :: "memory");
+            sb1 += s1 - sb0;
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
         if constexpr (i > IB1 && (i - IB1 - 1) % GE == 0 && (i - IB1 - 1) / GE < G) {
           if constexpr (!NOLOAD) piece(slot, t + NB, (i - IB1 - 1) / GE);
         }
         if constexpr (i == IB3) {
+          if constexpr (PROF) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sb0) :: "memory");
           pp_vm<VC>();
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
+          if constexpr (PROF) {
+            __builtin_amdgcn_sched_barrier(0);
+            unsigned long long s1;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(s1) :: "memory");
+            sb3 += s1 - sb0;
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
         if constexpr (i > IB3 && (i - IB3 - 1) % 2 == 0 && (i - IB3 - 1) / 2 < NR) {
           if constexpr (!NOREAD) rd0(base0, std::integral_constant<int, (i - IB3 - 1) / 2>{});
@@ -372,11 +390,14 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
       const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_s_waitcnt(0xC07F);
       rt_loop1 = rt1;
-      const float vals[4] = {(float)(st1 - st0), 0.f, (float)nt, (float)(rt1 - rt0)};
+      const float vals[6] = {(float)(st1 - st0), (float)(sb1 + sb3), (float)nt, (float)(rt1 - rt0), (float)sb1,
+                             (float)sb3};
       float* rec = D + ((size_t)blockIdx.x * 4 + wv) * 128;
-      if (lane < 4) rec[lane] = vals[lane & 3];
+      if (lane < 6) rec[lane < 4 ? lane : lane + 16] = vals[lane < 6 ? lane : 0];
     }
-  } else if (nt > 0) {
+  }
+  } else {
+  if (nt > 0) {
     using SC = PpSched<RT, CT>;
     constexpr int NMF = RT * CT;                       // 64 or 32 MFMAs per K-half
     // prologue: K-tiles 0 .. NB-1 in flight; wait for K-tile 0; read K-half 0 of it in the
@@ -486,6 +507,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
       if (lane < 4) rec[lane] = vals[lane & 3];
     }
   }
+  }
   // ---- epilogue: accumulators -> LDS output image (8-byte writes) -> 16-byte row stores.
   // acc[rt][ct] lane l holds C[row wm*TM + rt*16 + (l & 15)][col wn*TN + ct*16 + 4*(l >> 4) + v]
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -525,7 +547,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   }
   __syncthreads();
   constexpr int CPR = OUTW / 8;                        // 16-byte chunks per output row
-  constexpr int RPI = 256 / CPR;                       // rows per pass
+  constexpr int RPI = 64 * NW / CPR;                   // rows per pass
   const int ch = tid % CPR, r0 = tid / CPR;
   const int ldc = SWIGLU ? N / 2 : N;
   const int col0 = n_t * OUTW + ch * 8;

@@ -47,6 +47,12 @@ class Knobs:
     sq_min_m: int = 225
     sq_split: bool = False
     sq_variant: int = 4
+    # prefill-sized GEMMs on gemm_pp.hip (256 x 256 tiles, schedule 2, grouped tile order) from this
+    # M instead of hipBLASLt; 0 = off.  gate|up with the SwiGLU fused into the epilogue:
+    # 1444 vs 1382 TFLOP/s for hipBLASLt + silu_mul at T = 32768 (profiles/round3_gemm_experiments.md);
+    # the plain projections still trail hipBLASLt (1434-1448 vs 1546-1631), so off
+    pp_swiglu_min_m: int = 2048
+    pp_proj_min_m: int = 0
     # ---- attention (ops/__init__.py)
     attn_target_waves: int = 1024     # decode split-KV: waves to aim for (profiles/attn_decode_sweep.txt)
     prefill_attn: int = 4             # prefill kernel version 1..5 (4: LDS-shared K/V tiles)

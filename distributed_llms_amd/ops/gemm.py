@@ -10,10 +10,11 @@ the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..
     M <= knobs.wide_down_max_m (512);
   - the other projections (qkv, o, LM head): M <= knobs.wide_proj_max_m (256);
   with the 256 x 256 tile (gemm_sq.hip) taking unsplit grids at 225 <= M <= 256 (LM head);
-* everything else (prefill, M above the cutovers): hipBLASLt via torch (TunableOp table in
-  tuning/), the only non-HIP GPU path, chosen purely by shape.  (gemm_pp.hip, the 4-wave
-  256-row kernel with the fused SwiGLU epilogue, is callable as :func:`linear_pp`; it does not
-  beat hipBLASLt at prefill yet: profiles/round3_gemm_experiments.md.)
+* prefill gate|up (M >= knobs.pp_swiglu_min_m): gemm_pp.hip, the 4-wave 256 x 256-tile kernel
+  (schedule 2) with the SwiGLU fused into its epilogue -- faster than hipBLASLt + silu_mul
+  (profiles/round3_gemm_experiments.md);
+* everything else (prefill qkv / o / down, M above the cutovers): hipBLASLt via torch (TunableOp
+  table in tuning/), chosen purely by shape (knobs.pp_proj_min_m moves them to gemm_pp).
 
 The role is inferred from the shape: "down" = K >= 8192 and K > N, so the square / widening
 K = 8192 projections of 70B-class models (qkv 8192 -> 10240, o 8192 -> 8192) stay "proj".
@@ -86,7 +87,18 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         raise ValueError(f"linear: x[..., {k}] vs w {tuple(w.shape)}")
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
+    if bias is None and _use_pp(m, n, k, x, w, knobs.K.pp_proj_min_m):
+        return linear_pp(x, w, splits=1, variant=PP_PREFILL_VARIANT)
     return F.linear(x, w, bias)
+
+
+PP_PREFILL_VARIANT = 64 | 4        # gemm_pp: schedule 2, grouped row-tile order, 256-column tile
+
+
+def _use_pp(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, min_m: int) -> bool:
+    """Prefill-sized GEMM on gemm_pp (knobs.pp_swiglu_min_m / pp_proj_min_m)."""
+    return (0 < min_m <= m and n % 256 == 0 and k % 64 == 0 and x.dtype == w.dtype == torch.bfloat16
+            and x.is_contiguous() and w.is_contiguous() and m * k * 2 < (1 << 32) and n * k * 2 < (1 << 32))
 
 
 _ws = {}
@@ -265,4 +277,6 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Te
     m = x.numel() // k
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
+    if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):
+        return linear_pp(x, w_gate_up, splits=1, swiglu=True, variant=PP_PREFILL_VARIANT)
     return None

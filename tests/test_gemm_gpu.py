@@ -298,11 +298,14 @@ def test_pp_linear(cuda, m, n, k, splits, variant):
 def test_pp_swiglu(cuda, m, inter, k, splits, variant):
     if variant & 1 == 0 and (2 * inter) % 256:
         pytest.skip("256-column tile needs 2I % 256 == 0")
+    torch.manual_seed(m * 7 + splits + variant)
     x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
     y = gemm.linear_pp(x, w, splits=splits, swiglu=True, variant=variant)
     gu = x.float() @ w.float().t()
     ref = F.silu(gu[:, :inter]) * gu[:, inter:]
-    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+    # gate and up pass through f16 split-K slabs (splits > 1) or bf16 (schedule 2's two-phase
+    # epilogue) before the SiLU: absolute error up to ~(|u| + 1) x their rounding (|u| ~ 3 here)
+    torch.testing.assert_close(y.float(), ref, atol=6e-2, rtol=3e-2)
 
 
 def test_pp_deferred_splitk_matches_materialized_and_wide(cuda):

@@ -105,3 +105,16 @@ def test_knobs_move_the_cutovers_and_reject_unknown_names():
     assert knobs.parse("wide_variant=1, defer_qkv=1") == {"wide_variant": "1", "defer_qkv": "1"}
     knobs.update(knobs.parse('{"defer_qkv": "true"}'))
     assert knobs.K.defer_qkv is True and "defer_qkv" in knobs.changed()
+
+
+def test_prefill_gate_up_goes_to_gemm_pp():
+    """Prefill gate|up (SwiGLU) runs on gemm_pp's schedule 2 from knobs.pp_swiglu_min_m; the other
+    prefill projections stay on hipBLASLt (pp_proj_min_m = 0)."""
+    from distributed_llms_amd import knobs
+    x, w = _xw(32768, 28672, 4096)
+    assert gemm._use_pp(32768, 28672, 4096, x, w, knobs.K.pp_swiglu_min_m)
+    assert not gemm._use_pp(1024, 28672, 4096, x, w, knobs.K.pp_swiglu_min_m)
+    assert not gemm._use_pp(32768, 6144, 4096, x, w, knobs.K.pp_proj_min_m)
+    assert not gemm._use_pp(32768, 28672 + 128, 4096, x, w, knobs.K.pp_swiglu_min_m)   # N % 256
+    knobs.update(pp_swiglu_min_m=0)
+    assert not gemm._use_pp(32768, 28672, 4096, x, w, knobs.K.pp_swiglu_min_m)
