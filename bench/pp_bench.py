@@ -70,12 +70,12 @@ def decode_impls(x, n, k, sw, role):
             continue
         base = gemm.pp_splits(m, n, k, bn)
         for s in sorted({max(1, base // 2), base} | ({1, 2} if sw else set())):
-            for nt in (0, 2, 64):              # 64: schedule 2 (staging spread over the K-tile)
+            for nt in (0, 2, 64, 66):          # 64: schedule 2 (staging spread over the K-tile), 66: + nt
                 v = vb | nt
 
                 def f(w, s=s, v=v):
                     return gemm.linear_pp(x, w, splits=s, swiglu=sw, defer=defer, variant=v)
-                impls[f"pp{bn}s{s}{ {0: '', 2: 'nt', 64: 'S2'}[nt] }"] = f
+                impls[f"pp{bn}s{s}{ {0: '', 2: 'nt', 64: 'S2', 66: 'S2nt'}[nt] }"] = f
     return impls
 
 

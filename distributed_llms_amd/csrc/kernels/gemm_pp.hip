@@ -612,8 +612,8 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
 #define DLLM_PP_GO(BN_, MODE_, VAR_)                                                                     \
   hipLaunchKernelGGL((gemm_pp_kernel<BN_, MODE_, VAR_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, \
                      (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kps, S, dbg)
-  // variant bit 6: schedule 2 (the K-tile's fragments read early, staging spread; weights never
-  // nontemporal).  Bit 3: diagnostic build -- per-wave cycle stamps (loop, B_t waits) into the LAST
+  // variant bit 6: schedule 2 (the K-tile's fragments read early, staging spread; weights
+  // nontemporal with bit 1 only in the natural tile order).  Bit 3: diagnostic build -- per-wave cycle stamps (loop, B_t waits) into the LAST
   // grid x 512 floats of ws (after the slabs); output as usual.  With it (schedule 1 only), bit 4:
   // no LDS-DMA pieces in the loop, bit 5: no fragment reads in the loop (ablations: wrong results,
   // timing only)
@@ -629,6 +629,7 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
     if (sched2) {                                                    \
       if (prof) { if (grp) DLLM_PP_GO(BN_, MODE_, 38); else DLLM_PP_GO(BN_, MODE_, 36); } \
       else if (grp) DLLM_PP_GO(BN_, MODE_, 34);                      \
+      else if (nt) DLLM_PP_GO(BN_, MODE_, 33);                       \
       else DLLM_PP_GO(BN_, MODE_, 32);                               \
     } else if (prof) {                                               \
       if (grp) DLLM_PP_GO(BN_, MODE_, 6);                            \

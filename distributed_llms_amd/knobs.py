@@ -53,6 +53,9 @@ class Knobs:
     # the plain projections still trail hipBLASLt (1434-1448 vs 1546-1631), so off
     pp_swiglu_min_m: int = 2048
     pp_proj_min_m: int = 0
+    # decode LM head (N > 65536) at pp_head_min_m <= M <= 256 on gemm_pp schedule 2 with nontemporal
+    # weights: 230 vs 265 us for gemm_sq at M = 256 (Llama-3-8B); 0 = off
+    pp_head_min_m: int = 225
     # ---- attention (ops/__init__.py)
     attn_target_waves: int = 1024     # decode split-KV: waves to aim for (profiles/attn_decode_sweep.txt)
     prefill_attn: int = 4             # prefill kernel version 1..5 (4: LDS-shared K/V tiles)

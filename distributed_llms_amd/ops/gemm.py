@@ -9,7 +9,9 @@ the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..
   - down (K >= 8192 and K > N; split-K partials deferred into the next norm):
     M <= knobs.wide_down_max_m (512);
   - the other projections (qkv, o, LM head): M <= knobs.wide_proj_max_m (256);
-  with the 256 x 256 tile (gemm_sq.hip) taking unsplit grids at 225 <= M <= 256 (LM head);
+  with the 256 x 256 tile (gemm_sq.hip) taking unsplit grids at 225 <= M <= 256 (70B gate|up);
+* the decode LM head at 225 <= M <= 256: gemm_pp.hip schedule 2 with nontemporal weights
+  (knobs.pp_head_min_m);
 * prefill gate|up (M >= knobs.pp_swiglu_min_m): gemm_pp.hip, the 4-wave 256 x 256-tile kernel
   (schedule 2) with the SwiGLU fused into its epilogue -- faster than hipBLASLt + silu_mul
   (profiles/round3_gemm_experiments.md);
@@ -85,6 +87,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     m = x.numel() // k
     if w.shape[1] != k:
         raise ValueError(f"linear: x[..., {k}] vs w {tuple(w.shape)}")
+    kn = knobs.K
+    if bias is None and n > 65536 and 0 < kn.pp_head_min_m <= m <= 256 and _use_pp(m, n, k, x, w, 1):
+        return linear_pp(x, w, splits=1, variant=PP_HEAD_VARIANT)           # decode LM head
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
     if bias is None and _use_pp(m, n, k, x, w, knobs.K.pp_proj_min_m):
@@ -93,6 +98,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 PP_PREFILL_VARIANT = 64 | 4        # gemm_pp: schedule 2, grouped row-tile order, 256-column tile
+PP_HEAD_VARIANT = 64 | 2           # gemm_pp: schedule 2, nontemporal weights (read once per step)
 
 
 def _use_pp(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, min_m: int) -> bool:

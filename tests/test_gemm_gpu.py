@@ -284,7 +284,7 @@ def test_sq_deferred_into_fused_norm(cuda):
 @pytest.mark.parametrize("m", [1, 77, 200, 256, 300, 777])
 @pytest.mark.parametrize("n,k,splits", [(6144, 4096, 1), (6144, 4096, 10), (4096, 14336, 16), (512, 192, 3),
                                         (512, 128, 2), (256, 320, 1)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 64, 65, 68, 69])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 64, 65, 66, 68, 69])
 def test_pp_linear(cuda, m, n, k, splits, variant):
     x, w = _bf(m, k), _bf(n, k, scale=0.05)
     y = gemm.linear_pp(x, w, splits=splits, variant=variant)

@@ -118,3 +118,11 @@ def test_prefill_gate_up_goes_to_gemm_pp():
     assert not gemm._use_pp(32768, 28672 + 128, 4096, x, w, knobs.K.pp_swiglu_min_m)   # N % 256
     knobs.update(pp_swiglu_min_m=0)
     assert not gemm._use_pp(32768, 28672, 4096, x, w, knobs.K.pp_swiglu_min_m)
+
+
+def test_decode_lm_head_goes_to_gemm_pp():
+    from distributed_llms_amd import knobs
+    x, w = _xw(256, 128256, 4096)
+    kn = knobs.K
+    assert 0 < kn.pp_head_min_m <= 256 and gemm._use_pp(256, 128256, 4096, x, w, 1)
+    assert gemm.PP_HEAD_VARIANT & 64 and gemm.PP_HEAD_VARIANT & 2
