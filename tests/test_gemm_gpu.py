@@ -66,7 +66,7 @@ def test_small_m_graph_replay(cuda):
         torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("m,n,k", [(256, 4096, 14336), (96, 1024, 8192)])
+@pytest.mark.parametrize("m,n,k", [(256, 4096, 14336), (96, 1024, 8192), (64, 5120, 4096), (32, 8192, 8192)])
 def test_deferred_splitk_fused_add_rms_norm_bit_exact(cuda, m, n, k):
     """linear(defer=True) -> fused_add_rms_norm reduces the split-K partials inside the norm
     kernel; it must equal reduce-then-norm bit for bit, and match the fp32 reference."""
