@@ -83,6 +83,12 @@ def main():
         err = (f_hip().float() - f_blas().float()).abs().max().item()
         print(f"{t:5d} {active:6d} {th * 1e6:9.1f} {nbytes / th / 1e12:9.2f} {tb * 1e6:9.1f} {nbytes / tb / 1e12:9.2f} "
               f"{tb / th:8.2f} {err:8.4f}", flush=True)
+        if t <= moe.GROUPED_MAX_TOKENS:
+            knobs.K.moe_deep_ring = False
+            f_hip()
+            ts = timeit(f_hip, a.iters)
+            knobs.K.moe_deep_ring = True
+            print(f"      3-slot ring: {ts * 1e6:.1f} us ({nbytes / ts / 1e12:.2f} TB/s)", flush=True)
         if t <= moe.GROUPED_MAX_TOKENS and a.variants:
             row = []
             for v in a.variants:

@@ -1,0 +1,234 @@
+// Decode MLP gate|up + SwiGLU at 192 < M <= 256 with every CU busy:
+//   C[M, I] = silu(A Wg^T) * (A Wu^T),  W = [Wg; Wu] ([2I, K], nn.Linear layout), bf16 in, f32 acc.
+//
+// Why a kernel of its own: at M = 256 the SwiGLU-fused gemm_wide tile (256 rows x 64 outputs) gives
+// Llama-3-8B (I = 14336) 224 workgroups -- 32 of the 256 CUs idle -- and this projection is close to
+// MFMA-bound at that M (60 GFLOP against 235 MB of weights; the no-staging ablation of gemm_wide
+// still takes 52 of its 66 us, profiles/wide_gemm.md).  Here a workgroup owns 56 outputs
+// (I / 56 = 256 workgroups for I = 14336, 512 for the 70B's 28672), so the MFMA work spreads over
+// all CUs.
+//
+// Structure (gfx950, wave64, 8 waves = 2 per SIMD):
+//  * tile 256 rows x 112 weight rows x 64 K; the 112 weight rows are 7 MFMA column fragments of
+//    16 = 8 gate rows + the 8 matching up rows, so silu(g) * u pairs lanes l and l ^ 8 of one
+//    16-lane row (DPP row_ror:8 in the epilogue) -- no weight permutation, no [M, 2I] intermediate;
+//  * waves split the rows 8 ways (32 rows each): wave tile 32 x 112 = 2 x 7 accumulators of
+//    v_mfma_f32_16x16x32_bf16, every wave reads all 7 B fragments per 32-deep K step;
+//  * 3-slot LDS ring (46 KiB per K-tile) filled by global_load_lds_dwordx4 (128-byte rows, chunk
+//    swizzle c ^ ((row >> 1) & 7) on the source and the fragment read), two K-tiles in flight, one
+//    counted vmcnt + raw s_barrier per K-tile (gemm_wide.hip's pipeline);
+//  * fragment reads in inline asm with a COUNTED lgkmcnt before each MFMA that first uses a
+//    fragment (hipcc otherwise waits for all 18 reads of a K-tile before its first MFMA);
+//  * the next K-tile's 6 staging pieces per wave are spread over the 28 MFMAs (pinned with
+//    sched_barrier); weights nontemporal (streamed once per step).
+#include "common.h"
+#include "launchers.h"
+
+#include <type_traits>
+#include <utility>
+
+namespace dllm {
+
+namespace {
+constexpr int GU_BM = 256, GU_BN = 112, GU_BK = 64, GU_NBUF = 3;
+constexpr int GU_AEL = GU_BM * GU_BK, GU_BEL = GU_BN * GU_BK, GU_BUF = GU_AEL + GU_BEL;   // bf16 elements
+constexpr int GU_AI = 4, GU_BI = 2, GU_G = GU_AI + GU_BI;   // LDS-DMA pieces per wave per K-tile
+constexpr int GU_RT = 2, GU_CT = 7;                          // wave tile: 2 x 7 16x16 fragments
+constexpr int GU_OUT = GU_BN / 2;                            // 56 outputs per workgroup
+
+typedef __attribute__((address_space(3))) void* lds_vptr_g;
+typedef __attribute__((address_space(1))) void* glb_vptr_g;
+
+__device__ __forceinline__ int gswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int N>
+__device__ __forceinline__ void gu_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int OFF>
+__device__ __forceinline__ bf16x8 gu_frag(uint32_t addr) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+// s_waitcnt lgkmcnt(N) that the two fragments it names depend on (so the MFMAs using them stay
+// after it); N is clamped to the counter's 15 (waiting for a few more reads than needed)
+template <int N>
+__device__ __forceinline__ void gu_lgkm(bf16x8& a, bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N > 15 ? 15 : N));
+}
+
+// weight row of slot row r (0..111) of column tile n_t: fragment c = r / 16, j = r % 16;
+// j < 8 -> gate row, else up row, of output column n_t * 56 + c * 8 + (j & 7)
+__device__ __forceinline__ int gu_w_row(int r, int n_t, int I) {
+  const int c = r >> 4, j = r & 15;
+  return (j >= 8 ? I : 0) + n_t * GU_OUT + c * 8 + (j & 7);
+}
+
+template <int N>
+using gu_ic = std::integral_constant<int, N>;
+
+template <int... Is, class F>
+__device__ __forceinline__ void gu_for_impl(std::integer_sequence<int, Is...>, F&& f) {
+  (f(gu_ic<Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void gu_for(F&& f) {
+  gu_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+}  // namespace
+
+__global__ void __launch_bounds__(512, 1) gemm_gu_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                         bf16* __restrict__ C, int M, int I, int K) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[GU_NBUF * GU_BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int total = gridDim.x;
+  int b = blockIdx.x;
+  {   // bijective XCD remap: consecutive column tiles share an XCD (and its L2 copy of A)
+    const int q = total >> 3, r = total & 7, x = b & 7;
+    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  }
+  const int n_t = b;
+  const int nt = K / GU_BK;
+
+  // staging sources: piece i covers slot rows 8 i .. 8 i + 7, lane -> (row 8 i + lane / 8, physical
+  // chunk lane % 8) <- logical chunk gswz(row, lane % 8).  A: pieces 4 wv + j (rows past M clamp);
+  // B: 14 pieces over 8 waves, wave 7 repeats wave 6's second (identical bytes, same LDS place)
+  const bf16* srcA[GU_AI];
+  const bf16* srcB[GU_BI];
+  int dstB[GU_BI];
+#pragma unroll
+  for (int j = 0; j < GU_AI; ++j) {
+    const int r = 8 * (wv * GU_AI + j) + (lane >> 3);
+    srcA[j] = A + (size_t)min(r, M - 1) * K + gswz(r, lane & 7) * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < GU_BI; ++j) {
+    const int q = min(wv * GU_BI + j, GU_BN / 8 - 1);
+    const int r = 8 * q + (lane >> 3);
+    srcB[j] = B + (size_t)gu_w_row(r, n_t, I) * K + gswz(r, lane & 7) * 8;
+    dstB[j] = GU_AEL + q * 512;
+  }
+  auto piece = [&](int buf, int t, int p) {
+    bf16* base = smem + buf * GU_BUF;
+    const int ko = t * GU_BK;
+    if (p < GU_AI)
+      __builtin_amdgcn_global_load_lds((glb_vptr_g)(srcA[p] + ko), (lds_vptr_g)(base + (wv * GU_AI + p) * 512), 16, 0,
+                                       0);
+    else
+      __builtin_amdgcn_global_load_lds((glb_vptr_g)(srcB[p - GU_AI] + ko), (lds_vptr_g)(base + dstB[p - GU_AI]), 16,
+                                       0, 2);
+  };
+
+  // fragment read addresses: lane (row l & 15, logical chunk 4 s + l / 16) of a 16-row fragment in
+  // K step s; the swizzle of row r0 + x (r0 % 16 == 0) depends on x only, so fragment f of a K step
+  // sits at base_s + f * 2 KiB (immediate offsets)
+  const int fr = lane & 15, fq = lane >> 4;
+  const uint32_t lds0 = (uint32_t)(size_t)(lds_vptr_g)smem;
+  uint32_t aoff[2], boff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    aoff[s] = (uint32_t)(((wv * 32 + fr) * GU_BK + gswz(fr, 4 * s + fq) * 8) * 2);
+    boff[s] = (uint32_t)((GU_AEL + fr * GU_BK + gswz(fr, 4 * s + fq) * 8) * 2);
+  }
+
+  f32x4 acc[GU_RT][GU_CT];
+#pragma unroll
+  for (int r = 0; r < GU_RT; ++r)
+#pragma unroll
+    for (int c = 0; c < GU_CT; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one K-tile from slot `cur`; STG: stage K-tile `tn` into slot `nb` between the MFMAs.
+  // Read order (18 reads): s0: A0 B0..B6 A1, s1: A0 B0..B6 A1.  MFMA (s, rt, ct) waits for its A
+  // fragment (first of its row) and its B fragment (first row) with lgkmcnt = reads issued after.
+  auto ktile = [&](int cur, int nb, int tn, auto stg) {
+    constexpr bool STG = decltype(stg)::value;
+    const uint32_t base = lds0 + (uint32_t)(cur * GU_BUF * 2);
+    bf16x8 fa[2][GU_RT], fb[2][GU_CT];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t ab = base + aoff[s], bb = base + boff[s];
+      fa[s][0] = gu_frag<0>(ab);
+      fb[s][0] = gu_frag<0>(bb);
+      fb[s][1] = gu_frag<2048>(bb);
+      fb[s][2] = gu_frag<4096>(bb);
+      fb[s][3] = gu_frag<6144>(bb);
+      fb[s][4] = gu_frag<8192>(bb);
+      fb[s][5] = gu_frag<10240>(bb);
+      fb[s][6] = gu_frag<12288>(bb);
+      fa[s][1] = gu_frag<2048>(ab);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    gu_for<2 * GU_RT * GU_CT>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int s = i / (GU_RT * GU_CT), rt = (i / GU_CT) % GU_RT, ct = i % GU_CT;
+      // index of the last read this MFMA needs, in issue order
+      constexpr int need = s * 9 + (rt == 0 ? 1 + ct : 8);
+      constexpr int first_use = (rt == 0) || (ct == 0);
+      if constexpr (first_use) {
+        gu_lgkm<17 - need>(fa[s][rt], fb[s][ct]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][rt], fb[s][ct], acc[rt][ct], 0, 0, 0);
+      if constexpr (STG && (i % 4 == 2) && (i / 4 < GU_G)) piece(nb, tn, i / 4);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+
+  if (nt > 0) {
+#pragma unroll
+    for (int p = 0; p < GU_NBUF - 1; ++p)
+      if (p < nt)
+#pragma unroll
+        for (int q = 0; q < GU_G; ++q) piece(p, p, q);
+    int cur = 0, t = 0;
+    for (; t + GU_NBUF - 1 < nt; ++t) {
+      gu_vm<GU_G>();                                   // K-tile t landed; t + 1 may be in flight
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int nb = cur == 0 ? GU_NBUF - 1 : cur - 1;   // slot of K-tile t - 1: free after the barrier
+      ktile(cur, nb, t + GU_NBUF - 1, std::true_type{});
+      cur = cur == GU_NBUF - 1 ? 0 : cur + 1;
+    }
+    for (; t < nt; ++t) {
+      if (t + 1 < nt) gu_vm<GU_G>(); else gu_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      ktile(cur, 0, 0, std::false_type{});
+      cur = cur == GU_NBUF - 1 ? 0 : cur + 1;
+    }
+  }
+
+  // epilogue: acc[rt][ct] lane l holds column (l & 15) of fragment ct -- gate of output
+  // ct * 8 + (l & 7) for l & 15 < 8, its up partner 8 lanes on -- rows wv * 32 + rt * 16 + 4 (l >> 4) + i
+#pragma unroll
+  for (int rt = 0; rt < GU_RT; ++rt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = wv * 32 + rt * 16 + 4 * fq + i;
+#pragma unroll
+      for (int ct = 0; ct < GU_CT; ++ct) {
+        const float g = acc[rt][ct][i];
+        const float u = __int_as_float(
+            __builtin_amdgcn_update_dpp(0, __float_as_int(g), 0x128 /* row_ror:8 */, 0xf, 0xf, false));
+        if (fr < 8 && m < M) C[(size_t)m * I + n_t * GU_OUT + ct * 8 + fr] = f2bf(silu_f(g) * u);
+      }
+    }
+}
+
+// C [M, I] = silu(A Wg^T) * (A Wu^T), W = [Wg; Wu] [2I, K]; 1 <= M <= 256, I % 56 == 0, K % 64 == 0.
+void gemm_gate_up(uintptr_t c, uintptr_t a, uintptr_t w, int M, int I, int K, uintptr_t stream) {
+  DLLM_HOST_CHECK(M >= 1 && M <= GU_BM, "gemm_gate_up: 1 <= M <= 256");
+  DLLM_HOST_CHECK(I % GU_OUT == 0, "gemm_gate_up: I must be a multiple of 56");
+  DLLM_HOST_CHECK(K % GU_BK == 0 && K >= GU_BK, "gemm_gate_up: K must be a positive multiple of 64");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(gemm_gu_kernel, dim3(I / GU_OUT), dim3(512), 0, s, (const bf16*)a, (const bf16*)w, (bf16*)c, M, I,
+                     K);
+  DLLM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dllm

@@ -52,25 +52,26 @@ constexpr int WBN = 128, WBK = 64;
 
 __device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-#define DLLM_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
-// wait until at most `younger` tiles of G LDS-DMA instructions each are still in flight
+template <int N>
+__device__ __forceinline__ void wide_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+// wait until at most `younger` tiles of G LDS-DMA instructions each are still in flight (younger
+// is a compile-time constant after unrolling in the steady state, at most NBUF - 2 <= 6)
 template <int G>
 __device__ __forceinline__ void wait_tiles(int younger) {
-  static_assert(G == 3 || G == 4 || G == 5 || G == 6 || G == 7, "G");
-  if (younger <= 0) { DLLM_VM(0); return; }
-  if constexpr (G == 3) {
-    if (younger == 1) DLLM_VM(3); else if (younger == 2) DLLM_VM(6); else DLLM_VM(9);
-  } else if constexpr (G == 4) {
-    if (younger == 1) DLLM_VM(4); else if (younger == 2) DLLM_VM(8); else DLLM_VM(12);
-  } else if constexpr (G == 5) {
-    if (younger == 1) DLLM_VM(5); else if (younger == 2) DLLM_VM(10); else DLLM_VM(15);
-  } else if constexpr (G == 6) {
-    if (younger == 1) DLLM_VM(6); else if (younger == 2) DLLM_VM(12); else DLLM_VM(18);
-  } else {
-    if (younger == 1) DLLM_VM(7); else if (younger == 2) DLLM_VM(14); else DLLM_VM(21);
+  static_assert(G >= 3 && G <= 9, "G");
+  switch (younger <= 0 ? 0 : younger) {
+    case 0: wide_vm<0>(); break;
+    case 1: wide_vm<G>(); break;
+    case 2: wide_vm<2 * G>(); break;
+    case 3: wide_vm<3 * G>(); break;
+    case 4: wide_vm<4 * G>(); break;
+    case 5: wide_vm<5 * G>(); break;
+    default: wide_vm<(6 * G < 63 ? 6 * G : 63)>(); break;
   }
 }
-#undef DLLM_VM
 
 // Fragment reads the compiler does not count (inline asm), for the SPLITRD K-tile: hipcc waits
 // lgkmcnt(0) before the first MFMA of a K-tile whenever LDS-DMA shares the loop, exposing the
@@ -546,7 +547,7 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_fp8_kernel(const uint8_t* __
 // the decode regime of Mixtral at B >= 128 (32-128 rows per expert), where the weight-streaming
 // grouped kernel (moe.hip) runs its MFMAs at a fraction of the rate.
 // ---------------------------------------------------------------------------------------------
-template <int BM, bool SWIGLU, int VAR, bool FP8 = false>
+template <int BM, bool SWIGLU, int VAR, bool FP8 = false, int NBUF = 3>
 __device__ __forceinline__ void moe_wide_rows(bf16* smem, bf16* __restrict__ Y, const bf16* __restrict__ X,
                                               const int* __restrict__ gather, const bf16* __restrict__ We, int cnt,
                                               int off, int N, int K, int n_t, int wv, int lane,
@@ -575,21 +576,33 @@ __device__ __forceinline__ void moe_wide_rows(bf16* smem, bf16* __restrict__ Y, 
       srcB[j] = We + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * KU + wswz(r, lane & 7) * 8;
     }
     f32x4 acc[RT][4];
-    wide_mainloop<BM, 3, VAR, FP8>(smem, srcA, srcB, KU / WBK, acc, wv, lane);
+    wide_mainloop<BM, NBUF, VAR, FP8>(smem, srcA, srcB, KU / WBK, acc, wv, lane);
     wide_epilogue<BM, false, SWIGLU, FP8>(acc, Y + (size_t)(off + r0) * ldy, nullptr, rows, N, 0, n_t, 0, wm, wn,
                                           lane, FP8 ? sa + off + r0 : nullptr, sb);
     __syncthreads();   // the next chunk's prologue refills buffers other waves may still read
   }
 }
 
-template <bool SWIGLU, bool FP8 = false>
+// Ring depth (moe_wide_nbuf): at 32-128 rows per expert the K loop is bound by weight bytes in
+// flight, not by the MFMAs (a 64-row K-tile is 128 MFMA cycles per SIMD against ~1 us of HBM
+// latency), so the ring is as deep as the 160 KiB of LDS allow: 64-row tiles 6 x 24 KiB (five
+// K-tiles in flight), 128-row tiles 5 x 32 KiB (four).  NBUF_SEL 0 = the 3-slot ring (A/B runs).
+constexpr int MOE_LDS = 5 * (128 + WBN) * WBK;    // bf16 elements (160 KiB)
+template <int BM, int NBUF_SEL>
+constexpr int moe_nbuf() {
+  return NBUF_SEL == 0 ? 3 : (BM == 64 ? 6 : 5);
+}
+
+template <bool SWIGLU, bool FP8 = false, int NBUF_SEL = 1>
 __global__ void __launch_bounds__(512, 1) moe_wide_kernel(bf16* __restrict__ Y, const bf16* __restrict__ X,
                                                           const int* __restrict__ gather, const bf16* __restrict__ W,
                                                           const int* __restrict__ counts,
                                                           const int* __restrict__ offsets, int N, int K, int nt,
                                                           const float* __restrict__ sa = nullptr,
                                                           const float* __restrict__ wscale = nullptr) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[3 * (128 + WBN) * WBK];
+  static_assert(moe_nbuf<64, NBUF_SEL>() * (64 + WBN) * WBK <= MOE_LDS &&
+                moe_nbuf<128, NBUF_SEL>() * (128 + WBN) * WBK <= MOE_LDS, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16 smem[MOE_LDS];
   const int e = blockIdx.y;
   const int cnt = counts[e];
   if (cnt == 0) return;                       // uniform across the workgroup
@@ -597,15 +610,16 @@ __global__ void __launch_bounds__(512, 1) moe_wide_kernel(bf16* __restrict__ Y, 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bf16* We = W + (size_t)e * N * (FP8 ? K / 2 : K);
   const float* sb = FP8 ? wscale + (size_t)e * N : nullptr;
+  constexpr int NB64 = moe_nbuf<64, NBUF_SEL>(), NB128 = moe_nbuf<128, NBUF_SEL>();
   // an expert's weight tile is read once when its rows fit one row tile: stream it nt (variant 2);
   // with several row chunks the re-reads should hit the caches (default policy)
   if (cnt <= 64) {
-    if (nt) moe_wide_rows<64, SWIGLU, 2, FP8>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
-    else moe_wide_rows<64, SWIGLU, 1, FP8>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
+    if (nt) moe_wide_rows<64, SWIGLU, 2, FP8, NB64>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
+    else moe_wide_rows<64, SWIGLU, 1, FP8, NB64>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
   } else if (cnt <= 128 && nt) {
-    moe_wide_rows<128, SWIGLU, 2, FP8>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
+    moe_wide_rows<128, SWIGLU, 2, FP8, NB128>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
   } else {
-    moe_wide_rows<128, SWIGLU, 1, FP8>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
+    moe_wide_rows<128, SWIGLU, 1, FP8, NB128>(smem, Y, X, gather, We, cnt, off, N, K, blockIdx.x, wv, lane, sa, sb);
   }
 }
 
@@ -615,18 +629,20 @@ void moe_wide_gemm(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uint
   DLLM_HOST_CHECK(E >= 1, "experts >= 1");
   DLLM_HOST_CHECK(K % WBK == 0, "K must be a multiple of 64");
   DLLM_HOST_CHECK(N % 128 == 0, "N must be a multiple of 128");
+  // mode bit 2: the 3-slot ring instead of the deep one (A/B runs)
+  const bool shallow = (mode & 4) != 0;
+  mode &= 3;
   DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ntiles = mode == 1 ? (N / 2) / 64 : N / WBN;
   constexpr int nt = 1;   // expert weights are read once per step: nontemporal
-  if (mode == 1)
-    hipLaunchKernelGGL((moe_wide_kernel<true, false>), dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
-                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt,
-                       (const float*)nullptr, (const float*)nullptr);
-  else
-    hipLaunchKernelGGL((moe_wide_kernel<false, false>), dim3(ntiles, E), dim3(512), 0, s, (bf16*)y, (const bf16*)x,
-                       (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, K, nt,
-                       (const float*)nullptr, (const float*)nullptr);
+#define DLLM_MOE_GO(SW_, SEL_)                                                                                   \
+  hipLaunchKernelGGL((moe_wide_kernel<SW_, false, SEL_>), dim3(ntiles, E), dim3(512), 0, s, (bf16*)y,            \
+                     (const bf16*)x, (const int*)gather, (const bf16*)w, (const int*)counts, (const int*)offsets, N, \
+                     K, nt, (const float*)nullptr, (const float*)nullptr)
+  if (mode == 1) { if (shallow) DLLM_MOE_GO(true, 0); else DLLM_MOE_GO(true, 1); }
+  else { if (shallow) DLLM_MOE_GO(false, 0); else DLLM_MOE_GO(false, 1); }
+#undef DLLM_MOE_GO
   DLLM_HIP_CHECK(hipGetLastError());
 }
 

@@ -41,6 +41,10 @@ class Knobs:
     wide_target_wgs: int = 256        # split-K: about one workgroup per CU
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
+    # decode MLP gate|up on gemm_gu.hip (56-output tiles: I / 56 workgroups, every CU busy at
+    # I = 14336) for gu_min_m <= M <= 256 when I / 56 <= gu_max_wgs; 0 = off
+    gu_min_m: int = 193
+    gu_max_wgs: int = 256
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
     # from this M up to 256, unsplit grids only unless sq_split
     sq: str = "all"
@@ -69,6 +73,8 @@ class Knobs:
     moe_variant: int = 0
     moe_wide_min_pairs: int = 8       # token-expert pairs per expert from which the tiled GEMM serves
     moe_fused_router: bool = True
+    # grouped expert GEMM ring depth: 6 / 5 LDS slots at 64 / 128-row tiles (False: 3 slots)
+    moe_deep_ring: bool = True
     # ---- FP8 W8A8 (ops/quant.py)
     fp8_bm128: bool = True
     fp8_group_m: int = 4096

@@ -10,6 +10,8 @@ the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..
     M <= knobs.wide_down_max_m (512);
   - the other projections (qkv, o, LM head): M <= knobs.wide_proj_max_m (256);
   with the 256 x 256 tile (gemm_sq.hip) taking unsplit grids at 225 <= M <= 256 (70B gate|up);
+* the decode MLP gate|up at knobs.gu_min_m <= M <= 256: gemm_gu.hip, 56-output tiles so that
+  I / 56 workgroups (256 at I = 14336) keep every CU busy;
 * the decode LM head at 225 <= M <= 256: gemm_pp.hip schedule 2 with nontemporal weights
   (knobs.pp_head_min_m);
 * prefill gate|up (M >= knobs.pp_swiglu_min_m): gemm_pp.hip, the 4-wave 256 x 256-tile kernel
@@ -276,11 +278,35 @@ def linear_sq(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = 
     return y
 
 
+def use_gate_up56(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Decode gate|up on gemm_gu.hip (knobs.gu_min_m / gu_max_wgs)."""
+    kn = knobs.K
+    inter = n // 2
+    return (0 < kn.gu_min_m <= m <= 256 and n % 2 == 0 and inter % 56 == 0 and inter // 56 <= kn.gu_max_wgs
+            and k % 64 == 0 and x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous())
+
+
+def linear_gate_up56(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) on gemm_gu.hip: 256-row x 56-output tiles (M <= 256, I % 56 == 0)."""
+    k = x.shape[-1]
+    n = w_gate_up.shape[0]
+    m = x.numel() // k
+    if not (1 <= m <= 256 and n % 112 == 0 and k % 64 == 0 and x.dtype == w_gate_up.dtype == torch.bfloat16
+            and x.is_contiguous() and w_gate_up.is_contiguous()):
+        raise ValueError(f"linear_gate_up56: M {m} <= 256, 2I {n} % 112, K {k} % 64, bf16 contiguous")
+    y = torch.empty(*x.shape[:-1], n // 2, dtype=x.dtype, device=x.device)
+    _ext.kernels().gemm_gate_up(y.data_ptr(), x.data_ptr(), w_gate_up.data_ptr(), m, n // 2, k,
+                                torch.cuda.current_stream().cuda_stream)
+    return y
+
+
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Tensor]:
     """silu(x Wg^T) * (x Wu^T) with W = [Wg; Wu] in one launch; None if the shape is not eligible."""
     k = x.shape[-1]
     n = w_gate_up.shape[0]
     m = x.numel() // k
+    if use_gate_up56(m, n, k, x, w_gate_up):
+        return linear_gate_up56(x, w_gate_up)
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
     if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):

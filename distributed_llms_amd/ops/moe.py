@@ -110,9 +110,11 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
         rows = -(-t * top_k // e)        # expected rows per expert picks the kernel's row tile
         if 0 < knobs.K.moe_wide_min_pairs <= t * top_k and x.dtype == torch.bfloat16 and two_i % 128 == 0 and h % 128 == 0 \
                 and h % 64 == 0 and inter % 64 == 0:
+            ring = 0 if knobs.K.moe_deep_ring else 4          # mode bit 2: the 3-slot LDS ring
             k.moe_wide_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
-                            cnt_p, off_p, e_loc, two_i, h, 1, st)
-            k.moe_wide_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, 0, st)
+                            cnt_p, off_p, e_loc, two_i, h, 1 | ring, st)
+            k.moe_wide_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter,
+                            ring, st)
         else:
             k.moe_grouped_gemm(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(),
                                cnt_p, off_p, e_loc, two_i, h, 1, rows, knobs.K.moe_variant, st)

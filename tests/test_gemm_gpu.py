@@ -126,6 +126,33 @@ def test_wide_swiglu(cuda, m, inter, k, splits, variant):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("m", [1, 7, 64, 193, 200, 256])
+@pytest.mark.parametrize("inter,k", [(14336, 4096), (56, 64), (112, 128), (448, 1024), (1120, 320)])
+def test_gate_up56(cuda, m, inter, k):
+    """gemm_gu.hip (56-output tiles, gate/up paired across lanes l, l ^ 8) vs fp32: row tails, one
+    K-tile, K shorter than the ring, I = 56 (one workgroup) to 14336 (256)."""
+    x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
+    y = gemm.linear_gate_up56(x, w)
+    gu = x.float() @ w.float().t()
+    ref = F.silu(gu[:, :inter]) * gu[:, inter:]
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+def test_gate_up56_dispatch_and_graph(cuda):
+    """The engine's swiglu entry takes gemm_gu at M = 256 (Llama-3-8B dims) and replays in a graph."""
+    x, w = _bf(256, 4096), _bf(2 * 14336, 4096, scale=0.05)
+    assert gemm.use_gate_up56(256, 2 * 14336, 4096, x, w)
+    y0 = gemm.linear_swiglu(x, w)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        y = gemm.linear_swiglu(x, w)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+
+
 @pytest.mark.parametrize("m", [1, 37, 128, 200, 256, 300])
 @pytest.mark.parametrize("n,k,splits,swiglu", [(6144, 4096, 5, False), (4096, 14336, 8, False),
                                                (1024, 512, 1, False), (2048, 512, 1, True)])

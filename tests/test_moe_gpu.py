@@ -90,6 +90,26 @@ def test_moe_wide_grouped_kernel(cuda, monkeypatch, t, skew):
     torch.testing.assert_close(out.float(), expect, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("t,h,i", [(64, 128, 128), (150, 512, 384), (256, 1024, 2048), (40, 4096, 256)])
+def test_moe_wide_deep_ring_bit_exact(cuda, monkeypatch, t, h, i):
+    """The deep LDS ring of the grouped expert GEMM (6 / 5 slots) against the 3-slot ring: same
+    K-tile order, so bit-identical outputs; K from 2 K-tiles (shorter than the ring) to 64."""
+    from distributed_llms_amd import knobs
+    monkeypatch.setattr(knobs.K, "moe_wide_min_pairs", 1)
+    e, k = 8, 2
+    x, wr = _bf(t, h), _bf(e, h, scale=0.1)
+    wgu, wd = _bf(e, 2 * i, h, scale=0.05), _bf(e, h, i, scale=0.05)
+    monkeypatch.setattr(knobs.K, "moe_deep_ring", True)
+    deep = moe.forward(x, wr, wgu, wd, k)
+    monkeypatch.setattr(knobs.K, "moe_deep_ring", False)
+    shallow = moe.forward(x, wr, wgu, wd, k)
+    assert torch.equal(deep, shallow)
+    tw, tid = ref.moe_route(ref.linear(x, wr).float(), k)
+    # the bf16 SwiGLU intermediate rounds at K = 4096: tolerance scaled to the output magnitude
+    expect = ref.moe_mlp(x.float(), wgu.float(), wd.float(), tw, tid)
+    torch.testing.assert_close(deep.float(), expect, atol=2e-2 * expect.abs().max().item(), rtol=3e-2)
+
+
 @pytest.mark.parametrize("t", [1, 5, 64, 256])
 @pytest.mark.parametrize("e", [8, 16])
 def test_fused_router_matches_library_path(cuda, monkeypatch, t, e):
