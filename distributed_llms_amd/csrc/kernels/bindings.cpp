@@ -31,6 +31,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("gemm_sq", &dllm::gemm_sq);
   m.def("gemm_pp", &dllm::gemm_pp);
   m.def("gemm_gate_up", &dllm::gemm_gate_up);
+  m.def("gemm_band", &dllm::gemm_band);
   m.def("moe_combine", &dllm::moe_combine);
   m.def("moe_wide_gemm", &dllm::moe_wide_gemm);
   m.def("moe_router_route", &dllm::moe_router_route);

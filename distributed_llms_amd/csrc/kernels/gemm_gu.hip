@@ -30,11 +30,10 @@
 namespace dllm {
 
 namespace {
-constexpr int GU_BM = 256, GU_BN = 112, GU_BK = 64, GU_NBUF = 3;
-constexpr int GU_AEL = GU_BM * GU_BK, GU_BEL = GU_BN * GU_BK, GU_BUF = GU_AEL + GU_BEL;   // bf16 elements
-constexpr int GU_AI = 4, GU_BI = 2, GU_G = GU_AI + GU_BI;   // LDS-DMA pieces per wave per K-tile
-constexpr int GU_RT = 2, GU_CT = 7;                          // wave tile: 2 x 7 16x16 fragments
-constexpr int GU_OUT = GU_BN / 2;                            // 56 outputs per workgroup
+constexpr int GU_BM = 256, GU_BK = 64, GU_NBUF = 3;
+constexpr int GU_AEL = GU_BM * GU_BK;                       // A slot elements (bf16)
+constexpr int GU_AI = 4;                                    // A pieces per wave per K-tile
+constexpr int GU_RT = 2;                                    // 32-row wave band = 2 fragments
 
 typedef __attribute__((address_space(3))) void* lds_vptr_g;
 typedef __attribute__((address_space(1))) void* glb_vptr_g;
@@ -61,11 +60,13 @@ __device__ __forceinline__ void gu_lgkm(bf16x8& a, bf16x8& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N > 15 ? 15 : N));
 }
 
-// weight row of slot row r (0..111) of column tile n_t: fragment c = r / 16, j = r % 16;
-// j < 8 -> gate row, else up row, of output column n_t * 56 + c * 8 + (j & 7)
-__device__ __forceinline__ int gu_w_row(int r, int n_t, int I) {
+// weight row of slot row r (0 .. 16 CT - 1) of column tile n_t.  SwiGLU: fragment c = r / 16,
+// j = r % 16; j < 8 -> gate row, else up row, of output column n_t * 8 CT + c * 8 + (j & 7)
+template <int CT, bool SWIGLU>
+__device__ __forceinline__ int gu_w_row(int r, int n_t, int half) {
+  if constexpr (!SWIGLU) return n_t * 16 * CT + r;
   const int c = r >> 4, j = r & 15;
-  return (j >= 8 ? I : 0) + n_t * GU_OUT + c * 8 + (j & 7);
+  return (j >= 8 ? half : 0) + n_t * 8 * CT + c * 8 + (j & 7);
 }
 
 template <int N>
@@ -81,40 +82,57 @@ __device__ __forceinline__ void gu_for(F&& f) {
 }
 }  // namespace
 
+// MODE 0: C bf16 [M, N];  1: split-K slab P (part_store, common.h) [S, M, N];  2: SwiGLU C [M, N/2].
+// CT: 16-column fragments per workgroup (tile 256 x 16 CT weight rows).
+template <int CT, int MODE>
 __global__ void __launch_bounds__(512, 1) gemm_gu_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                         bf16* __restrict__ C, int M, int I, int K) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[GU_NBUF * GU_BUF];
+                                                         bf16* __restrict__ C, float* __restrict__ P, int M, int N,
+                                                         int K, int kt_per_split, int nsplit) {
+  constexpr bool SWIGLU = MODE == 2;
+  constexpr int BN = 16 * CT, BEL = BN * GU_BK, BUF = GU_AEL + BEL;
+  constexpr int NBP = BN / 8;                                 // B pieces per K-tile
+  constexpr int BI = (NBP + 7) / 8;                           // ... per wave (the excess repeat)
+  constexpr int G = GU_AI + BI;                               // LDS-DMA pieces per wave per K-tile
+  constexpr int NR = CT + 2;                                  // fragment reads per 32-deep K step
+  constexpr int NMF = 2 * GU_RT * CT;                         // MFMAs per wave per K-tile
+  constexpr int GE = NMF / (G + 1) > 0 ? NMF / (G + 1) : 1;   // a staging piece every GE MFMAs
+  static_assert(GU_NBUF * BUF * 2 <= 160 * 1024, "LDS");
+  static_assert(G * GE <= NMF, "pieces fit the MFMA stream");
+  __shared__ __attribute__((aligned(16))) bf16 smem[GU_NBUF * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int total = gridDim.x;
   int b = blockIdx.x;
-  {   // bijective XCD remap: consecutive column tiles share an XCD (and its L2 copy of A)
+  {   // bijective XCD remap: the K slices of a column tile, then neighbouring tiles, share an XCD
     const int q = total >> 3, r = total & 7, x = b & 7;
     b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
   }
-  const int n_t = b;
-  const int nt = K / GU_BK;
+  const int split = b % nsplit, n_t = b / nsplit;
+  const int kt0 = split * kt_per_split;
+  const int nt = max(0, min(K / GU_BK, kt0 + kt_per_split) - kt0);
+  const int half = N / 2;
 
   // staging sources: piece i covers slot rows 8 i .. 8 i + 7, lane -> (row 8 i + lane / 8, physical
   // chunk lane % 8) <- logical chunk gswz(row, lane % 8).  A: pieces 4 wv + j (rows past M clamp);
-  // B: 14 pieces over 8 waves, wave 7 repeats wave 6's second (identical bytes, same LDS place)
+  // B: NBP pieces over 8 waves, a wave past the last repeats it (identical bytes, same LDS place)
   const bf16* srcA[GU_AI];
-  const bf16* srcB[GU_BI];
-  int dstB[GU_BI];
+  const bf16* srcB[BI];
+  int dstB[BI];
 #pragma unroll
   for (int j = 0; j < GU_AI; ++j) {
     const int r = 8 * (wv * GU_AI + j) + (lane >> 3);
-    srcA[j] = A + (size_t)min(r, M - 1) * K + gswz(r, lane & 7) * 8;
+    srcA[j] = A + (size_t)min(r, M - 1) * K + (size_t)kt0 * GU_BK + gswz(r, lane & 7) * 8;
   }
 #pragma unroll
-  for (int j = 0; j < GU_BI; ++j) {
-    const int q = min(wv * GU_BI + j, GU_BN / 8 - 1);
+  for (int j = 0; j < BI; ++j) {
+    const int q = min(wv * BI + j, NBP - 1);
     const int r = 8 * q + (lane >> 3);
-    srcB[j] = B + (size_t)gu_w_row(r, n_t, I) * K + gswz(r, lane & 7) * 8;
+    srcB[j] = B + (size_t)gu_w_row<CT, SWIGLU>(r, n_t, half) * K + (size_t)kt0 * GU_BK + gswz(r, lane & 7) * 8;
     dstB[j] = GU_AEL + q * 512;
   }
+  // weights nontemporal when each byte is read once per step (no K split re-reads none either way)
   auto piece = [&](int buf, int t, int p) {
-    bf16* base = smem + buf * GU_BUF;
+    bf16* base = smem + buf * BUF;
     const int ko = t * GU_BK;
     if (p < GU_AI)
       __builtin_amdgcn_global_load_lds((glb_vptr_g)(srcA[p] + ko), (lds_vptr_g)(base + (wv * GU_AI + p) * 512), 16, 0,
@@ -136,45 +154,37 @@ __global__ void __launch_bounds__(512, 1) gemm_gu_kernel(const bf16* __restrict_
     boff[s] = (uint32_t)((GU_AEL + fr * GU_BK + gswz(fr, 4 * s + fq) * 8) * 2);
   }
 
-  f32x4 acc[GU_RT][GU_CT];
+  f32x4 acc[GU_RT][CT];
 #pragma unroll
   for (int r = 0; r < GU_RT; ++r)
 #pragma unroll
-    for (int c = 0; c < GU_CT; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < CT; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // one K-tile from slot `cur`; STG: stage K-tile `tn` into slot `nb` between the MFMAs.
-  // Read order (18 reads): s0: A0 B0..B6 A1, s1: A0 B0..B6 A1.  MFMA (s, rt, ct) waits for its A
+  // Read order (2 NR reads): per K step A0 B0 .. B(CT-1) A1.  MFMA (s, rt, ct) waits for its A
   // fragment (first of its row) and its B fragment (first row) with lgkmcnt = reads issued after.
   auto ktile = [&](int cur, int nb, int tn, auto stg) {
     constexpr bool STG = decltype(stg)::value;
-    const uint32_t base = lds0 + (uint32_t)(cur * GU_BUF * 2);
-    bf16x8 fa[2][GU_RT], fb[2][GU_CT];
+    const uint32_t base = lds0 + (uint32_t)(cur * BUF * 2);
+    bf16x8 fa[2][GU_RT], fb[2][CT];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t ab = base + aoff[s], bb = base + boff[s];
       fa[s][0] = gu_frag<0>(ab);
-      fb[s][0] = gu_frag<0>(bb);
-      fb[s][1] = gu_frag<2048>(bb);
-      fb[s][2] = gu_frag<4096>(bb);
-      fb[s][3] = gu_frag<6144>(bb);
-      fb[s][4] = gu_frag<8192>(bb);
-      fb[s][5] = gu_frag<10240>(bb);
-      fb[s][6] = gu_frag<12288>(bb);
+      gu_for<CT>([&](auto cc) { fb[s][decltype(cc)::value] = gu_frag<decltype(cc)::value * 2048>(bb); });
       fa[s][1] = gu_frag<2048>(ab);
     }
     __builtin_amdgcn_sched_barrier(0);
-    gu_for<2 * GU_RT * GU_CT>([&](auto ic) {
+    gu_for<NMF>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      constexpr int s = i / (GU_RT * GU_CT), rt = (i / GU_CT) % GU_RT, ct = i % GU_CT;
-      // index of the last read this MFMA needs, in issue order
-      constexpr int need = s * 9 + (rt == 0 ? 1 + ct : 8);
-      constexpr int first_use = (rt == 0) || (ct == 0);
-      if constexpr (first_use) {
-        gu_lgkm<17 - need>(fa[s][rt], fb[s][ct]);
+      constexpr int s = i / (GU_RT * CT), rt = (i / CT) % GU_RT, ct = i % CT;
+      constexpr int need = s * NR + (rt == 0 ? 1 + ct : NR - 1);   // last read this MFMA needs
+      if constexpr (rt == 0 || ct == 0) {
+        gu_lgkm<2 * NR - 1 - need>(fa[s][rt], fb[s][ct]);
         __builtin_amdgcn_sched_barrier(0);
       }
       acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][rt], fb[s][ct], acc[rt][ct], 0, 0, 0);
-      if constexpr (STG && (i % 4 == 2) && (i / 4 < GU_G)) piece(nb, tn, i / 4);
+      if constexpr (STG && (i % GE == GE / 2) && (i / GE < G)) piece(nb, tn, i / GE);
       __builtin_amdgcn_sched_barrier(0);
     });
   };
@@ -184,10 +194,10 @@ __global__ void __launch_bounds__(512, 1) gemm_gu_kernel(const bf16* __restrict_
     for (int p = 0; p < GU_NBUF - 1; ++p)
       if (p < nt)
 #pragma unroll
-        for (int q = 0; q < GU_G; ++q) piece(p, p, q);
+        for (int q = 0; q < G; ++q) piece(p, p, q);
     int cur = 0, t = 0;
     for (; t + GU_NBUF - 1 < nt; ++t) {
-      gu_vm<GU_G>();                                   // K-tile t landed; t + 1 may be in flight
+      gu_vm<G>();                                      // K-tile t landed; t + 1 may be in flight
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const int nb = cur == 0 ? GU_NBUF - 1 : cur - 1;   // slot of K-tile t - 1: free after the barrier
@@ -195,7 +205,7 @@ __global__ void __launch_bounds__(512, 1) gemm_gu_kernel(const bf16* __restrict_
       cur = cur == GU_NBUF - 1 ? 0 : cur + 1;
     }
     for (; t < nt; ++t) {
-      if (t + 1 < nt) gu_vm<GU_G>(); else gu_vm<0>();
+      if (t + 1 < nt) gu_vm<G>(); else gu_vm<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       ktile(cur, 0, 0, std::false_type{});
@@ -203,19 +213,26 @@ __global__ void __launch_bounds__(512, 1) gemm_gu_kernel(const bf16* __restrict_
     }
   }
 
-  // epilogue: acc[rt][ct] lane l holds column (l & 15) of fragment ct -- gate of output
-  // ct * 8 + (l & 7) for l & 15 < 8, its up partner 8 lanes on -- rows wv * 32 + rt * 16 + 4 (l >> 4) + i
+  // epilogue: acc[rt][ct] lane l holds column (l & 15) of fragment ct, rows wv * 32 + rt * 16 +
+  // 4 (l >> 4) + i.  SwiGLU: lane l & 15 < 8 holds the gate of output ct * 8 + (l & 7), its up
+  // partner sits 8 lanes on (DPP row_ror:8 within the 16-lane row)
 #pragma unroll
   for (int rt = 0; rt < GU_RT; ++rt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = wv * 32 + rt * 16 + 4 * fq + i;
 #pragma unroll
-      for (int ct = 0; ct < GU_CT; ++ct) {
-        const float g = acc[rt][ct][i];
-        const float u = __int_as_float(
-            __builtin_amdgcn_update_dpp(0, __float_as_int(g), 0x128 /* row_ror:8 */, 0xf, 0xf, false));
-        if (fr < 8 && m < M) C[(size_t)m * I + n_t * GU_OUT + ct * 8 + fr] = f2bf(silu_f(g) * u);
+      for (int ct = 0; ct < CT; ++ct) {
+        const float v = acc[rt][ct][i];
+        if constexpr (SWIGLU) {
+          const float u = __int_as_float(
+              __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128 /* row_ror:8 */, 0xf, 0xf, false));
+          if (fr < 8 && m < M) C[(size_t)m * half + n_t * 8 * CT + ct * 8 + fr] = f2bf(silu_f(v) * u);
+        } else if (m < M) {
+          const int n = n_t * BN + ct * 16 + fr;
+          if constexpr (MODE == 1) part_store(P, ((size_t)split * M + m) * N + n, v);
+          else C[(size_t)m * N + n] = f2bf(v);
+        }
       }
     }
 }
@@ -223,12 +240,40 @@ __global__ void __launch_bounds__(512, 1) gemm_gu_kernel(const bf16* __restrict_
 // C [M, I] = silu(A Wg^T) * (A Wu^T), W = [Wg; Wu] [2I, K]; 1 <= M <= 256, I % 56 == 0, K % 64 == 0.
 void gemm_gate_up(uintptr_t c, uintptr_t a, uintptr_t w, int M, int I, int K, uintptr_t stream) {
   DLLM_HOST_CHECK(M >= 1 && M <= GU_BM, "gemm_gate_up: 1 <= M <= 256");
-  DLLM_HOST_CHECK(I % GU_OUT == 0, "gemm_gate_up: I must be a multiple of 56");
+  DLLM_HOST_CHECK(I % 56 == 0, "gemm_gate_up: I must be a multiple of 56");
   DLLM_HOST_CHECK(K % GU_BK == 0 && K >= GU_BK, "gemm_gate_up: K must be a positive multiple of 64");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(gemm_gu_kernel, dim3(I / GU_OUT), dim3(512), 0, s, (const bf16*)a, (const bf16*)w, (bf16*)c, M, I,
-                     K);
+  hipLaunchKernelGGL((gemm_gu_kernel<7, 2>), dim3(I / 56), dim3(512), 0, s, (const bf16*)a, (const bf16*)w, (bf16*)c,
+                     (float*)nullptr, M, 2 * I, K, K / GU_BK, 1);
   DLLM_HIP_CHECK(hipGetLastError());
+}
+
+// Plain / split-K form: C = A B^T (mode 0) or split-K slabs in ws (mode 2, S > 1, natural column
+// order as gemm_wide's); 1 <= M <= 256; N % (16 CT) == 0 with CT = ct (6, 7 or 8).  Returns S.
+int gemm_band(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
+              int mode, int ct, uintptr_t stream) {
+  DLLM_HOST_CHECK(M >= 1 && M <= GU_BM, "gemm_band: 1 <= M <= 256");
+  DLLM_HOST_CHECK(ct == 6 || ct == 7 || ct == 8, "gemm_band: ct in 6, 7, 8");
+  DLLM_HOST_CHECK(N % (16 * ct) == 0, "gemm_band: N % (16 ct)");
+  DLLM_HOST_CHECK(K % GU_BK == 0 && K >= GU_BK, "gemm_band: K must be a positive multiple of 64");
+  DLLM_HOST_CHECK(mode == 0 || mode == 2, "gemm_band: mode 0 (bf16) or 2 (slabs)");
+  DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
+  const int ktiles = K / GU_BK, kts = (ktiles + splits - 1) / splits, S = (ktiles + kts - 1) / kts;
+  DLLM_HOST_CHECK(mode == 0 ? S == 1 : S > 1, "gemm_band: mode 2 needs a K split, mode 0 none");
+  if (S > 1) DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const unsigned grid = (unsigned)((N / (16 * ct)) * S);
+#define DLLM_BAND_GO(CT_, MODE_)                                                                                \
+  hipLaunchKernelGGL((gemm_gu_kernel<CT_, MODE_>), dim3(grid), dim3(512), 0, s, (const bf16*)a, (const bf16*)b,  \
+                     (bf16*)c, (float*)ws, M, N, K, kts, S)
+  if (S == 1) {
+    if (ct == 6) DLLM_BAND_GO(6, 0); else if (ct == 7) DLLM_BAND_GO(7, 0); else DLLM_BAND_GO(8, 0);
+  } else {
+    if (ct == 6) DLLM_BAND_GO(6, 1); else if (ct == 7) DLLM_BAND_GO(7, 1); else DLLM_BAND_GO(8, 1);
+  }
+#undef DLLM_BAND_GO
+  DLLM_HIP_CHECK(hipGetLastError());
+  return S;
 }
 
 }  // namespace dllm

@@ -300,6 +300,37 @@ def linear_gate_up56(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     return y
 
 
+def band_splits(m: int, n: int, k: int, ct: int, target_wgs: int = 256) -> int:
+    """K slices for gemm_band: about one workgroup per CU, >= 4 K-tiles (256) per slice."""
+    tiles = n // (16 * ct)
+    return max(1, min(round(target_wgs / max(1, tiles)), (k // 64) // 4, 16))
+
+
+def linear_band(x: torch.Tensor, w: torch.Tensor, splits: int = 0, ct: int = 8, defer: bool = False):
+    """y = x w^T on gemm_gu.hip's band kernel (256 rows x 16 ct columns per workgroup, 8 waves of
+    32-row bands, M <= 256).  Split-K partials are reduced by splitk_reduce, or returned as a
+    :class:`SplitKPartial` with ``defer``."""
+    k = x.shape[-1]
+    n = w.shape[0]
+    m = x.numel() // k
+    if not (1 <= m <= 256 and n % (16 * ct) == 0 and k % 64 == 0 and x.dtype == w.dtype == torch.bfloat16
+            and x.is_contiguous() and w.is_contiguous()):
+        raise ValueError(f"linear_band: M {m} <= 256, N {n} % {16 * ct}, K {k} % 64, bf16 contiguous")
+    s = splits or band_splits(m, n, k, ct)
+    ws = _workspace(x.device)
+    if s > 1 and s * m * n > ws.numel():
+        s = max(1, ws.numel() // (m * n))
+    stream = torch.cuda.current_stream().cuda_stream
+    kern = _ext.kernels()
+    if s == 1:
+        y = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
+        kern.gemm_band(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, 0, m, n, k, 1, 0, ct, stream)
+        return y
+    se = kern.gemm_band(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, ct, stream)
+    part = SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
+    return part if defer else part.materialize()
+
+
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Tensor]:
     """silu(x Wg^T) * (x Wu^T) with W = [Wg; Wu] in one launch; None if the shape is not eligible."""
     k = x.shape[-1]

@@ -138,6 +138,27 @@ def test_gate_up56(cuda, m, inter, k):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("m", [1, 37, 200, 256])
+@pytest.mark.parametrize("n,k,ct,splits", [(4096, 4096, 8, 8), (6144, 4096, 6, 4), (6144, 4096, 8, 5),
+                                           (4096, 14336, 8, 8), (896, 512, 7, 1), (768, 320, 6, 2)])
+def test_band_linear(cuda, m, n, k, ct, splits):
+    """gemm_gu.hip band kernel, plain and split-K (slabs reduced by splitk_reduce), vs fp32."""
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear_band(x, w, splits=splits, ct=ct)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
+def test_band_deferred_matches_wide_slab_layout(cuda):
+    """The band kernel's split-K slabs use gemm_wide's layout: a deferred partial feeds the fused
+    add + RMSNorm exactly like gemm_wide's (same K slicing -> same sums up to MFMA order)."""
+    m, n, k = 256, 4096, 4096
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    p = gemm.linear_band(x, w, splits=8, ct=8, defer=True)
+    assert isinstance(p, gemm.SplitKPartial) and p.splits == 8
+    y = p.materialize()
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
 def test_gate_up56_dispatch_and_graph(cuda):
     """The engine's swiglu entry takes gemm_gu at M = 256 (Llama-3-8B dims) and replays in a graph."""
     x, w = _bf(256, 4096), _bf(2 * 14336, 4096, scale=0.05)
