@@ -18,11 +18,14 @@ def main():
     var = int(os.environ.get("PP_VAR", "4"))
     x, w = bf(8192, 4096), bf(14336, 4096, sc=0.02)
     xd, wd = bf(256, 4096), bf(28672, 4096, sc=0.02)
+    decode_only = os.environ.get("DECODE_ONLY") == "1"
     for _ in range(4):
-        gemm.linear_pp(x, w, splits=1, variant=var)
-        F.linear(x, w)
+        if not decode_only:
+            gemm.linear_pp(x, w, splits=1, variant=var)
+            F.linear(x, w)
+            gemm.linear_pp(xd, wd, splits=1, swiglu=True, variant=1 | 2)
         gemm.linear_wide(xd, wd, swiglu=True)
-        gemm.linear_pp(xd, wd, splits=1, swiglu=True, variant=1 | 2)
+        gemm.linear_gate_up56(xd, wd)
     torch.cuda.synchronize()
 
 

@@ -70,6 +70,11 @@ __device__ __forceinline__ int gu_w_row(int r, int n_t, int half) {
 }
 
 template <int N>
+__device__ __forceinline__ void gu_lgkm1(bf16x8& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(N > 15 ? 15 : N));
+}
+
+template <int N>
 using gu_ic = std::integral_constant<int, N>;
 
 template <int... Is, class F>
@@ -237,14 +242,184 @@ __global__ void __launch_bounds__(512, 1) gemm_gu_kernel(const bf16* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// AREG form: the activations bypass LDS.  With 32-row bands each wave's A fragments are its own
+// (no other wave reads them), so they are loaded straight into VGPRs in MFMA operand layout
+// (16 contiguous bytes per lane: row l & 15, K 8 (l >> 4) .. + 8) three K-tiles ahead; only the
+// weight tile goes through the LDS ring (16 CT rows x 128 B per slot, NB slots).  Per K-tile and
+// CU this drops the LDS traffic from 32 KiB A staging + 8 x 2 KiB A fragment reads + the B share
+// to the B share alone (the LDS array sat ~85 % busy feeding the MFMAs in the form above).
+// Issue order per K-tile j (counted vmcnt): B pieces of K-tile j + NB - 1 between the MFMAs, then
+// the 4 A loads of K-tile j + 3 at its end (into the ring registers K-tile j just released).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bf16x8 gua_load(const bf16* p) {
+  bf16x8 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
+template <int CT, int MODE, int NB>
+__global__ void __launch_bounds__(512, 1) gemm_gua_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                          bf16* __restrict__ C, float* __restrict__ P, int M, int N,
+                                                          int K, int kt_per_split, int nsplit) {
+  constexpr bool SWIGLU = MODE == 2;
+  constexpr int BN = 16 * CT, BUF = BN * GU_BK;              // LDS slot: the weight tile only
+  constexpr int NBP = BN / 8, BI = (NBP + 7) / 8;            // B pieces per K-tile / per wave
+  constexpr int DA = 3;                                       // A K-tiles held in registers
+  constexpr int NMF = 2 * GU_RT * CT;
+  constexpr int GE = NMF / (BI + 1) > 0 ? NMF / (BI + 1) : 1;
+  constexpr int VWAIT = (DA - 1) * (BI + 4);                  // ops younger than K-tile t's A loads
+  static_assert(NB >= 4 && NB * BUF * 2 <= 160 * 1024, "ring");
+  static_assert(VWAIT <= 63, "vmcnt");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NB * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int total = gridDim.x;
+  int b = blockIdx.x;
+  {
+    const int q = total >> 3, r = total & 7, x = b & 7;
+    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  }
+  const int split = b % nsplit, n_t = b / nsplit;
+  const int kt0 = split * kt_per_split;
+  const int nt = max(0, min(K / GU_BK, kt0 + kt_per_split) - kt0);
+  const int half = N / 2;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // A: this lane's operand rows (clamped past M) and K offset within a 32-deep step
+  const bf16* arow[GU_RT];
+#pragma unroll
+  for (int rt = 0; rt < GU_RT; ++rt)
+    arow[rt] = A + (size_t)min(wv * 32 + rt * 16 + fr, M - 1) * K + (size_t)kt0 * GU_BK + fq * 8;
+  // B staging (as gemm_gu_kernel)
+  const bf16* srcB[BI];
+  int dstB[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int q = min(wv * BI + j, NBP - 1);
+    const int r = 8 * q + (lane >> 3);
+    srcB[j] = B + (size_t)gu_w_row<CT, SWIGLU>(r, n_t, half) * K + (size_t)kt0 * GU_BK + gswz(r, lane & 7) * 8;
+    dstB[j] = q * 512;
+  }
+  // K-tiles past this split's range (the pipeline's tail) re-load the last one: static op counts
+  auto bpiece = [&](int slot, int t, int j) {
+    t = min(t, nt - 1);
+    __builtin_amdgcn_global_load_lds((glb_vptr_g)(srcB[j] + t * GU_BK), (lds_vptr_g)(smem + slot * BUF + dstB[j]), 16,
+                                     0, 2);
+  };
+  bf16x8 fa[DA][2][GU_RT];                                  // [ring][K step][row fragment]
+  auto aload = [&](bf16x8 (&dst)[2][GU_RT], int t) {
+    t = min(t, nt - 1);
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int rt = 0; rt < GU_RT; ++rt) dst[st][rt] = gua_load(arow[rt] + t * GU_BK + st * 32);
+  };
+
+  const uint32_t lds0 = (uint32_t)(size_t)(lds_vptr_g)smem;
+  uint32_t boff[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) boff[st] = (uint32_t)((fr * GU_BK + gswz(fr, 4 * st + fq) * 8) * 2);
+
+  f32x4 acc[GU_RT][CT];
+#pragma unroll
+  for (int r = 0; r < GU_RT; ++r)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // K-tile t (slot t % NB, A ring slot R): wait for its A registers and B slot, barrier, B
+  // fragment reads (counted lgkmcnt per first use), MFMAs with the B pieces of K-tile t + NB - 1
+  // spread between them, then the A loads of K-tile t + DA into ring slot R
+  // W: ops issued after K-tile t's A loads (VWAIT in the steady state, fewer in the first DA - 1
+  // K-tiles, whose A loads sit in the prologue)
+  auto step = [&](int t, auto rc, auto wc) {
+    constexpr int R = decltype(rc)::value, W = decltype(wc)::value;
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(fa[R][0][0]), "+v"(fa[R][0][1]), "+v"(fa[R][1][0]), "+v"(fa[R][1][1])
+                 : "i"(W) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int cur = t % NB, nb = (t + NB - 1) % NB;
+    const uint32_t base = lds0 + (uint32_t)(cur * BUF * 2);
+    bf16x8 fb[2][CT];
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+      gu_for<CT>([&](auto cc) { fb[st][decltype(cc)::value] = gu_frag<decltype(cc)::value * 2048>(base + boff[st]); });
+    __builtin_amdgcn_sched_barrier(0);
+    gu_for<NMF>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int st = i / (GU_RT * CT), rt = (i / CT) % GU_RT, ct = i % CT;
+      if constexpr (rt == 0) {
+        gu_lgkm1<2 * CT - 1 - (st * CT + ct)>(fb[st][ct]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[R][st][rt], fb[st][ct], acc[rt][ct], 0, 0, 0);
+      if constexpr ((i % GE == GE / 2) && (i / GE < BI)) bpiece(nb, t + NB - 1, i / GE);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    aload(fa[R], t + DA);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (nt > 0) {
+    // prologue: B K-tiles 0 .. NB - 2 into their slots (one issue group per K-tile, in the order
+    // the loop's counts assume: the B group of K-tile j precedes the A group of K-tile j + DA ...)
+    // -- simplest static order: every B group, then the A groups of K-tiles 0 .. DA - 1
+#pragma unroll
+    for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+      for (int q = 0; q < BI; ++q) bpiece(j, j, q);
+#pragma unroll
+    for (int j = 0; j < DA; ++j) aload(fa[j], j);
+    static_assert(DA == 3, "the loop below is unrolled for DA = 3");
+    // K-tile t < DA: younger than its A group are the later prologue A groups and t full K-tiles
+    step(0, gu_ic<0>{}, gu_ic<4 * (DA - 1)>{});
+    if (nt > 1) step(1, gu_ic<1>{}, gu_ic<4 * (DA - 2) + (BI + 4)>{});
+    if (nt > 2) step(2, gu_ic<2>{}, gu_ic<VWAIT>{});
+    int t = DA;
+    for (; t + DA <= nt; t += DA) {
+      step(t, gu_ic<0>{}, gu_ic<VWAIT>{});
+      step(t + 1, gu_ic<1>{}, gu_ic<VWAIT>{});
+      step(t + 2, gu_ic<2>{}, gu_ic<VWAIT>{});
+    }
+    if (t < nt) step(t, gu_ic<0>{}, gu_ic<VWAIT>{});
+    if (t + 1 < nt) step(t + 1, gu_ic<1>{}, gu_ic<VWAIT>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+#pragma unroll
+  for (int rt = 0; rt < GU_RT; ++rt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = wv * 32 + rt * 16 + 4 * fq + i;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const float v = acc[rt][ct][i];
+        if constexpr (SWIGLU) {
+          const float u = __int_as_float(
+              __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128 /* row_ror:8 */, 0xf, 0xf, false));
+          if (fr < 8 && m < M) C[(size_t)m * half + n_t * 8 * CT + ct * 8 + fr] = f2bf(silu_f(v) * u);
+        } else if (m < M) {
+          const int n = n_t * BN + ct * 16 + fr;
+          if constexpr (MODE == 1) part_store(P, ((size_t)split * M + m) * N + n, v);
+          else C[(size_t)m * N + n] = f2bf(v);
+        }
+      }
+    }
+}
+
 // C [M, I] = silu(A Wg^T) * (A Wu^T), W = [Wg; Wu] [2I, K]; 1 <= M <= 256, I % 56 == 0, K % 64 == 0.
-void gemm_gate_up(uintptr_t c, uintptr_t a, uintptr_t w, int M, int I, int K, uintptr_t stream) {
+void gemm_gate_up(uintptr_t c, uintptr_t a, uintptr_t w, int M, int I, int K, int variant, uintptr_t stream) {
   DLLM_HOST_CHECK(M >= 1 && M <= GU_BM, "gemm_gate_up: 1 <= M <= 256");
   DLLM_HOST_CHECK(I % 56 == 0, "gemm_gate_up: I must be a multiple of 56");
   DLLM_HOST_CHECK(K % GU_BK == 0 && K >= GU_BK, "gemm_gate_up: K must be a positive multiple of 64");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL((gemm_gu_kernel<7, 2>), dim3(I / 56), dim3(512), 0, s, (const bf16*)a, (const bf16*)w, (bf16*)c,
-                     (float*)nullptr, M, 2 * I, K, K / GU_BK, 1);
+  // variant 1: activations straight into registers (gemm_gua_kernel), 6-slot weight ring
+  if (variant == 1)
+    hipLaunchKernelGGL((gemm_gua_kernel<7, 2, 6>), dim3(I / 56), dim3(512), 0, s, (const bf16*)a, (const bf16*)w,
+                       (bf16*)c, (float*)nullptr, M, 2 * I, K, K / GU_BK, 1);
+  else
+    hipLaunchKernelGGL((gemm_gu_kernel<7, 2>), dim3(I / 56), dim3(512), 0, s, (const bf16*)a, (const bf16*)w, (bf16*)c,
+                       (float*)nullptr, M, 2 * I, K, K / GU_BK, 1);
   DLLM_HIP_CHECK(hipGetLastError());
 }
 
@@ -252,6 +427,8 @@ void gemm_gate_up(uintptr_t c, uintptr_t a, uintptr_t w, int M, int I, int K, ui
 // order as gemm_wide's); 1 <= M <= 256; N % (16 CT) == 0 with CT = ct (6, 7 or 8).  Returns S.
 int gemm_band(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
               int mode, int ct, uintptr_t stream) {
+  const bool areg = (ct & 256) != 0;                         // ct | 256: gemm_gua_kernel (A in registers)
+  ct &= 255;
   DLLM_HOST_CHECK(M >= 1 && M <= GU_BM, "gemm_band: 1 <= M <= 256");
   DLLM_HOST_CHECK(ct == 6 || ct == 7 || ct == 8, "gemm_band: ct in 6, 7, 8");
   DLLM_HOST_CHECK(N % (16 * ct) == 0, "gemm_band: N % (16 ct)");
@@ -263,9 +440,15 @@ int gemm_band(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   if (S > 1) DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const unsigned grid = (unsigned)((N / (16 * ct)) * S);
-#define DLLM_BAND_GO(CT_, MODE_)                                                                                \
-  hipLaunchKernelGGL((gemm_gu_kernel<CT_, MODE_>), dim3(grid), dim3(512), 0, s, (const bf16*)a, (const bf16*)b,  \
-                     (bf16*)c, (float*)ws, M, N, K, kts, S)
+#define DLLM_BAND_GO(CT_, MODE_)                                                                                 \
+  do {                                                                                                          \
+    if (areg)                                                                                                   \
+      hipLaunchKernelGGL((gemm_gua_kernel<CT_, MODE_, 6>), dim3(grid), dim3(512), 0, s, (const bf16*)a,          \
+                         (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S);                                 \
+    else                                                                                                        \
+      hipLaunchKernelGGL((gemm_gu_kernel<CT_, MODE_>), dim3(grid), dim3(512), 0, s, (const bf16*)a, (const bf16*)b, \
+                         (bf16*)c, (float*)ws, M, N, K, kts, S);                                                 \
+  } while (0)
   if (S == 1) {
     if (ct == 6) DLLM_BAND_GO(6, 0); else if (ct == 7) DLLM_BAND_GO(7, 0); else DLLM_BAND_GO(8, 0);
   } else {

@@ -45,6 +45,7 @@ class Knobs:
     # I = 14336) for gu_min_m <= M <= 256 when I / 56 <= gu_max_wgs; 0 = off
     gu_min_m: int = 193
     gu_max_wgs: int = 256
+    gu_variant: int = 0               # 1: activations straight into registers (gemm_gua_kernel)
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
     # from this M up to 256, unsplit grids only unless sq_split
     sq: str = "all"

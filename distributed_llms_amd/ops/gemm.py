@@ -286,8 +286,9 @@ def use_gate_up56(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> b
             and k % 64 == 0 and x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous())
 
 
-def linear_gate_up56(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
-    """silu(x Wg^T) * (x Wu^T) on gemm_gu.hip: 256-row x 56-output tiles (M <= 256, I % 56 == 0)."""
+def linear_gate_up56(x: torch.Tensor, w_gate_up: torch.Tensor, variant: int = -1) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) on gemm_gu.hip: 256-row x 56-output tiles (M <= 256, I % 56 == 0).
+    ``variant`` 1: activations straight into registers (gemm_gua_kernel); -1 = knobs.gu_variant."""
     k = x.shape[-1]
     n = w_gate_up.shape[0]
     m = x.numel() // k
@@ -295,7 +296,8 @@ def linear_gate_up56(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
             and x.is_contiguous() and w_gate_up.is_contiguous()):
         raise ValueError(f"linear_gate_up56: M {m} <= 256, 2I {n} % 112, K {k} % 64, bf16 contiguous")
     y = torch.empty(*x.shape[:-1], n // 2, dtype=x.dtype, device=x.device)
-    _ext.kernels().gemm_gate_up(y.data_ptr(), x.data_ptr(), w_gate_up.data_ptr(), m, n // 2, k,
+    v = knobs.K.gu_variant if variant < 0 else variant
+    _ext.kernels().gemm_gate_up(y.data_ptr(), x.data_ptr(), w_gate_up.data_ptr(), m, n // 2, k, v,
                                 torch.cuda.current_stream().cuda_stream)
     return y
 
@@ -306,9 +308,10 @@ def band_splits(m: int, n: int, k: int, ct: int, target_wgs: int = 256) -> int:
     return max(1, min(round(target_wgs / max(1, tiles)), (k // 64) // 4, 16))
 
 
-def linear_band(x: torch.Tensor, w: torch.Tensor, splits: int = 0, ct: int = 8, defer: bool = False):
+def linear_band(x: torch.Tensor, w: torch.Tensor, splits: int = 0, ct: int = 8, defer: bool = False,
+                areg: bool = False):
     """y = x w^T on gemm_gu.hip's band kernel (256 rows x 16 ct columns per workgroup, 8 waves of
-    32-row bands, M <= 256).  Split-K partials are reduced by splitk_reduce, or returned as a
+    32-row bands, M <= 256; ``areg``: activations straight into registers, gemm_gua_kernel).  Split-K partials are reduced by splitk_reduce, or returned as a
     :class:`SplitKPartial` with ``defer``."""
     k = x.shape[-1]
     n = w.shape[0]
@@ -324,9 +327,10 @@ def linear_band(x: torch.Tensor, w: torch.Tensor, splits: int = 0, ct: int = 8, 
     kern = _ext.kernels()
     if s == 1:
         y = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
-        kern.gemm_band(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, 0, m, n, k, 1, 0, ct, stream)
+        kern.gemm_band(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, 0, m, n, k, 1, 0, ct | (256 if areg else 0), stream)
         return y
-    se = kern.gemm_band(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, ct, stream)
+    se = kern.gemm_band(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2,
+                        ct | (256 if areg else 0), stream)
     part = SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
     return part if defer else part.materialize()
 

@@ -128,11 +128,12 @@ def test_wide_swiglu(cuda, m, inter, k, splits, variant):
 
 @pytest.mark.parametrize("m", [1, 7, 64, 193, 200, 256])
 @pytest.mark.parametrize("inter,k", [(14336, 4096), (56, 64), (112, 128), (448, 1024), (1120, 320)])
-def test_gate_up56(cuda, m, inter, k):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_gate_up56(cuda, m, inter, k, variant):
     """gemm_gu.hip (56-output tiles, gate/up paired across lanes l, l ^ 8) vs fp32: row tails, one
-    K-tile, K shorter than the ring, I = 56 (one workgroup) to 14336 (256)."""
+    K-tile, K shorter than the ring, I = 56 (one workgroup) to 14336 (256); variant 1 = A in VGPRs."""
     x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
-    y = gemm.linear_gate_up56(x, w)
+    y = gemm.linear_gate_up56(x, w, variant=variant)
     gu = x.float() @ w.float().t()
     ref = F.silu(gu[:, :inter]) * gu[:, inter:]
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
@@ -141,10 +142,11 @@ def test_gate_up56(cuda, m, inter, k):
 @pytest.mark.parametrize("m", [1, 37, 200, 256])
 @pytest.mark.parametrize("n,k,ct,splits", [(4096, 4096, 8, 8), (6144, 4096, 6, 4), (6144, 4096, 8, 5),
                                            (4096, 14336, 8, 8), (896, 512, 7, 1), (768, 320, 6, 2)])
-def test_band_linear(cuda, m, n, k, ct, splits):
+@pytest.mark.parametrize("areg", [False, True])
+def test_band_linear(cuda, m, n, k, ct, splits, areg):
     """gemm_gu.hip band kernel, plain and split-K (slabs reduced by splitk_reduce), vs fp32."""
     x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    y = gemm.linear_band(x, w, splits=splits, ct=ct)
+    y = gemm.linear_band(x, w, splits=splits, ct=ct, areg=areg)
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
 
 
