@@ -25,7 +25,8 @@ def main():
             F.linear(x, w)
             gemm.linear_pp(xd, wd, splits=1, swiglu=True, variant=1 | 2)
         gemm.linear_wide(xd, wd, swiglu=True)
-        gemm.linear_gate_up56(xd, wd)
+        gemm.linear_gate_up56(xd, wd, variant=0)
+        gemm.linear_gate_up56(xd, wd, variant=1)
     torch.cuda.synchronize()
 
 
