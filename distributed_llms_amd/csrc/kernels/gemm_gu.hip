@@ -252,9 +252,14 @@ __global__ void __launch_bounds__(512, 1) gemm_gu_kernel(const bf16* __restrict_
 // Issue order per K-tile j (counted vmcnt): B pieces of K-tile j + NB - 1 between the MFMAs, then
 // the 4 A loads of K-tile j + 3 at its end (into the ring registers K-tile j just released).
 // ---------------------------------------------------------------------------------------------
+// The A loads are inline asm so that hipcc's waitcnt pass leaves the counting to the kernel (with
+// plain loads it drains vmcnt(0) at every loop head).  The asm destination looks written at issue,
+// so: early-clobber (never shares a register with the address), every ring register stays live
+// until a wait that names it (`+v`), and the kernel's last wait names all of them (the tail's
+// clamped loads must land before the epilogue may reuse their registers).
 __device__ __forceinline__ bf16x8 gua_load(const bf16* p) {
   bf16x8 r;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(r) : "v"(p) : "memory");
   return r;
 }
 
@@ -368,13 +373,19 @@ __global__ void __launch_bounds__(512, 1) gemm_gua_kernel(const bf16* __restrict
     for (int j = 0; j < NB - 1; ++j)
 #pragma unroll
       for (int q = 0; q < BI; ++q) bpiece(j, j, q);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < DA; ++j) aload(fa[j], j);
+    for (int j = 0; j < DA; ++j) {
+      aload(fa[j], j);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     static_assert(DA == 3, "the loop below is unrolled for DA = 3");
     // K-tile t < DA: younger than its A group are the later prologue A groups and t full K-tiles
+    // (the host guarantees nt >= DA per split: no branch here, so hipcc's own vmcnt scoreboard
+    // reaches the loop with one pending-op pattern and keeps counted waits)
     step(0, gu_ic<0>{}, gu_ic<4 * (DA - 1)>{});
-    if (nt > 1) step(1, gu_ic<1>{}, gu_ic<4 * (DA - 2) + (BI + 4)>{});
-    if (nt > 2) step(2, gu_ic<2>{}, gu_ic<VWAIT>{});
+    step(1, gu_ic<1>{}, gu_ic<4 * (DA - 2) + (BI + 4)>{});
+    step(2, gu_ic<2>{}, gu_ic<VWAIT>{});
     int t = DA;
     for (; t + DA <= nt; t += DA) {
       step(t, gu_ic<0>{}, gu_ic<VWAIT>{});
@@ -384,7 +395,13 @@ __global__ void __launch_bounds__(512, 1) gemm_gua_kernel(const bf16* __restrict
     if (t < nt) step(t, gu_ic<0>{}, gu_ic<VWAIT>{});
     if (t + 1 < nt) step(t + 1, gu_ic<1>{}, gu_ic<VWAIT>{});
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  static_assert(DA == 3 && GU_RT == 2, "final wait names every ring register");
+  asm volatile("s_waitcnt vmcnt(0)"
+               : "+v"(fa[0][0][0]), "+v"(fa[0][0][1]), "+v"(fa[0][1][0]), "+v"(fa[0][1][1]), "+v"(fa[1][0][0]),
+                 "+v"(fa[1][0][1]), "+v"(fa[1][1][0]), "+v"(fa[1][1][1]), "+v"(fa[2][0][0]), "+v"(fa[2][0][1]),
+                 "+v"(fa[2][1][0]), "+v"(fa[2][1][1])
+               :
+               : "memory");
 
 #pragma unroll
   for (int rt = 0; rt < GU_RT; ++rt)
@@ -414,10 +431,11 @@ void gemm_gate_up(uintptr_t c, uintptr_t a, uintptr_t w, int M, int I, int K, in
   DLLM_HOST_CHECK(K % GU_BK == 0 && K >= GU_BK, "gemm_gate_up: K must be a positive multiple of 64");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // variant 1: activations straight into registers (gemm_gua_kernel), 6-slot weight ring
-  if (variant == 1)
+  if (variant == 1) {
+    DLLM_HOST_CHECK(K >= 3 * GU_BK, "gemm_gate_up variant 1: K >= 192");
     hipLaunchKernelGGL((gemm_gua_kernel<7, 2, 6>), dim3(I / 56), dim3(512), 0, s, (const bf16*)a, (const bf16*)w,
                        (bf16*)c, (float*)nullptr, M, 2 * I, K, K / GU_BK, 1);
-  else
+  } else
     hipLaunchKernelGGL((gemm_gu_kernel<7, 2>), dim3(I / 56), dim3(512), 0, s, (const bf16*)a, (const bf16*)w, (bf16*)c,
                        (float*)nullptr, M, 2 * I, K, K / GU_BK, 1);
   DLLM_HIP_CHECK(hipGetLastError());
@@ -436,6 +454,8 @@ int gemm_band(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   DLLM_HOST_CHECK(mode == 0 || mode == 2, "gemm_band: mode 0 (bf16) or 2 (slabs)");
   DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
   const int ktiles = K / GU_BK, kts = (ktiles + splits - 1) / splits, S = (ktiles + kts - 1) / kts;
+  // gemm_gua_kernel runs >= 3 K-tiles in every split (its pipeline prologue is unconditional)
+  DLLM_HOST_CHECK(!areg || (kts >= 3 && ktiles - (S - 1) * kts >= 3), "gemm_band areg: >= 3 K-tiles per split");
   DLLM_HOST_CHECK(mode == 0 ? S == 1 : S > 1, "gemm_band: mode 2 needs a K split, mode 0 none");
   if (S > 1) DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

@@ -297,6 +297,8 @@ def linear_gate_up56(x: torch.Tensor, w_gate_up: torch.Tensor, variant: int = -1
         raise ValueError(f"linear_gate_up56: M {m} <= 256, 2I {n} % 112, K {k} % 64, bf16 contiguous")
     y = torch.empty(*x.shape[:-1], n // 2, dtype=x.dtype, device=x.device)
     v = knobs.K.gu_variant if variant < 0 else variant
+    if k < 192:
+        v = 0                       # the register-A form runs >= 3 K-tiles
     _ext.kernels().gemm_gate_up(y.data_ptr(), x.data_ptr(), w_gate_up.data_ptr(), m, n // 2, k, v,
                                 torch.cuda.current_stream().cuda_stream)
     return y
@@ -325,6 +327,10 @@ def linear_band(x: torch.Tensor, w: torch.Tensor, splits: int = 0, ct: int = 8, 
         s = max(1, ws.numel() // (m * n))
     stream = torch.cuda.current_stream().cuda_stream
     kern = _ext.kernels()
+    kt = k // 64
+    kts = -(-kt // s)
+    if kts < 3 or kt - (-(-kt // kts) - 1) * kts < 3:
+        areg = False                # the register-A form runs >= 3 K-tiles per split
     if s == 1:
         y = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
         kern.gemm_band(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, 0, m, n, k, 1, 0, ct | (256 if areg else 0), stream)
