@@ -10,8 +10,8 @@ the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..
     M <= knobs.wide_down_max_m (512);
   - the other projections (qkv, o, LM head): M <= knobs.wide_proj_max_m (256);
   with the 256 x 256 tile (gemm_sq.hip) taking unsplit grids at 225 <= M <= 256 (70B gate|up);
-* the decode MLP gate|up at knobs.gu_min_m <= M <= 256: gemm_gu.hip, 56-output tiles so that
-  I / 56 workgroups (256 at I = 14336) keep every CU busy;
+* opt-in (knobs.gu_min_m, off by default: 0.93-1.03x of gemm_wide): the decode MLP gate|up on
+  gemm_gu.hip, 56-output tiles so that I / 56 workgroups (256 at I = 14336) keep every CU busy;
 * the decode LM head at 225 <= M <= 256: gemm_pp.hip schedule 2 with nontemporal weights
   (knobs.pp_head_min_m);
 * prefill gate|up (M >= knobs.pp_swiglu_min_m): gemm_pp.hip, the 4-wave 256 x 256-tile kernel

@@ -161,8 +161,11 @@ def test_band_deferred_matches_wide_slab_layout(cuda):
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
 
 
-def test_gate_up56_dispatch_and_graph(cuda):
-    """The engine's swiglu entry takes gemm_gu at M = 256 (Llama-3-8B dims) and replays in a graph."""
+def test_gate_up56_dispatch_and_graph(cuda, monkeypatch):
+    """With knobs.gu_min_m set, the engine's swiglu entry takes gemm_gu at M = 256 (Llama-3-8B dims)
+    and replays in a graph."""
+    from distributed_llms_amd import knobs
+    monkeypatch.setattr(knobs.K, "gu_min_m", 193)
     x, w = _bf(256, 4096), _bf(2 * 14336, 4096, scale=0.05)
     assert gemm.use_gate_up56(256, 2 * 14336, 4096, x, w)
     y0 = gemm.linear_swiglu(x, w)
