@@ -9,7 +9,7 @@ timeout -k 10 300 python bench/gemm_bench.py --shapes gate_up_8b gate_up_70b qkv
 cat gpurun_out/gu_bench.log
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -40 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log | cut -c1-600
-if [ -n "${SESSION_MOE:-1}" ]; then
+if [ "${SESSION_MOE:-1}" = "1" ]; then
 timeout -k 10 300 python bench/moe_bench.py --tokens 64 128 256 --variants > gpurun_out/moe_bench.log 2>&1 || { echo "moe bench failed"; tail -30 gpurun_out/moe_bench.log; exit 1; }
 cat gpurun_out/moe_bench.log
 timeout -k 10 600 python bench.py --model mixtral-8x7b --batch 256 --steps 2 --warmup 1 > gpurun_out/bench_mixtral.log 2>&1 || { echo "mixtral bench failed"; tail -30 gpurun_out/bench_mixtral.log; exit 1; }
