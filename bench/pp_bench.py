@@ -85,10 +85,11 @@ def main():
     ap.add_argument("--prefill", type=int, nargs="*", default=[32768])
     ap.add_argument("--shapes", nargs="+", default=["qkv", "o", "gate_up", "down"])
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     torch.manual_seed(0)
-    for name in a.shapes:
+    for name in ([] if a.no_decode else a.shapes):
         n, k, sw, role = SHAPES[name]
         copies = max(2, -(-(768 << 20) // (n * k * 2)))
         ws = [(torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(copies)]
@@ -117,8 +118,10 @@ def main():
             w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
             x = torch.randn(T, k, device="cuda").to(torch.bfloat16)
             impls = {"blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w))}
-            for bn, vb in ((256, 0),):
-                for grp in (4, 68):                    # grouped order; 68 = grouped + schedule 2
+            for bn, vb in ((256, 0), (128, 1)):
+                if n % bn:
+                    continue
+                for grp in ((4, 68) if bn == 256 else (68,)):                    # grouped order; 68 = grouped + schedule 2
                     v = vb | grp
                     impls[f"pp{bn}g{'S2' if grp & 64 else ''}"] = (lambda w, v=v: gemm.linear_pp(
                         x, w, splits=1, swiglu=sw, variant=v))
