@@ -67,7 +67,10 @@ class Knobs:
     prefill_attn: int = 4             # prefill kernel version 1..5 (4: LDS-shared K/V tiles)
     # ---- model / engine
     fused_rope: bool = True           # decode: RoPE + KV append fused into attention
-    defer_qkv: bool = False           # split-K qkv consumed by the attention kernel (measured -3 %: off)
+    # split-K qkv partials summed inside the fused RoPE + attention kernel (no splitk_reduce launch):
+    # +0.2-0.6 % tok/s in 4 of 4 interleaved in-engine pairs on two boxes (round 3,
+    # profiles/round3_gemm_experiments.md; a round-2 build measured -3 %)
+    defer_qkv: bool = True
     defer_o: bool = True              # split-K o-proj reduce fused into the next add + RMSNorm
     lookahead: bool = True            # single-GPU engine: issue step n+1 before step n's tokens land
     pp_lookahead: bool = True         # pipeline driver: the same across stages
