@@ -103,8 +103,9 @@ def test_knobs_move_the_cutovers_and_reject_unknown_names():
     with pytest.raises(ValueError):
         knobs.update(no_such_knob=1)
     assert knobs.parse("wide_variant=1, defer_qkv=1") == {"wide_variant": "1", "defer_qkv": "1"}
-    knobs.update(knobs.parse('{"defer_qkv": "true"}'))
-    assert knobs.K.defer_qkv is True and "defer_qkv" in knobs.changed()
+    assert knobs.K.defer_qkv is True and "defer_qkv" not in knobs.changed()      # the shipped default
+    knobs.update(knobs.parse('{"defer_qkv": "false"}'))
+    assert knobs.K.defer_qkv is False and knobs.changed()["defer_qkv"] is False
 
 
 def test_prefill_gate_up_goes_to_gemm_pp():
