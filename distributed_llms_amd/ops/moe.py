@@ -5,7 +5,9 @@ GPU path (bf16):
   moe_route      : softmax -> top-k -> renormalise, expert-sorted slots    (HIP, one launch)
   decode-sized T : grouped weight-streaming GEMMs on the sorted slots (gate|up + SwiGLU, then down)
                    entirely on device -- no host sync, so the decode step stays graph-capturable
-  prefill-sized T: per-expert library GEMMs over the gathered rows (needs the counts on the host)
+  prefill-sized T: per-expert GEMMs over the gathered rows (needs the counts on the host): gate|up
+                   through ops.linear_swiglu (gemm_pp + fused SwiGLU at prefill row counts), down
+                   on hipBLASLt
   moe_combine    : weighted sum of each token's top-k expert outputs        (HIP)
 CPU path: the PyTorch reference (ops/reference.py).
 """
@@ -54,7 +56,7 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
         if fp8:
             return quant.moe_mlp_ref(x, w_gate_up, w_down, tw, tid - expert_offset)
         return ref.moe_mlp(x, w_gate_up, w_down, tw, tid - expert_offset)
-    from . import linear, silu_mul
+    from . import linear, linear_swiglu
     k = _ext.kernels()
     st = torch.cuda.current_stream().cuda_stream
     t, h = x.shape
@@ -126,7 +128,8 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
         for j in range(e_loc):
             a, b = off[expert_offset + j], off[expert_offset + j + 1]
             if b > a:
-                ys[a:b] = F.linear(silu_mul(F.linear(xs[a:b], w_gate_up[j])), w_down[j])
+                # gate|up with the SwiGLU in the GEMM epilogue (gemm_pp at >= 2048 rows per expert)
+                ys[a:b] = F.linear(linear_swiglu(xs[a:b], w_gate_up[j]), w_down[j])
     out = torch.empty_like(x)
     k.moe_combine(out.data_ptr(), ys.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), t, h, top_k, st)
     return out
