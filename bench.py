@@ -60,6 +60,10 @@ def parse(argv=None):
                     help="fp8: W8A8 e4m3 dense projections (opt-in serving mode; the headline stays bf16)")
     ap.add_argument("--streams", type=int, default=1, help="1-GPU engine: microbatch slots on separate streams")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--rate", type=float, default=0.0,
+                    help="open-loop latency mode (1 GPU): requests arrive as a Poisson process of this many "
+                         "requests/s (steps x batch requests in all) instead of a batch per round; reports "
+                         "p50/p99 request latency, TTFT and ITL under that load (the headline mode is unchanged)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace", default=None, metavar="DIR",
                     help="record a roctx/host/GPU timeline of the timed steps: DIR/trace_rank<r>.json "
@@ -183,9 +187,77 @@ def run_single(args):
     emit(args, 1, elapsed, lat, extra)
 
 
+def run_open_loop(args):
+    """Latency under load (plan.md:470-473): one warmup round, then steps x batch requests whose
+    arrivals are a Poisson process of ``--rate`` requests/s (seeded), admitted into the running
+    engine as they arrive (continuous batching).  A request's latency counts from its scheduled
+    arrival, so queueing behind a busy step is included.  One JSON line: p50 request latency is
+    the value (lower is better); p99, TTFT, ITL, offered and achieved rates ride along."""
+    import numpy as np
+    import torch
+    from distributed_llms_amd.config import EngineConfig
+    from distributed_llms_amd.engine.llm_engine import LLMEngine
+    from distributed_llms_amd.engine.sequence import SamplingParams
+    from distributed_llms_amd.utils.metrics import percentile, request_timing, seq_timing
+
+    ecfg = EngineConfig(model=f"synthetic:{args.model}", max_batch=args.batch,
+                        max_prefill_tokens=max(16384, args.batch * args.prompt_len),
+                        max_seq_len=args.prompt_len + args.gen_len + 32, use_graphs=not args.no_graphs,
+                        seed=args.seed, streams=args.streams, quant=args.quant)
+    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    eng = LLMEngine(ecfg)
+    params = SamplingParams(max_new_tokens=args.gen_len, ignore_eos=True)
+    vocab = eng.mcfg.vocab_size
+    for r in range(max(1, args.warmup)):
+        for p in make_prompts(args.batch, args.prompt_len, vocab, 10_000 + r):
+            eng.add_request(p, params)
+        eng.run_until_done()
+    sync()
+    n = args.steps * args.batch
+    rng = np.random.default_rng(args.seed + 7)
+    arrivals = np.cumsum(rng.exponential(1.0 / args.rate, size=n))
+    prompts = make_prompts(n, args.prompt_len, vocab, args.seed)
+    seqs, i = [], 0
+    t0 = time.perf_counter()
+    while i < n or eng.has_work():
+        now = time.perf_counter() - t0
+        while i < n and arrivals[i] <= now:
+            s = eng.add_request(prompts[i], params)
+            s.arrival = t0 + float(arrivals[i])
+            seqs.append(s)
+            i += 1
+        if eng.has_work():
+            eng.step()
+        elif i < n:
+            time.sleep(max(0.0, float(arrivals[i]) - (time.perf_counter() - t0)))
+    sync()
+    elapsed = time.perf_counter() - t0
+    assert all(len(s.output) == args.gen_len for s in seqs)
+    lat = [s.latency() for s in seqs]
+    rec = {"metric": f"request latency under Poisson load (open loop), {args.model}", "value":
+           round(1000 * percentile(lat, 50), 3), "unit": "ms", "higher_is_better": False, "n_gpus": 1,
+           "requests": n, "offered_rate_rps": args.rate, "achieved_rate_rps": round(n / elapsed, 3),
+           "p50_latency_ms": round(1000 * percentile(lat, 50), 3),
+           "p99_latency_ms": round(1000 * percentile(lat, 99), 3),
+           "output_tok_per_s": round(n * args.gen_len / elapsed, 2), "dtype": "bf16" if args.quant == "none" else "fp8",
+           "data": "synthetic (random-init weights, random prompt ids)",
+           "config": {"model": args.model, "max_batch": args.batch, "prompt_len": args.prompt_len,
+                      "gen_len": args.gen_len}, "kernel_knobs": _knobs_changed(),
+           **request_timing(*seq_timing(seqs))}
+    line = json.dumps(rec)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(line + "\n")
+
+
 def main(argv=None):
     args = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.rate > 0:
+        if world > 1 or args.gpus > 1:
+            raise SystemExit("--rate (open-loop latency mode) runs on one GPU")
+        return run_open_loop(args)
     if world > 1 or args.gpus > 1:
         from distributed_llms_amd.parallel.bench_dist import run_distributed
         return run_distributed(args, emit, make_prompts, start_trace, finish_trace)

@@ -57,8 +57,13 @@ _rccl = None
 
 
 def rccl():
-    """The native RCCL p2p module; raises if it is not built."""
+    """The native RCCL p2p module; raises if it is not built.  ``DLLM_RCCL_STANDIN=1`` (tests /
+    rehearsal only) returns parallel/rccl_standin.py instead: the same interface over the
+    torch.distributed store, so the transport's multi-rank path runs where RCCL cannot."""
     global _rccl
+    if os.environ.get("DLLM_RCCL_STANDIN", "0") == "1":
+        from .parallel import rccl_standin
+        return rccl_standin
     if _rccl is None:
         try:
             _rccl = _import("_C_rccl")

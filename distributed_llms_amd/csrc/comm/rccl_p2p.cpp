@@ -14,8 +14,10 @@
 #include <pybind11/pybind11.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <mutex>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -45,6 +47,13 @@ class RcclComm {
   // timeout_s > 0: a NON-BLOCKING communicator -- init and every enqueue that returns
   // ncclInProgress (lazy p2p connection setup) are polled against the deadline, and a peer that
   // never shows up aborts the communicator and raises instead of hanging the rank forever.
+  //
+  // Threading: send / recv / sendrecv release the GIL for the whole enqueue + settle (the first
+  // hop of an edge can wait seconds for its peer: the heartbeat thread, the master handler and
+  // the teardown path must keep running meanwhile).  mu_ serialises the calls that use comm_;
+  // abort() first raises aborting_ -- every settle loop and every later call sees it and leaves
+  // without touching comm_ -- then takes mu_ (bounded wait) and aborts, so a serve thread still
+  // inside a send can never use a communicator abort() has freed.
   RcclComm(int nranks, int rank, const std::string& uid, int device, double timeout_s)
       : nranks_(nranks), rank_(rank), timeout_s_(timeout_s) {
     if (uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("unique id must be 128 bytes");
@@ -53,6 +62,7 @@ class RcclComm {
     std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
     hip_check(hipSetDevice(device), "hipSetDevice");
     py::gil_scoped_release nogil;   // init rendezvous blocks until every rank joins
+    std::lock_guard<std::timed_mutex> g(mu_);
     if (timeout_s_ > 0) {
       ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
       cfg.blocking = 0;
@@ -67,11 +77,15 @@ class RcclComm {
   }
 
   void send(uintptr_t ptr, long nbytes, int peer, uintptr_t stream) {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::timed_mutex> g(mu_);
     live();
     enqueue(ncclSend(reinterpret_cast<const void*>(ptr), (size_t)nbytes, ncclUint8, peer, comm_,
                      reinterpret_cast<hipStream_t>(stream)), "ncclSend");
   }
   void recv(uintptr_t ptr, long nbytes, int peer, uintptr_t stream) {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::timed_mutex> g(mu_);
     live();
     enqueue(ncclRecv(reinterpret_cast<void*>(ptr), (size_t)nbytes, ncclUint8, peer, comm_,
                      reinterpret_cast<hipStream_t>(stream)), "ncclRecv");
@@ -79,6 +93,8 @@ class RcclComm {
   // fused exchange (both directions in one group: no ordering deadlock between the two; also the
   // only legal form of a send to self)
   void sendrecv(uintptr_t sptr, long sbytes, int speer, uintptr_t rptr, long rbytes, int rpeer, uintptr_t stream) {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::timed_mutex> g(mu_);
     live();
     check(ncclGroupStart(), "ncclGroupStart");
     check(ncclSend(reinterpret_cast<const void*>(sptr), (size_t)sbytes, ncclUint8, speer, comm_,
@@ -88,7 +104,10 @@ class RcclComm {
     enqueue(ncclGroupEnd(), "ncclGroupEnd");
   }
   // the communicator's asynchronous error state: "" (healthy), "in_progress", or the error text
-  std::string status() const {
+  std::string status() {
+    if (aborting_.load()) return "aborted";
+    std::unique_lock<std::timed_mutex> g(mu_, std::try_to_lock);
+    if (!g.owns_lock()) return "in_progress";   // a call is settling right now
     if (!comm_) return "aborted";
     ncclResult_t r = ncclSuccess;
     ncclCommGetAsyncError(comm_, &r);
@@ -97,47 +116,58 @@ class RcclComm {
     return ncclGetErrorString(r);
   }
   void abort() {
-    if (comm_) {
-      py::gil_scoped_release nogil;
-      ncclCommAbort(comm_);
-      comm_ = nullptr;
-    }
+    aborting_.store(true);
+    py::gil_scoped_release nogil;
+    // a settling call notices aborting_ within one poll (50 us); a call blocked INSIDE RCCL (a
+    // blocking communicator's lazy connect) never returns on its own: after the bounded wait the
+    // abort goes ahead without the lock -- that call then finds aborting_ set and leaves without
+    // touching comm_
+    std::unique_lock<std::timed_mutex> g(mu_, std::defer_lock);
+    (void)g.try_lock_for(std::chrono::seconds(2));
+    ncclComm_t c = comm_;
+    comm_ = nullptr;
+    if (c) ncclCommAbort(c);
   }
   void destroy() {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::timed_mutex> g(mu_);
     if (comm_) {
-      check(ncclCommDestroy(comm_), "ncclCommDestroy");
+      ncclComm_t c = comm_;
       comm_ = nullptr;
+      check(ncclCommDestroy(c), "ncclCommDestroy");
     }
   }
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }
-  bool alive() const { return comm_ != nullptr; }
+  bool alive() const { return comm_ != nullptr && !aborting_.load(); }
 
  private:
   void live() const {
-    if (!comm_) throw std::runtime_error("RCCL communicator was aborted/destroyed");
+    if (!comm_ || aborting_.load()) throw std::runtime_error("RCCL communicator was aborted/destroyed");
   }
   void enqueue(ncclResult_t r, const char* what) {
+    if (aborting_.load()) throw std::runtime_error(std::string("RCCL ") + what + ": communicator aborted");
     check(r, what);
     if (r == ncclInProgress || timeout_s_ > 0) settle(what);
   }
-  // poll a non-blocking communicator until its last call finished; abort + raise at the deadline
+  // poll a non-blocking communicator until its last call finished; abort + raise at the deadline.
+  // Caller holds mu_.
   void settle(const char* what) {
     if (timeout_s_ <= 0) return;
     const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s_);
     for (;;) {
+      if (aborting_.load()) throw std::runtime_error(std::string("RCCL ") + what + ": communicator aborted");
       ncclResult_t r = ncclSuccess;
       ncclCommGetAsyncError(comm_, &r);
       if (r == ncclSuccess) return;
-      if (r != ncclInProgress) {
-        ncclCommAbort(comm_);
+      if (r != ncclInProgress || std::chrono::steady_clock::now() > t_end) {
+        aborting_.store(true);
+        ncclComm_t c = comm_;
         comm_ = nullptr;
-        throw std::runtime_error(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(r));
-      }
-      if (std::chrono::steady_clock::now() > t_end) {
-        ncclCommAbort(comm_);
-        comm_ = nullptr;
-        throw std::runtime_error(std::string("RCCL ") + what + ": peer did not respond within the timeout");
+        ncclCommAbort(c);
+        throw std::runtime_error(std::string("RCCL ") + what +
+                                 (r != ncclInProgress ? std::string(" failed: ") + ncclGetErrorString(r)
+                                                      : std::string(": peer did not respond within the timeout")));
       }
       std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
@@ -145,6 +175,8 @@ class RcclComm {
   ncclComm_t comm_ = nullptr;
   int nranks_, rank_;
   double timeout_s_;
+  std::timed_mutex mu_;
+  std::atomic<bool> aborting_{false};
 };
 
 }  // namespace

@@ -29,6 +29,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("moe_wide_gemm_fp8", &dllm::moe_wide_gemm_fp8);
   m.def("splitk_add_rms_norm_q8", &dllm::splitk_add_rms_norm_q8);
   m.def("gemm_sq", &dllm::gemm_sq);
+  m.def("gemm_rw", &dllm::gemm_rw);
   m.def("gemm_pp", &dllm::gemm_pp);
   m.def("gemm_gate_up", &dllm::gemm_gate_up);
   m.def("gemm_band", &dllm::gemm_band);

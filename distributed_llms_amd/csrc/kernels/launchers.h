@@ -37,6 +37,8 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
 int gemm_band(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
               int mode, int ct, uintptr_t stream);
 void gemm_gate_up(uintptr_t c, uintptr_t a, uintptr_t w, int M, int I, int K, int variant, uintptr_t stream);
+int gemm_rw(uintptr_t c, uintptr_t a, uintptr_t w, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
+            int mode, int variant, uintptr_t stream);
 int gemm_sq(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream);
 

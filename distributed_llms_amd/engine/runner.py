@@ -53,8 +53,11 @@ class StageRunner:
         self.stage = stage
         self.ecfg = ecfg
         self.tracer = get_tracer()
+        # before any launch / graph capture: defaults (+ DLLM_KNOBS), then this config's overrides --
+        # a previous engine's overrides in the same process must not leak into this one
+        knobs.reset()
         if ecfg.kernel_knobs:
-            knobs.update(ecfg.kernel_knobs)   # before any launch / graph capture
+            knobs.update(ecfg.kernel_knobs)
         if stage.device.type == "cuda":
             enable_tuned_gemms()          # before any graph capture fixes the GEMM solutions
         self.block_size = ecfg.kv_block_size

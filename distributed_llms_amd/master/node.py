@@ -80,6 +80,7 @@ class MasterNode:
         self._tasks: Dict[str, cf.Future] = {}
         self._reqs: Dict[str, Dict[str, Any]] = {}       # task_id -> prompt / params / attempts (for retry)
         self._retry: List[Dict[str, Any]] = []           # requests parked while the pipeline recovers
+        self.max_parked = 4096                            # bound on requests held while degraded
         self._streams: Dict[str, "queue.Queue"] = {}     # task_id -> (offset, new ids) chunks, None = done
         self._acks: Dict[str, cf.Future] = {}
         self._status_futs: Dict[str, cf.Future] = {}
@@ -249,28 +250,37 @@ class MasterNode:
         for fut in list(tasks.values()) + [r["future"] for r in parked]:
             if not fut.done():
                 fut.set_exception(exc)
-        for q in streams:
-            q.put(None)                               # streams end; their futures carry the error
+        # streams end (their futures carry the error) -- the parked ones too: their queues left
+        # self._streams when they were parked
+        for q in streams + [r["stream"] for r in parked if r.get("stream") is not None]:
+            q.put(None)
 
     def _park_inflight(self, exc: Exception):
         """The pipeline lost a stage: keep every in-flight request's future pending and park it
-        for re-submission once the pipeline is back (requests out of retries fail now)."""
+        for re-submission once the pipeline is back.  Fail now: requests out of retries, and
+        SAMPLED streaming requests -- a re-run from the prompt draws different tokens, which the
+        client would get spliced onto the prefix it already streamed (greedy re-runs reproduce the
+        prefix exactly, so the stream resumes where it was)."""
         with self._lock:
             tasks, self._tasks = self._tasks, {}
             reqs, self._reqs = self._reqs, {}
             fail = []
             for tid, fut in tasks.items():
                 r = reqs.get(tid)
+                q = self._streams.pop(tid, None)
                 if fut.done():
                     continue
-                if r is None or r["attempts"] >= self.max_retries:
-                    fail.append(fut)
+                sampled = r is not None and float(r["params"].get("temperature", 0.0) or 0.0) > 0.0
+                if r is None or r["attempts"] >= self.max_retries or (q is not None and sampled):
+                    fail.append((fut, q))
                     continue
                 r["future"] = fut
-                r["stream"] = self._streams.pop(tid, None)
+                r["stream"] = q
                 self._retry.append(r)
-        for fut in fail:
+        for fut, q in fail:
             fut.set_exception(exc)
+            if q is not None:
+                q.put(None)
         log.warning("%d in-flight requests parked for retry, %d failed", len(self._retry), len(fail))
 
     def _resubmit_parked(self):
@@ -283,6 +293,8 @@ class MasterNode:
             except WorkerFailure as e:
                 if not r["future"].done():
                     r["future"].set_exception(e)
+                if r.get("stream") is not None:
+                    r["stream"].put(None)
         if parked:
             log.info("re-submitted %d requests after recovery", len(parked))
 
@@ -480,11 +492,23 @@ class MasterNode:
     # ---------------------------------------------------------------- inference
     def submit(self, prompt_ids: Sequence[int], params: Optional[Dict[str, Any]] = None, _stream_queue=None,
                _task_out=None) -> cf.Future:
-        if self.state != "ready":
-            raise WorkerFailure(f"pipeline not ready (state={self.state})")
         fut: cf.Future = cf.Future()
         fut.t_submit = time.perf_counter()
-        self._send_request(list(prompt_ids), dict(params or {}), fut, _stream_queue, _task_out, 0)
+        ids, params = list(prompt_ids), dict(params or {})
+        with self._lock:
+            # degraded with recovery on: hold the request with the parked in-flight ones (bounded)
+            # until the stage is re-admitted (plan.md:430-436) -- checked under the
+            # lock that _resubmit_parked takes after the state is back to "ready", so a request
+            # is either parked before the resubmission or sent directly after it
+            if self.state == "degraded" and self.auto_recover:
+                if len(self._retry) >= self.max_parked:
+                    raise WorkerFailure(f"pipeline degraded and {len(self._retry)} requests already held")
+                self._retry.append({"ids": ids, "params": params, "attempts": 0, "hint": _task_out,
+                                    "future": fut, "stream": _stream_queue})
+                return fut
+            if self.state != "ready":
+                raise WorkerFailure(f"pipeline not ready (state={self.state})")
+        self._send_request(ids, params, fut, _stream_queue, _task_out, 0)
         return fut
 
     def _send_request(self, ids: List[int], params: Dict[str, Any], fut: cf.Future, stream_q, hint, attempts: int):

@@ -182,6 +182,41 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     return y
 
 
+def rw_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 256) -> int:
+    """K slices for gemm_rw: about one workgroup per CU (128-column tiles x slices), >= 4 K-tiles
+    (256) per slice."""
+    tiles = n // 128
+    return max(1, min(round(target_wgs / max(1, tiles)), (k // 64) // 4, 16))
+
+
+def linear_rw(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = False, defer: bool = False,
+              variant: int = 0):
+    """Register-weight decode GEMM (csrc/kernels/gemm_rw.hip), M <= 256: weights stream straight
+    into VGPRs as MFMA fragments, activations through an LDS-DMA ring; fused SwiGLU (``w`` =
+    [Wg; Wu]) and split-K.  ``defer``: may return a :class:`SplitKPartial` (no SwiGLU).
+    ``variant``: bits 0-3 ring slots (0 = 4), bit 4 weights with the default cache policy."""
+    k = x.shape[-1]
+    n = w.shape[0]
+    m = x.numel() // k
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        raise ValueError("linear_rw: bf16 contiguous operands")
+    if not 1 <= m <= 256 or n % 128 or k % 64:
+        raise ValueError(f"linear_rw: M {m} <= 256, N {n} % 128, K {k} % 64")
+    s = splits or rw_splits(m, n, k, swiglu)
+    ws = _workspace(x.device)
+    if s > 1 and s * m * n > ws.numel():
+        s = max(1, ws.numel() // (m * n))
+    stream = torch.cuda.current_stream().cuda_stream
+    if defer and not swiglu and s > 1:
+        se = _ext.kernels().gemm_rw(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, variant,
+                                    stream)
+        return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
+    y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
+    _ext.kernels().gemm_rw(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s,
+                           1 if swiglu else 0, variant, stream)
+    return y
+
+
 def pp_splits(m: int, n: int, k: int, bn: int = 256, target_wgs: int = 256) -> int:
     """K slices for gemm_pp: about one workgroup per CU (tiles x slices <= target), >= 3 K-tiles
     (192) per slice."""

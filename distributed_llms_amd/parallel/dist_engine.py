@@ -141,10 +141,15 @@ def resolve_transport(kind: str, device: str, host_staged: bool) -> str:
     """The activation transport a stage uses: CPU stages and host-staged GPU stages always ride
     torch.distributed (gloo) -- or HIP IPC when asked for (stages sharing one GPU); on GPUs "auto"
     is the native RCCL edge transport."""
-    if not str(device).startswith("cuda"):
-        return "torch"
     kind = os.environ.get("DLLM_TRANSPORT", "") or kind or "auto"    # env: test / rehearsal override
+    if not str(device).startswith("cuda"):
+        # CPU stages ride gloo -- except the RCCL transport's stand-in rehearsal (rccl_standin.py)
+        from . import rccl_standin
+        return "rccl" if kind == "rccl" and rccl_standin.enabled() else "torch"
     if host_staged:                     # stages sharing one GPU: HIP IPC if asked, else gloo
+        from . import rccl_standin      # (or the RCCL transport over its stand-in: rehearsal)
+        if kind == "rccl" and rccl_standin.enabled():
+            return "rccl"
         return "ipc" if kind == "ipc" else "torch"
     return "rccl" if kind == "auto" else kind
 
@@ -158,12 +163,13 @@ def make_transport(ranks, stage: int, ctrl_group, data_group, device: str, ring_
     library or topology problem costs speed, not the run."""
     kind = resolve_transport(kind, device, data_group is not None)
     on_gpu = str(device).startswith("cuda")
+    from . import rccl_standin
     if kind == "ipc" and on_gpu:
         from .ipc_transport import IpcTransport
         rows, hidden, dtype, window = hop
         return IpcTransport(ranks, stage, ctrl_group, device, rows, hidden, dtype, ring_group=ring_group,
                             window=window)
-    if kind == "rccl" and on_gpu:
+    if kind == "rccl" and (on_gpu or rccl_standin.enabled()):
         from .rccl_transport import RcclTransport
         rows, hidden, dtype, window = hop
         t, err = None, None

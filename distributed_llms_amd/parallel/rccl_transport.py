@@ -32,6 +32,29 @@ from .. import _ext
 from .comm import DistTransport
 
 
+class _HostStream:
+    """CPU stage (stand-in communicators only): every transfer is synchronous, so the streams and
+    events of the GPU path become no-ops with the same interface."""
+    cuda_stream = 0
+
+    def wait_event(self, ev):
+        pass
+
+    def synchronize(self):
+        pass
+
+
+class _HostEvent:
+    def record(self, stream=None):
+        pass
+
+    def query(self):
+        return True
+
+    def synchronize(self):
+        pass
+
+
 class RcclTransport(DistTransport):
     kind = "rccl"
 
@@ -45,12 +68,13 @@ class RcclTransport(DistTransport):
         super().__init__(ranks, stage, ctrl_group=ctrl_group, data_group=None, ring_group=ring_group,
                          timeout_s=timeout_s)
         dev = torch.device(device)
-        if dev.type != "cuda":
-            raise ValueError("RcclTransport needs a GPU stage")
+        from . import rccl_standin
+        self.host = dev.type != "cuda"
+        if self.host and not rccl_standin.enabled():
+            raise ValueError("RcclTransport needs a GPU stage (CPU stages: the stand-in communicators only)")
         if window < 1:
             raise ValueError("in-flight window must be >= 1")
         self.device = dev
-        self.m = _ext.rccl()
         self.timeout_s = float(timeout_s)
         self.slots = window + 1
         self.slot_elems = int(max_rows) * int(hidden)
@@ -58,19 +82,31 @@ class RcclTransport(DistTransport):
         self.loopback = loopback
         self.comm_in = self.comm_out = self.ring_out = self.ring_in = None
         first, last = stage == 0, stage == len(self.ranks) - 1
-        di = dev.index or 0
+        di = -1 if self.host else (dev.index or 0)
         if loopback:
+            self.m = _ext.rccl()
             self.comm_out = self.comm_in = self.m.RcclComm(1, 0, self.m.unique_id(), di, self.timeout_s)
             self.ring_out = self.ring_in = self.comm_out
             self.next = self.prev = self.ranks[0]
         else:
-            # one unique id per communicator, made by its sender; every rank of the ctrl group
-            # takes part in the exchange (any dp x pp layout)
-            mine = {"edge": self.m.unique_id() if self.next is not None else b"",
-                    "ring": self.m.unique_id() if last and not first else b""}
+            # one unique id per communicator, made by its sender.  Every rank of the ctrl group
+            # takes part in the exchange (any dp x pp layout) UNCONDITIONALLY: a rank whose module
+            # or unique id failed contributes its error instead, so every rank sees the same table
+            # and raises before any communicator is built (the caller's fallback agreement then
+            # runs on all ranks; a rank that skipped the exchange would hang the others in it)
+            mine, err = {"edge": b"", "ring": b""}, ""
+            try:
+                self.m = _ext.rccl()
+                mine = {"edge": self.m.unique_id() if self.next is not None else b"",
+                        "ring": self.m.unique_id() if last and not first else b""}
+            except Exception as e:          # noqa: BLE001 - reported through the exchange
+                err = f"{type(e).__name__}: {e}"
             allv = [None] * dist.get_world_size(group=ctrl_group)
-            dist.all_gather_object(allv, (dist.get_rank(), mine), group=ctrl_group)
-            table = dict(allv)
+            dist.all_gather_object(allv, (dist.get_rank(), mine, err), group=ctrl_group)
+            bad = [(r, e) for r, _, e in allv if e]
+            if bad:
+                raise RuntimeError(f"native RCCL unavailable on rank(s) {bad}")
+            table = {r: m for r, m, _ in allv}
             # ascending edge order on every rank (in-edge first), the ring last: the chain of
             # inits cannot deadlock
             if self.prev is not None:
@@ -81,8 +117,8 @@ class RcclTransport(DistTransport):
                 self.ring_out = self.m.RcclComm(2, 0, mine["ring"], di, self.timeout_s)
             elif first and not last:
                 self.ring_in = self.m.RcclComm(2, 1, table[self.last]["ring"], di, self.timeout_s)
-        self.send_stream = torch.cuda.Stream(device=dev) if self.comm_out is not None else None
-        self.recv_stream = torch.cuda.Stream(device=dev) if self.comm_in is not None else None
+        self.send_stream = self._stream() if self.comm_out is not None else None
+        self.recv_stream = self._stream() if self.comm_in is not None else None
         if loopback:
             self.recv_stream = self.send_stream
         self.tx = torch.empty(self.slots, self.slot_elems, dtype=dtype, device=dev) if self.comm_out else None
@@ -96,7 +132,7 @@ class RcclTransport(DistTransport):
         # sampled-ids ring closure: int32 slots of max_ids, deeper than the in-flight window
         self.max_ids = int(max_ids or max_rows)
         self.id_slots = 2 * window + 2
-        self.ring_stream = torch.cuda.Stream(device=dev) if (self.ring_out or self.ring_in) else None
+        self.ring_stream = self._stream() if (self.ring_out or self.ring_in) else None
         self.ids_tx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_out else None
         self.ids_rx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_in else None
         self._ids_sent = [None] * self.id_slots
@@ -104,6 +140,16 @@ class RcclTransport(DistTransport):
         self._ids_tx_n = self._ids_rx_n = 0
         self._ids_deferred = []
         self._copy_stream = None
+
+    # streams / events of this stage's device (no-op shims on a CPU stage)
+    def _stream(self):
+        return _HostStream() if self.host else torch.cuda.Stream(device=self.device)
+
+    def _event(self):
+        return _HostEvent() if self.host else torch.cuda.Event()
+
+    def _cur(self):
+        return _HostStream() if self.host else torch.cuda.current_stream(self.device)
 
     @property
     def comm_ranks(self):
@@ -119,28 +165,28 @@ class RcclTransport(DistTransport):
         n = self._tx_n
         self._tx_n += 1
         slot = n % self.slots
-        cur = torch.cuda.current_stream(self.device)
+        cur = self._cur()
         if self._sent[slot] is not None:
             cur.wait_event(self._sent[slot])      # the slot's previous send has left
         dst = self.tx[slot, : t.numel()]
         dst.copy_(t.reshape(-1))
         nbytes = t.numel() * t.element_size()
-        ready = torch.cuda.Event()
+        ready = self._event()
         ready.record(cur)
         if self.loopback:
             self._deferred.append((slot, nbytes, ready))
             return
         self.send_stream.wait_event(ready)
         self.comm_out.send(dst.data_ptr(), nbytes, 1, self.send_stream.cuda_stream)
-        sent = torch.cuda.Event()
+        sent = self._event()
         sent.record(self.send_stream)
         self._sent[slot] = sent
 
     def recv_hidden(self, rows, hidden, dtype, device):
         self._check_hop(rows * hidden, dtype)
-        cur = torch.cuda.current_stream(self.device)
+        cur = self._cur()
         if self._last_rx is not None:             # everything enqueued so far consumed that slot
-            ev = torch.cuda.Event()
+            ev = self._event()
             ev.record(cur)
             self._consumed[self._last_rx] = ev
         n = self._rx_n
@@ -157,12 +203,12 @@ class RcclTransport(DistTransport):
                 raise RuntimeError(f"loopback hop size mismatch: sent {tbytes} B, receiving {nbytes} B")
             rs.wait_event(ready)
             self.comm_out.sendrecv(self.tx[tslot].data_ptr(), tbytes, 0, buf.data_ptr(), nbytes, 0, rs.cuda_stream)
-            sent = torch.cuda.Event()
+            sent = self._event()
             sent.record(rs)
             self._sent[tslot] = sent
         else:
             self.comm_in.recv(buf.data_ptr(), nbytes, 0, rs.cuda_stream)
-        landed = torch.cuda.Event()
+        landed = self._event()
         landed.record(rs)
         cur.wait_event(landed)
         self._last_rx = slot
@@ -176,19 +222,19 @@ class RcclTransport(DistTransport):
         n = self._ids_tx_n
         self._ids_tx_n += 1
         slot = n % self.id_slots
-        cur = torch.cuda.current_stream(self.device)
+        cur = self._cur()
         if self._ids_sent[slot] is not None:
             cur.wait_event(self._ids_sent[slot])
         dst = self.ids_tx[slot, :n_ids]
         dst.copy_(ids.reshape(-1))
-        ready = torch.cuda.Event()
+        ready = self._event()
         ready.record(cur)
         if self.loopback:
             self._ids_deferred.append((slot, n_ids, ready))
             return
         self.ring_stream.wait_event(ready)
         self.ring_out.send(dst.data_ptr(), n_ids * 4, 1, self.ring_stream.cuda_stream)
-        sent = torch.cuda.Event()
+        sent = self._event()
         sent.record(self.ring_stream)
         self._ids_sent[slot] = sent
 
@@ -196,14 +242,14 @@ class RcclTransport(DistTransport):
         from .comm import PendingIds
         if n_ids > self.max_ids:
             raise ValueError(f"{n_ids} sampled ids exceed the ring slot ({self.max_ids})")
-        cur = torch.cuda.current_stream(self.device)
+        cur = self._cur()
         n = self._ids_rx_n
         self._ids_rx_n += 1
         slot = n % self.id_slots
         rs = self.ring_stream
         # the slot's previous ids: consumed by device work enqueued before now (lookahead gathers)
         # and by their host copy
-        free = torch.cuda.Event()
+        free = self._event()
         free.record(cur)
         rs.wait_event(free)
         old = self._ids_users[slot]
@@ -217,16 +263,19 @@ class RcclTransport(DistTransport):
             rs.wait_event(ready)
             self.ring_out.sendrecv(self.ids_tx[tslot].data_ptr(), tn * 4, 0, buf.data_ptr(), n_ids * 4, 0,
                                    rs.cuda_stream)
-            sent = torch.cuda.Event()
+            sent = self._event()
             sent.record(rs)
             self._ids_sent[tslot] = sent
         else:
             self.ring_in.recv(buf.data_ptr(), n_ids * 4, 0, rs.cuda_stream)
-        landed = torch.cuda.Event()
+        landed = self._event()
         landed.record(rs)
-        if self._copy_stream is None:
-            self._copy_stream = torch.cuda.Stream(device=self.device)
-        p = PendingIds(buf, ready=landed, copy_stream=self._copy_stream, timeout_s=self.timeout_s)
+        if self.host:
+            p = PendingIds(buf, timeout_s=self.timeout_s)      # the stand-in recv already landed it
+        else:
+            if self._copy_stream is None:
+                self._copy_stream = torch.cuda.Stream(device=self.device)
+            p = PendingIds(buf, ready=landed, copy_stream=self._copy_stream, timeout_s=self.timeout_s)
         self._ids_users[slot] = p
         return p
 

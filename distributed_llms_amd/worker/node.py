@@ -590,7 +590,8 @@ class WorkerNode:
         self.stage_runner = None
         tp = getattr(self, "_transport", None)
         self._transport = None
-        if tp is not None and send_stop is False and hasattr(tp, "abort"):
+        own_comms = tp is not None and hasattr(tp, "abort") and getattr(tp, "kind", "") == "rccl"
+        if tp is not None and send_stop is False and own_comms:
             # membership changed (a peer died or the master re-planned): ncclCommAbort on the
             # communicators this stage owns (parallel/rccl_transport.py), so p2p still pending
             # against a dead peer returns instead of hanging
@@ -598,6 +599,18 @@ class WorkerNode:
                 tp.abort()
             except Exception as e:          # noqa: BLE001 - teardown continues regardless
                 log.warning("transport abort: %s", e)
+        if send_stop is False and not own_comms and self._dist_ctx is not None:
+            # every other transport (torch.distributed's groups, the job-wide fallback from the
+            # native one, HIP IPC's control plane) keeps its p2p on c10d groups: abort those, or a
+            # receive still pending against the dead peer makes destroy_process_group hang and the
+            # next LOAD_SHARD (recovery) never happens
+            try:
+                import torch.distributed as dist
+                from torch.distributed import distributed_c10d as c10d
+                if dist.is_initialized():
+                    c10d._abort_process_group()
+            except Exception as e:          # noqa: BLE001
+                log.warning("process group abort: %s", e)
         if self._dist_ctx is not None:
             # the control / default groups hold no pending p2p of the data plane any more;
             # destroy them (the next LOAD_SHARD re-initialises)

@@ -72,6 +72,20 @@ def test_single_process_bench_json_cpu():
     assert rec["ttft_p50_ms"] > 0 and rec["itl_p50_ms"] > 0 and rec["kernel_knobs"] == {}
 
 
+def test_open_loop_rate_mode_cpu():
+    """bench.py --rate: Poisson arrivals into the running engine; p50 request latency (ms, lower
+    is better) with p99 / TTFT / ITL and the offered vs achieved request rate."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--model",
+                        "tiny-llama", "--batch", "4", "--prompt-len", "5", "--gen-len", "4", "--rate", "40"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["higher_is_better"] is False and rec["unit"] == "ms" and rec["requests"] == 12
+    assert 0 < rec["p50_latency_ms"] <= rec["p99_latency_ms"] and rec["value"] == rec["p50_latency_ms"]
+    assert rec["ttft_p50_ms"] > 0 and rec["offered_rate_rps"] == 40 and rec["achieved_rate_rps"] > 0
+
+
 @pytest.mark.slow
 def test_torchrun_bench_hybrid_dp_pp_cpu():
     """world 4 = 2 pipelines x 2 stages: each pipeline owns its own scheduler, KV pool and

@@ -1,0 +1,90 @@
+"""gemm_rw (register-weight decode GEMM, csrc/kernels/gemm_rw.hip) vs a plain fp32 PyTorch GEMM of
+the same operands: plain / split-K / deferred slabs / fused SwiGLU, every ring depth, M tails."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_llms_amd import ops
+from distributed_llms_amd.ops import gemm
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(*s, scale=1.0):
+    return (torch.randn(*s, device="cuda") * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("m", [1, 31, 100, 255, 256])
+@pytest.mark.parametrize("n,k,splits", [(6144, 4096, 1), (6144, 4096, 5), (4096, 14336, 8), (4096, 4096, 8),
+                                        (1024, 512, 1), (256, 64, 1), (384, 192, 2)])
+@pytest.mark.parametrize("ns", [3, 4, 5])
+def test_rw_linear(cuda, m, n, k, splits, ns):
+    torch.manual_seed(m * 7 + n + k + ns)
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear_rw(x, w, splits=splits, variant=ns)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [1, 77, 256])
+@pytest.mark.parametrize("inter,k,splits", [(14336, 4096, 1), (1024, 512, 1), (1024, 1024, 2), (64, 64, 1)])
+@pytest.mark.parametrize("ns", [3, 4, 5])
+def test_rw_swiglu(cuda, m, inter, k, splits, ns):
+    torch.manual_seed(m + inter + k + ns)
+    x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
+    y = gemm.linear_rw(x, w, splits=splits, swiglu=True, variant=ns)
+    gu = x.float() @ w.float().t()
+    ref = F.silu(gu[:, :inter]) * gu[:, inter:]
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("variant", [4, 16 | 4])
+def test_rw_cache_policy_bit_exact(cuda, variant):
+    """The nontemporal and default-policy weight loads produce identical results."""
+    x, w = _bf(256, 4096), _bf(6144, 4096, scale=0.05)
+    a = gemm.linear_rw(x, w, splits=5, variant=4)
+    b = gemm.linear_rw(x, w, splits=5, variant=variant)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 4096, 14336), (200, 4096, 4096), (64, 1024, 8192)])
+def test_rw_deferred_splitk_fused_add_rms_norm(cuda, m, n, k):
+    """Deferred split-K slabs reduced inside the next add + RMSNorm equal reduce-then-norm."""
+    from distributed_llms_amd.ops import reference as ref
+    torch.manual_seed(1)
+    x = (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16)
+    w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(n, device="cuda")).to(torch.bfloat16)
+    res0 = torch.randn(m, n, device="cuda").to(torch.bfloat16)
+    p = gemm.linear_rw(x, w, defer=True)
+    assert isinstance(p, gemm.SplitKPartial) and p.splits > 1
+    r1 = res0.clone()
+    y1, _ = ops.fused_add_rms_norm(p, r1, g, 1e-5)
+    h = gemm.linear_rw(x, w, defer=True).materialize()
+    r2 = res0.clone()
+    y2, _ = ops.fused_add_rms_norm(h, r2, g, 1e-5)
+    assert torch.equal(y1, y2) and torch.equal(r1, r2)
+    torch.testing.assert_close(h.float(), ref.linear(x.float(), w.float()), atol=2e-2, rtol=2e-2)
+
+
+def test_rw_graph_replay(cuda):
+    x, w = _bf(256, 4096), _bf(28672, 4096, scale=0.05)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gemm.linear_rw(x, w, swiglu=True)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        y = gemm.linear_rw(x, w, swiglu=True)
+    for _ in range(3):
+        x.copy_(_bf(256, 4096))
+        g.replay()
+        gu = x.float() @ w.float().t()
+        torch.testing.assert_close(y.float(), F.silu(gu[:, :14336]) * gu[:, 14336:], atol=3e-2, rtol=3e-2)
+
+
+def test_rw_rejects_bad_shapes(cuda):
+    with pytest.raises(ValueError):
+        gemm.linear_rw(_bf(257, 256), _bf(256, 256))
+    with pytest.raises(ValueError):
+        gemm.linear_rw(_bf(8, 256), _bf(200, 256))

@@ -97,19 +97,34 @@ def test_worker_failure_eviction_and_recovery(cluster):
     m.assign_shards()
     m.distribute_shards(timeout=300)
     futs = [m.submit(p, {"max_new_tokens": 40, "ignore_eos": True}) for p in PROMPTS]
+    streamed = {}
+
+    def consume(key, prompt):      # stream() submits on its first iteration, in this thread
+        streamed[key] = list(m.stream(prompt, max_new_tokens=40, ignore_eos=True, timeout=240))
+    import threading
+    th_inflight = threading.Thread(target=consume, args=("inflight", PROMPTS[0]))
+    th_inflight.start()            # in flight when the stage dies: parked, re-run, resumed
     t0 = time.time()
     while m.state != "degraded" and time.time() - t0 < 30:
         time.sleep(0.2)
     assert m.state == "degraded"
     assert m.running                                    # the master survives
     assert not any(f.done() for f in futs)              # parked, not failed
-    with pytest.raises(WorkerFailure):
-        m.submit(PROMPTS[0], {"max_new_tokens": 2})     # new work is refused while degraded
+    late = m.submit(PROMPTS[1], {"max_new_tokens": 40, "ignore_eos": True})   # held while degraded
+    th_late = threading.Thread(target=consume, args=("late", PROMPTS[2]))
+    th_late.start()
+    time.sleep(0.5)
+    assert not late.done() and m.state == "degraded"
     procs.append(_spawn_worker(m.port))                 # a replacement worker joins
     res = [m._finish(f, 180) for f in futs]
     assert m.state == "ready"
     ref = LLMEngine(_cfg("synthetic:tiny-llama")).generate(PROMPTS, SamplingParams(max_new_tokens=40, ignore_eos=True))
     assert [r["tokens"] for r in res] == ref
+    assert m._finish(late, 180)["tokens"] == ref[1]     # the held request ran after recovery
+    th_inflight.join(240)
+    th_late.join(240)
+    assert sum(streamed["inflight"], []) == ref[0]      # greedy stream resumed exactly
+    assert sum(streamed["late"], []) == ref[2]          # a held stream too
     res = m.generate(PROMPTS[:2], max_new_tokens=4, ignore_eos=True, timeout=120)
     assert [r["tokens"] for r in res] == [r[:4] for r in ref[:2]]
 

@@ -35,6 +35,10 @@ def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fi
     # does, so a different plan can flip a near-tie greedy token of this random-init model;
     # sub-layer plans are checked by agreement below
     os.environ["DLLM_PP_FINE"] = fine
+    standin = transport == "rccl-standin"
+    if standin:             # RcclTransport's multi-rank path over the stand-in communicators
+        transport = "rccl"
+        os.environ["DLLM_RCCL_STANDIN"] = "1"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), DLLM_SHARE_GPU="1", DLLM_DATA_BACKEND="gloo", DLLM_TRANSPORT=transport)
     import torch.distributed as dist
@@ -45,6 +49,10 @@ def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fi
     if transport == "ipc":
         from distributed_llms_amd.parallel.ipc_transport import IpcTransport
         assert isinstance(role.transport, IpcTransport)
+    if standin:
+        from distributed_llms_amd.parallel.rccl_transport import RcclTransport
+        assert isinstance(role.transport, RcclTransport) and role.transport.comm_ranks
+        assert not role.transport.host
     p = SamplingParams(max_new_tokens=12, ignore_eos=True)
     outs = []
     for _ in range(rounds):        # several rounds: the IPC sequence numbers carry across them
@@ -115,6 +123,19 @@ def test_multiprocess_gpu_pipeline_ipc(cuda, world):
     ref = LLMEngine(_mp_ecfg(1)).generate(prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
     res = _run_ranks(world, prompts, "ipc", rounds=3)
     assert res[0] == [ref, ref, ref]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_multiprocess_gpu_pipeline_rccl_transport_standin(cuda, world):
+    """RcclTransport's multi-rank path on the GPU (stage processes sharing the one device): the
+    unique-id exchange, edge / ring communicator init, the send / recv / ring HIP streams with
+    their slot events and the device-side ids ring, over the stand-in communicators
+    (parallel/rccl_standin.py; RCCL itself refuses two ranks on one device).  Two rounds reproduce
+    the single-process engine token for token."""
+    prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
+    ref = LLMEngine(_mp_ecfg(1)).generate(prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
+    res = _run_ranks(world, prompts, "rccl-standin", rounds=2)
+    assert res[0] == [ref, ref]
 
 
 @pytest.mark.parametrize("units,exact", [("5:0,8;8,11;11,20", True), ("5:0,7;7,12;12,20", True),
