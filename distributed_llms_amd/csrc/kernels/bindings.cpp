@@ -30,9 +30,8 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("splitk_add_rms_norm_q8", &dllm::splitk_add_rms_norm_q8);
   m.def("gemm_sq", &dllm::gemm_sq);
   m.def("gemm_rw", &dllm::gemm_rw);
+  m.def("gemm_pp_moe", &dllm::gemm_pp_moe);
   m.def("gemm_pp", &dllm::gemm_pp);
-  m.def("gemm_gate_up", &dllm::gemm_gate_up);
-  m.def("gemm_band", &dllm::gemm_band);
   m.def("moe_combine", &dllm::moe_combine);
   m.def("moe_wide_gemm", &dllm::moe_wide_gemm);
   m.def("moe_router_route", &dllm::moe_router_route);

@@ -150,7 +150,9 @@ __device__ __forceinline__ int pp_b_row(int r, int n_t, int half) {
 template <int BN, int MODE, int VAR>
 __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                          bf16* __restrict__ C, float* __restrict__ P, int M, int N,
-                                                         int K, int ks_per_split, int nsplit, float* __restrict__ D) {
+                                                         int K, int ks_per_split, int nsplit, float* __restrict__ D,
+                                                         const int* __restrict__ gather, const int* __restrict__ counts,
+                                                         const int* __restrict__ offsets, int E) {
   constexpr int NW = 4, NWN = 2;
   constexpr int BM = 256, TM = 128, TN = BN / NWN;     // waves as 2 (M) x NWN (N)
   constexpr int RT = TM / 16, CT = TN / 16;            // 16 x 16 fragments per wave: 8 x 8 or 8 x 4
@@ -183,8 +185,12 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv / NWN, wn = wv % NWN;
-  const int mtiles = (M + BM - 1) / BM;
+  // MOE (VAR 128): grouped expert GEMM -- the row tiles of every expert's segment of the
+  // expert-sorted slot space, counts / offsets read on the device (no host sync); the grid holds an
+  // upper bound of row tiles (slots / 256 + E), the surplus workgroups exit at once
+  constexpr bool MOE = (VAR & 128) != 0;
   const int ntiles = N / BN;
+  const int mtiles = MOE ? (int)(gridDim.x / ntiles) : (M + BM - 1) / BM;
   const int total = gridDim.x;
   int b = blockIdx.x;
   {   // bijective XCD remap: consecutive logical blocks share an XCD
@@ -204,6 +210,25 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
     n_t = rest / nsplit;
   }
   const int m0 = m_t * BM;
+  // the tile's rows: [r0, min(r0 + BM, rcnt)) of the row range that starts at slot roff (dense:
+  // roff 0, rows m0 .. M); MOE: expert ex's segment, its weight We = B + ex N K
+  int r0 = m0, rcnt = M, roff = 0;
+  const bf16* We = B;
+  if constexpr (MOE) {
+    int base = 0, ex = -1;
+    for (int x = 0; x < E; ++x) {
+      const int c = counts[x], nx = (c + BM - 1) / BM;
+      if (ex < 0 && m_t < base + nx) {
+        ex = x;
+        r0 = (m_t - base) * BM;
+        rcnt = c;
+      }
+      base += nx;
+    }
+    if (ex < 0) return;                                // past the last real row tile (uniform)
+    roff = offsets[ex];
+    We = B + (size_t)ex * N * K;
+  }
   const int ks0 = split * ks_per_split;
   const int nt = max(0, min(K / PBK, ks0 + ks_per_split) - ks0);
 
@@ -213,7 +238,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   // per A piece (rows past M clamp to M - 1) and ONE for every B piece -- a B piece's row is a
   // uniform function of the piece index plus lane / 8, also for the SwiGLU row interleave
   const char* Ab = reinterpret_cast<const char*>(A) + (size_t)ks0 * PBK * 2;
-  const char* Bb = reinterpret_cast<const char*>(B) + (size_t)ks0 * PBK * 2;
+  const char* Bb = reinterpret_cast<const char*>(We) + (size_t)ks0 * PBK * 2;
   // the swizzle of row 8 q + lane / 8 depends on q's parity: ((8 q + x) >> 1) & 7 = (4 q + x / 2) & 7
   uint32_t chunk_q[2];
 #pragma unroll
@@ -222,7 +247,14 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
 #pragma unroll
   for (int j = 0; j < GA; ++j) {
     const int q = wv * GA + j, r = 8 * q + (lane >> 3);
-    offA[j] = (uint32_t)min(m0 + r, M - 1) * (uint32_t)(K * 2) + chunk_q[q & 1];
+    int srow;
+    if constexpr (MOE) {
+      const int slot = roff + min(r0 + r, rcnt - 1);
+      srow = gather ? gather[slot] : slot;
+    } else {
+      srow = min(m0 + r, M - 1);
+    }
+    offA[j] = (uint32_t)srow * (uint32_t)(K * 2) + chunk_q[q & 1];
   }
   uint32_t offB[2];
 #pragma unroll
@@ -548,16 +580,16 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
   __syncthreads();
   constexpr int CPR = OUTW / 8;                        // 16-byte chunks per output row
   constexpr int RPI = 64 * NW / CPR;                   // rows per pass
-  const int ch = tid % CPR, r0 = tid / CPR;
+  const int ch = tid % CPR, rs0 = tid / CPR;
   const int ldc = SWIGLU ? N / 2 : N;
   const int col0 = n_t * OUTW + ch * 8;
   // SWI2: output columns 8 ch .. 8 ch + 7 sit in 16-column group ch / 2 -> gate at image column
   // 32 (ch / 2) + 8 (ch % 2), up 16 further
   const int icol = SWI2 ? 32 * (ch >> 1) + 8 * (ch & 1) : ch * 8;
 #pragma unroll 4
-  for (int r = r0; r < BM; r += RPI) {
-    const int m = m0 + r;
-    if (m >= M) break;
+  for (int r = rs0; r < BM; r += RPI) {
+    if (r0 + r >= rcnt) break;
+    const int m = roff + r0 + r;
     int4 v = *reinterpret_cast<const int4*>(smem + r * OPITCH + icol);
     if constexpr (SWI2) {
       const bf16x8 g = *reinterpret_cast<const bf16x8*>(&v);
@@ -611,7 +643,8 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
   const bool grp = (variant & 4) != 0 && S == 1 && mtiles > 1;
 #define DLLM_PP_GO(BN_, MODE_, VAR_)                                                                     \
   hipLaunchKernelGGL((gemm_pp_kernel<BN_, MODE_, VAR_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, \
-                     (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kps, S, dbg)
+                     (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kps, S, dbg, (const int*)nullptr,       \
+                     (const int*)nullptr, (const int*)nullptr, 0)
   // variant bit 6: schedule 2 (the K-tile's fragments read early, staging spread; weights
   // nontemporal with bit 1 only in the natural tile order).  Bit 3: diagnostic build -- per-wave cycle stamps (loop, B_t waits) into the LAST
   // grid x 512 floats of ws (after the slabs); output as usual.  With it (schedule 1 only), bit 4:
@@ -656,6 +689,33 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
   if (mode == 2) return S;
   splitk_reduce_ex(c, ws, 0, S, M, N, swiglu ? 1 : 0, stream);
   return S;
+}
+
+// Grouped expert GEMM over the expert-sorted slot space (MoE prefill): expert e owns
+// slots [offsets[e], offsets[e] + counts[e]) (device arrays, never read on the host); its rows are
+// x[gather[slot]] (gather null: x[slot]) and its weight W[e] ([N, K]; SwiGLU: [2I, K] = [Wg; Wu]).
+// y [slots, N] (SwiGLU: [slots, N / 2]).  Schedule 2, 256 x 256 tiles, grouped row-tile order.
+// xrows: rows of x (buffer range), slots: total slot count (grid bound: slots / 256 + E row tiles).
+void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets, int E,
+                 int N, int K, int xrows, int slots, int mode, uintptr_t stream) {
+  DLLM_HOST_CHECK(E >= 1 && E <= 256, "1 <= experts <= 256");
+  DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
+  DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
+  DLLM_HOST_CHECK(xrows >= 1 && slots >= 1, "rows");
+  DLLM_HOST_CHECK((long)xrows * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32), "operands must be < 4 GiB");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const long grid = (long)(N / 256) * ((slots + 255) / 256 + E);
+  DLLM_HOST_CHECK(grid < (1L << 31), "grid");
+  if (mode == 1)
+    hipLaunchKernelGGL((gemm_pp_kernel<256, 2, 128 | 32 | 2>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)x,
+                       (const bf16*)w, (bf16*)y, (float*)nullptr, xrows, N, K, K / PBK, 1, (float*)nullptr,
+                       (const int*)gather, (const int*)counts, (const int*)offsets, E);
+  else
+    hipLaunchKernelGGL((gemm_pp_kernel<256, 0, 128 | 32 | 2>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)x,
+                       (const bf16*)w, (bf16*)y, (float*)nullptr, xrows, N, K, K / PBK, 1, (float*)nullptr,
+                       (const int*)gather, (const int*)counts, (const int*)offsets, E);
+  DLLM_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace dllm

@@ -211,17 +211,17 @@ __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict_
   };
   auto no_vm = [](auto) {};
 
-  // ---- prologue: K-tiles 0 .. NS-2 (each: its 4 weight fragments, then its 8 LDS-DMA pieces)
-  const int pro = nt < NS - 1 ? nt : NS - 1;
+  // ---- prologue: K-tiles 0 .. NS-2 (each: its 4 weight fragments, then its 8 LDS-DMA pieces).
+  // Straight-line: a K-tile past the slice (nt < NS - 1, tiny K only) is a dummy copy of K-tile
+  // nt - 1 into a buffer / slot nothing reads -- it only makes the waits below more conservative
   rw_for<NS - 1>([&](auto p) {
-    if (p.value < pro) {
+    const int tp = min((int)p.value, nt - 1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) load_w(wreg[p.value][j], p.value, j);
+    for (int j = 0; j < 4; ++j) load_w(wreg[p.value][j], tp, j);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) piece(p.value, p.value, q);
-    }
+    for (int q = 0; q < 8; ++q) piece(p.value, tp, q);
   });
-  rw_wait_tiles<NS - 2>(pro - 1, wreg[0]);
+  rw_wait_tiles<NS - 2>(NS - 2, wreg[0]);
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   rw_for<4>([&](auto g) { reads2(fs0, lds0 + foff[0], g); });   // K-tile 0, k-step 0

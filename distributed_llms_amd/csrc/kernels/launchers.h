@@ -34,9 +34,8 @@ int gemm_wide_fp8(uintptr_t c, uintptr_t a, uintptr_t a_scale, uintptr_t b, uint
 void quant_fp8_rows(uintptr_t q, uintptr_t scale, uintptr_t x, int M, int K, uintptr_t stream);
 int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream);
-int gemm_band(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
-              int mode, int ct, uintptr_t stream);
-void gemm_gate_up(uintptr_t c, uintptr_t a, uintptr_t w, int M, int I, int K, int variant, uintptr_t stream);
+void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets, int E,
+                 int N, int K, int xrows, int slots, int mode, uintptr_t stream);
 int gemm_rw(uintptr_t c, uintptr_t a, uintptr_t w, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream);
 int gemm_sq(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,

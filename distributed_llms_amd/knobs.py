@@ -41,12 +41,6 @@ class Knobs:
     wide_target_wgs: int = 256        # split-K: about one workgroup per CU
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
-    # decode MLP gate|up on gemm_gu.hip (56-output tiles: I / 56 workgroups, every CU busy at
-    # I = 14336) for gu_min_m <= M <= 256 when I / 56 <= gu_max_wgs; 0 = off.  Measured 0.93-1.03x
-    # of gemm_wide across boxes (profiles/round3_gu_experiments.md): off
-    gu_min_m: int = 0
-    gu_max_wgs: int = 256
-    gu_variant: int = 0               # 1: activations straight into registers (gemm_gua_kernel)
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
     # from this M up to 256, unsplit grids only unless sq_split
     sq: str = "all"

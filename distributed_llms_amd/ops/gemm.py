@@ -10,8 +10,6 @@ the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..
     M <= knobs.wide_down_max_m (512);
   - the other projections (qkv, o, LM head): M <= knobs.wide_proj_max_m (256);
   with the 256 x 256 tile (gemm_sq.hip) taking unsplit grids at 225 <= M <= 256 (70B gate|up);
-* opt-in (knobs.gu_min_m, off by default: 0.93-1.03x of gemm_wide): the decode MLP gate|up on
-  gemm_gu.hip, 56-output tiles so that I / 56 workgroups (256 at I = 14336) keep every CU busy;
 * the decode LM head at 225 <= M <= 256: gemm_pp.hip schedule 2 with nontemporal weights
   (knobs.pp_head_min_m);
 * prefill gate|up (M >= knobs.pp_swiglu_min_m): gemm_pp.hip, the 4-wave 256 x 256-tile kernel
@@ -313,76 +311,11 @@ def linear_sq(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = 
     return y
 
 
-def use_gate_up56(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor) -> bool:
-    """Decode gate|up on gemm_gu.hip (knobs.gu_min_m / gu_max_wgs)."""
-    kn = knobs.K
-    inter = n // 2
-    return (0 < kn.gu_min_m <= m <= 256 and n % 2 == 0 and inter % 56 == 0 and inter // 56 <= kn.gu_max_wgs
-            and k % 64 == 0 and x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous())
-
-
-def linear_gate_up56(x: torch.Tensor, w_gate_up: torch.Tensor, variant: int = -1) -> torch.Tensor:
-    """silu(x Wg^T) * (x Wu^T) on gemm_gu.hip: 256-row x 56-output tiles (M <= 256, I % 56 == 0).
-    ``variant`` 1: activations straight into registers (gemm_gua_kernel); -1 = knobs.gu_variant."""
-    k = x.shape[-1]
-    n = w_gate_up.shape[0]
-    m = x.numel() // k
-    if not (1 <= m <= 256 and n % 112 == 0 and k % 64 == 0 and x.dtype == w_gate_up.dtype == torch.bfloat16
-            and x.is_contiguous() and w_gate_up.is_contiguous()):
-        raise ValueError(f"linear_gate_up56: M {m} <= 256, 2I {n} % 112, K {k} % 64, bf16 contiguous")
-    y = torch.empty(*x.shape[:-1], n // 2, dtype=x.dtype, device=x.device)
-    v = knobs.K.gu_variant if variant < 0 else variant
-    if k < 192:
-        v = 0                       # the register-A form runs >= 3 K-tiles
-    _ext.kernels().gemm_gate_up(y.data_ptr(), x.data_ptr(), w_gate_up.data_ptr(), m, n // 2, k, v,
-                                torch.cuda.current_stream().cuda_stream)
-    return y
-
-
-def band_splits(m: int, n: int, k: int, ct: int, target_wgs: int = 256) -> int:
-    """K slices for gemm_band: about one workgroup per CU, >= 4 K-tiles (256) per slice."""
-    tiles = n // (16 * ct)
-    return max(1, min(round(target_wgs / max(1, tiles)), (k // 64) // 4, 16))
-
-
-def linear_band(x: torch.Tensor, w: torch.Tensor, splits: int = 0, ct: int = 8, defer: bool = False,
-                areg: bool = False):
-    """y = x w^T on gemm_gu.hip's band kernel (256 rows x 16 ct columns per workgroup, 8 waves of
-    32-row bands, M <= 256; ``areg``: activations straight into registers, gemm_gua_kernel).  Split-K partials are reduced by splitk_reduce, or returned as a
-    :class:`SplitKPartial` with ``defer``."""
-    k = x.shape[-1]
-    n = w.shape[0]
-    m = x.numel() // k
-    if not (1 <= m <= 256 and n % (16 * ct) == 0 and k % 64 == 0 and x.dtype == w.dtype == torch.bfloat16
-            and x.is_contiguous() and w.is_contiguous()):
-        raise ValueError(f"linear_band: M {m} <= 256, N {n} % {16 * ct}, K {k} % 64, bf16 contiguous")
-    s = splits or band_splits(m, n, k, ct)
-    ws = _workspace(x.device)
-    if s > 1 and s * m * n > ws.numel():
-        s = max(1, ws.numel() // (m * n))
-    stream = torch.cuda.current_stream().cuda_stream
-    kern = _ext.kernels()
-    kt = k // 64
-    kts = -(-kt // s)
-    if kts < 3 or kt - (-(-kt // kts) - 1) * kts < 3:
-        areg = False                # the register-A form runs >= 3 K-tiles per split
-    if s == 1:
-        y = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
-        kern.gemm_band(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, 0, m, n, k, 1, 0, ct | (256 if areg else 0), stream)
-        return y
-    se = kern.gemm_band(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2,
-                        ct | (256 if areg else 0), stream)
-    part = SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
-    return part if defer else part.materialize()
-
-
 def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Tensor]:
     """silu(x Wg^T) * (x Wu^T) with W = [Wg; Wu] in one launch; None if the shape is not eligible."""
     k = x.shape[-1]
     n = w_gate_up.shape[0]
     m = x.numel() // k
-    if use_gate_up56(m, n, k, x, w_gate_up):
-        return linear_gate_up56(x, w_gate_up)
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
     if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):

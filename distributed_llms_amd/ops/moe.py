@@ -5,9 +5,10 @@ GPU path (bf16):
   moe_route      : softmax -> top-k -> renormalise, expert-sorted slots    (HIP, one launch)
   decode-sized T : grouped weight-streaming GEMMs on the sorted slots (gate|up + SwiGLU, then down)
                    entirely on device -- no host sync, so the decode step stays graph-capturable
-  prefill-sized T: per-expert GEMMs over the gathered rows (needs the counts on the host): gate|up
-                   through ops.linear_swiglu (gemm_pp + fused SwiGLU at prefill row counts), down
-                   on hipBLASLt
+  prefill-sized T: grouped 256 x 256-tile GEMMs over the expert-sorted slots (gemm_pp.hip
+                   gemm_pp_moe: one launch per projection, every expert's row tiles in one grid,
+                   counts / offsets read on the device -- no host sync, no per-expert loop; gate|up
+                   with the SwiGLU in its epilogue, the token gather in its A staging)
   moe_combine    : weighted sum of each token's top-k expert outputs        (HIP)
 CPU path: the PyTorch reference (ops/reference.py).
 """
@@ -73,9 +74,10 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
     offsets = torch.empty(e + 1, dtype=torch.int32, device=dev)
     sorted_tok = torch.empty(t * top_k, dtype=torch.int32, device=dev)
     inv = torch.empty(t * top_k, dtype=torch.int32, device=dev)
-    if knobs.K.moe_fused_router and t <= GROUPED_MAX_TOKENS and e in (8, 16) and h % 32 == 0 and x.dtype == w_router.dtype == torch.bfloat16 \
+    if knobs.K.moe_fused_router and e in (8, 16) and h % 32 == 0 and x.dtype == w_router.dtype == torch.bfloat16 \
             and w_router.is_contiguous():
-        # decode: router GEMV + softmax/top-k + scatter in two launches (no [T, E] logits round trip)
+        # router GEMV + softmax/top-k + scatter in two launches (no [T, E] logits round trip), at
+        # decode and prefill T alike
         k.moe_router_route(x.data_ptr(), w_router.data_ptr(), t, h, e, top_k, topk_w.data_ptr(), topk_ids.data_ptr(),
                            counts.data_ptr(), offsets.data_ptr(), sorted_tok.data_ptr(), inv.data_ptr(), st)
     else:
@@ -122,13 +124,21 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
                                cnt_p, off_p, e_loc, two_i, h, 1, rows, knobs.K.moe_variant, st)
             k.moe_grouped_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, 0,
                                rows, knobs.K.moe_variant, st)
+    elif x.dtype == torch.bfloat16 and two_i % 256 == 0 and h % 256 == 0 and inter % 64 == 0 and h % 64 == 0:
+        # prefill: one grouped launch per projection over every local expert's row tiles
+        slots = t * top_k
+        act = torch.empty(slots, inter, dtype=x.dtype, device=dev)
+        k.gemm_pp_moe(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p, e_loc,
+                      two_i, h, t, slots, 1, st)
+        k.gemm_pp_moe(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, slots,
+                      slots, 0, st)
     else:
+        # odd expert dims (test-size models): per-expert GEMMs, counts read on the host
         xs = x.index_select(0, sorted_tok.long())
-        off = offsets.cpu().tolist()          # prefill only: eager, host sync is fine here
+        off = offsets.cpu().tolist()
         for j in range(e_loc):
             a, b = off[expert_offset + j], off[expert_offset + j + 1]
             if b > a:
-                # gate|up with the SwiGLU in the GEMM epilogue (gemm_pp at >= 2048 rows per expert)
                 ys[a:b] = F.linear(linear_swiglu(xs[a:b], w_gate_up[j]), w_down[j])
     out = torch.empty_like(x)
     k.moe_combine(out.data_ptr(), ys.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), t, h, top_k, st)

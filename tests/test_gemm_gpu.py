@@ -126,59 +126,6 @@ def test_wide_swiglu(cuda, m, inter, k, splits, variant):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("m", [1, 7, 64, 193, 200, 256])
-@pytest.mark.parametrize("inter,k", [(14336, 4096), (56, 64), (112, 128), (448, 1024), (1120, 320)])
-@pytest.mark.parametrize("variant", [0, 1])
-def test_gate_up56(cuda, m, inter, k, variant):
-    """gemm_gu.hip (56-output tiles, gate/up paired across lanes l, l ^ 8) vs fp32: row tails, one
-    K-tile, K shorter than the ring, I = 56 (one workgroup) to 14336 (256); variant 1 = A in VGPRs."""
-    x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
-    y = gemm.linear_gate_up56(x, w, variant=variant)
-    gu = x.float() @ w.float().t()
-    ref = F.silu(gu[:, :inter]) * gu[:, inter:]
-    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
-
-
-@pytest.mark.parametrize("m", [1, 37, 200, 256])
-@pytest.mark.parametrize("n,k,ct,splits", [(4096, 4096, 8, 8), (6144, 4096, 6, 4), (6144, 4096, 8, 5),
-                                           (4096, 14336, 8, 8), (896, 512, 7, 1), (768, 320, 6, 2)])
-@pytest.mark.parametrize("areg", [False, True])
-def test_band_linear(cuda, m, n, k, ct, splits, areg):
-    """gemm_gu.hip band kernel, plain and split-K (slabs reduced by splitk_reduce), vs fp32."""
-    x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    y = gemm.linear_band(x, w, splits=splits, ct=ct, areg=areg)
-    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
-
-
-def test_band_deferred_matches_wide_slab_layout(cuda):
-    """The band kernel's split-K slabs use gemm_wide's layout: a deferred partial feeds the fused
-    add + RMSNorm exactly like gemm_wide's (same K slicing -> same sums up to MFMA order)."""
-    m, n, k = 256, 4096, 4096
-    x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    p = gemm.linear_band(x, w, splits=8, ct=8, defer=True)
-    assert isinstance(p, gemm.SplitKPartial) and p.splits == 8
-    y = p.materialize()
-    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
-
-
-def test_gate_up56_dispatch_and_graph(cuda, monkeypatch):
-    """With knobs.gu_min_m set, the engine's swiglu entry takes gemm_gu at M = 256 (Llama-3-8B dims)
-    and replays in a graph."""
-    from distributed_llms_amd import knobs
-    monkeypatch.setattr(knobs.K, "gu_min_m", 193)
-    x, w = _bf(256, 4096), _bf(2 * 14336, 4096, scale=0.05)
-    assert gemm.use_gate_up56(256, 2 * 14336, 4096, x, w)
-    y0 = gemm.linear_swiglu(x, w)
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
-        y = gemm.linear_swiglu(x, w)
-    g.replay()
-    torch.cuda.synchronize()
-    assert torch.equal(y, y0)
-
-
 @pytest.mark.parametrize("m", [1, 37, 128, 200, 256, 300])
 @pytest.mark.parametrize("n,k,splits,swiglu", [(6144, 4096, 5, False), (4096, 14336, 8, False),
                                                (1024, 512, 1, False), (2048, 512, 1, True)])

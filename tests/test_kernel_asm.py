@@ -1,11 +1,13 @@
 """Static checks of the compiled gfx950 code (CPU: hipcc cross-compiles, nothing runs).
 
-gemm_gu.hip's register-A kernels load activations with inline-asm global loads whose destination
-registers hipcc believes written at issue; a first build let the allocator reuse such registers as
-address registers before the data landed (a GPU memory fault).  This test compiles the file to
-assembly and runs scripts/check_async_loads.py over every gemm_gua_kernel instantiation: no
-non-MFMA instruction may touch a VGPR with an asm load still in flight, and the K loop keeps its
-counted waits (no compiler-inserted vmcnt(0) before the tail)."""
+gemm_rw.hip loads its weight fragments with inline-asm buffer loads straight into VGPRs: hipcc
+believes the destination written at issue, so any instruction that touches such a register before
+the covering ``s_waitcnt vmcnt`` -- a compiler-inserted copy, an address computation, an MFMA --
+reads bytes that have not landed (wrong results, or a fault if the value feeds an address).  The
+test compiles the file to assembly and runs scripts/check_async_loads.py over every gemm_rw
+instantiation: no instruction may touch a VGPR with an asm load still in flight, the waits are
+counted (the K loop never drains with vmcnt(0); only the epilogue does), and the main loop holds
+no register copies (v_mov / v_accvgpr_mov: the window structure keeps every value in place)."""
 import os
 import re
 import shutil
@@ -19,17 +21,43 @@ ROOT = Path(__file__).resolve().parent.parent
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
-@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_gua_kernels_have_no_async_load_hazards(tmp_path):
-    src = ROOT / "distributed_llms_amd" / "csrc" / "kernels" / "gemm_gu.hip"
-    out = tmp_path / "gu.s"
+@pytest.fixture(scope="module")
+def rw_asm(tmp_path_factory):
+    src = ROOT / "distributed_llms_amd" / "csrc" / "kernels" / "gemm_rw.hip"
+    out = tmp_path_factory.mktemp("asm") / "rw.s"
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "--offload-device-only", "-S",
-                    str(src), f"-I{src.parent}", "-o", str(out)], check=True, capture_output=True, timeout=600)
-    res = subprocess.run([sys.executable, str(ROOT / "scripts" / "check_async_loads.py"), str(out)],
+                    str(src), f"-I{src.parent}", "-o", str(out)], check=True, capture_output=True, timeout=900)
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_rw_kernels_have_no_async_load_hazards(rw_asm):
+    res = subprocess.run([sys.executable, str(ROOT / "scripts" / "check_async_loads.py"), str(rw_asm)],
                          check=True, capture_output=True, text=True).stdout
     lines = [l for l in res.splitlines() if "hazards" in l]
-    assert len(lines) >= 7, res                      # 3 plain + 3 slab + 1 SwiGLU instantiations
+    assert len(lines) == 24, res                 # 3 ring depths x 4 modes x 2 cache policies
     for l in lines:
-        assert re.search(r"hazards 0 ", l), l
+        assert re.search(r"hazards 0 ", l), res
         waits = [int(x) for x in re.findall(r"\d+", l.split("vmcnt", 1)[1])]
-        assert waits[0] > 0 and 0 not in waits[:-1], l   # counted waits; vmcnt(0) only at the end
+        assert waits[-1] == 0 and any(w > 0 for w in waits), l
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_rw_main_loop_has_no_register_copies(rw_asm):
+    s = rw_asm.read_text()
+    names = re.findall(r"^(_ZN4dllm14gemm_rw_kernel\w+):", s, re.M)
+    assert names
+    for name in names:
+        body = s[s.index(name + ":"): s.index(".Lfunc_end", s.index(name + ":"))]
+        # the K loop's basic blocks: hipcc annotates every block of a loop ("Loop Header" /
+        # "in Loop: Header=...")
+        loop, inside = [], False
+        for l in body.split("\n"):
+            if re.match(r"^\.LBB\S*:|^; %bb", l):
+                inside = "Loop Header" in l or "in Loop:" in l
+                continue
+            if inside and l.strip() and not l.strip().startswith((";", ".")):
+                loop.append(l.strip())
+        copies = [l for l in loop if l.startswith(("v_mov_b", "v_accvgpr_mov", "v_accvgpr_write", "v_accvgpr_read"))]
+        assert not copies, (name, copies[:4])
+        assert sum(l.startswith("v_mfma_f32_32x32x16_bf16") for l in loop) >= 32
