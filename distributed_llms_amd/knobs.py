@@ -41,6 +41,12 @@ class Knobs:
     wide_target_wgs: int = 256        # split-K: about one workgroup per CU
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
+    # register-weight decode GEMM (gemm_rw.hip: weight fragments straight into VGPRs, activations
+    # through an LDS-DMA ring) for rw_min_m <= M <= 256: roles ("all", "none", or a comma list of
+    # gate_up / down / proj) -- ahead of gemm_sq / gemm_wide; rw_ns: ring slots (K-tiles in flight)
+    rw: str = "none"
+    rw_min_m: int = 1
+    rw_ns: int = 4
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
     # from this M up to 256, unsplit grids only unless sq_split
     sq: str = "all"
@@ -61,6 +67,9 @@ class Knobs:
     prefill_attn: int = 4             # prefill kernel version 1..5 (4: LDS-shared K/V tiles)
     # ---- model / engine
     fused_rope: bool = True           # decode: RoPE + KV append fused into attention
+    # fused decode: the KV append in workgroups of its own (no attention wave waits on its cache
+    # stores) instead of inside the attention waves
+    attn_append_sep: bool = False
     # split-K qkv partials summed inside the fused RoPE + attention kernel (no splitk_reduce launch):
     # +0.2-0.6 % tok/s in 4 of 4 interleaved in-engine pairs on two boxes (round 3,
     # profiles/round3_gemm_experiments.md; a round-2 build measured -3 %)

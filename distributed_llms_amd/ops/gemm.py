@@ -3,6 +3,8 @@
 Decode-sized M goes to hand-written gfx950 kernels, per projection role (cutovers measured in
 the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..knobs`):
 
+* register-weight kernel (gemm_rw.hip, knobs.rw roles): weight fragments stream straight into
+  VGPRs, activations through an LDS-DMA ring, split-K / SwiGLU like gemm_wide, M <= 256;
 * wide-M kernel (gemm_wide.hip: 64/128/192/256-row x 128 tiles, 3-stage LDS-DMA pipeline,
   split-K over workgroups) for every decode M:
   - gate|up (SwiGLU fused into the epilogue): M <= knobs.wide_gate_up_max_m (256);
@@ -90,6 +92,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     kn = knobs.K
     if bias is None and n > 65536 and 0 < kn.pp_head_min_m <= m <= 256 and _use_pp(m, n, k, x, w, 1):
         return linear_pp(x, w, splits=1, variant=PP_HEAD_VARIANT)           # decode LM head
+    if bias is None and use_rw(m, n, k, x, w):
+        return linear_rw(x, w, defer=defer, variant=kn.rw_ns)
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
     if bias is None and _use_pp(m, n, k, x, w, knobs.K.pp_proj_min_m):
@@ -178,6 +182,20 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     _ext.kernels().gemm_wide(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s,
                              1 if swiglu else 0, v, stream)
     return y
+
+
+def use_rw(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
+    """Decode GEMM on gemm_rw.hip (knobs.rw roles, rw_min_m <= M <= 256)."""
+    kn = knobs.K
+    roles = {t for t in kn.rw.split(",") if t and t != "none"}
+    if not roles or not (kn.rw_min_m <= m <= 256) or n % 128 or k % 64 or n > 65536:
+        return False
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        return False
+    if n * k * 2 >= (1 << 31) or m * k * 2 >= (1 << 31):
+        return False
+    role = "gate_up" if swiglu else ("down" if is_down_proj(n, k) else "proj")
+    return "all" in roles or role in roles
 
 
 def rw_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 256) -> int:
@@ -316,6 +334,8 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Te
     k = x.shape[-1]
     n = w_gate_up.shape[0]
     m = x.numel() // k
+    if use_rw(m, n, k, x, w_gate_up, swiglu=True):
+        return linear_rw(x, w_gate_up, swiglu=True, variant=knobs.K.rw_ns)
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
     if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):

@@ -12,3 +12,4 @@ timeout -k 10 400 $T tests/test_moe_gpu.py > gpurun_out/r4a_moe.log 2>&1 || { ta
 tail -2 gpurun_out/r4a_moe.log
 timeout -k 10 300 $T tests/test_pipeline_gpu.py -k standin > gpurun_out/r4a_standin.log 2>&1 || { tail -30 gpurun_out/r4a_standin.log; exit 1; }
 tail -2 gpurun_out/r4a_standin.log
+AB_RUNS="base: rw:rw=all base2: rw2:rw=all" bash scripts/gpu_ab_knobs.sh || exit 1
