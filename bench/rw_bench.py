@@ -22,6 +22,7 @@ SHAPES = {  # name: (N, K, swiglu, role)
     "gate_up": (28672, 4096, True, "swiglu"), "down": (4096, 14336, False, "defer"),
     "qkv70": (10240, 8192, False, "mat"), "o70": (8192, 8192, False, "defer"),
     "gate_up70": (57344, 8192, True, "swiglu"), "down70": (8192, 28672, False, "defer"),
+    "head": (128256, 4096, False, "mat"),
 }
 
 
@@ -54,7 +55,7 @@ def graph_of(fn, ws, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, nargs="+", default=[256])
-    ap.add_argument("--shapes", nargs="+", default=["qkv", "o", "gate_up", "down"])
+    ap.add_argument("--shapes", nargs="+", default=["qkv", "o", "gate_up", "down", "head"])
     ap.add_argument("--ns", type=int, nargs="+", default=[3, 4, 5])
     ap.add_argument("--splits", type=int, nargs="*", default=[])
     ap.add_argument("--rounds", type=int, default=3)
@@ -70,7 +71,9 @@ def main():
         for m in a.m:
             x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
             impls = {}
-            if m <= 512:
+            if name == "head":       # the engine's LM head today: gemm_pp schedule 2, nt weights
+                impls["wide"] = lambda w: gemm.linear_pp(x, w, splits=1, variant=gemm.PP_HEAD_VARIANT)
+            elif m <= 512:
                 impls["wide"] = (lambda w: gemm.linear_wide(x, w, swiglu=True)) if sw else \
                     (lambda w: gemm.linear_wide(x, w, defer=defer))
             base = gemm.rw_splits(m, n, k, sw)

@@ -43,7 +43,8 @@ class Knobs:
     wide_small_bm_maxw: int = 4096 * 4096
     # register-weight decode GEMM (gemm_rw.hip: weight fragments straight into VGPRs, activations
     # through an LDS-DMA ring) for rw_min_m <= M <= 256: roles ("all", "none", or a comma list of
-    # gate_up / down / proj) -- ahead of gemm_sq / gemm_wide; rw_ns: ring slots (K-tiles in flight)
+    # gate_up / down / proj / head) -- ahead of gemm_sq / gemm_wide / the gemm_pp LM head; rw_ns:
+    # ring slots (K-tiles in flight)
     rw: str = "none"
     rw_min_m: int = 1
     rw_ns: int = 4

@@ -90,10 +90,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if w.shape[1] != k:
         raise ValueError(f"linear: x[..., {k}] vs w {tuple(w.shape)}")
     kn = knobs.K
-    if bias is None and n > 65536 and 0 < kn.pp_head_min_m <= m <= 256 and _use_pp(m, n, k, x, w, 1):
-        return linear_pp(x, w, splits=1, variant=PP_HEAD_VARIANT)           # decode LM head
     if bias is None and use_rw(m, n, k, x, w):
         return linear_rw(x, w, defer=defer, variant=kn.rw_ns)
+    if bias is None and n > 65536 and 0 < kn.pp_head_min_m <= m <= 256 and _use_pp(m, n, k, x, w, 1):
+        return linear_pp(x, w, splits=1, variant=PP_HEAD_VARIANT)           # decode LM head
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
     if bias is None and _use_pp(m, n, k, x, w, knobs.K.pp_proj_min_m):
@@ -188,13 +188,13 @@ def use_rw(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: boo
     """Decode GEMM on gemm_rw.hip (knobs.rw roles, rw_min_m <= M <= 256)."""
     kn = knobs.K
     roles = {t for t in kn.rw.split(",") if t and t != "none"}
-    if not roles or not (kn.rw_min_m <= m <= 256) or n % 128 or k % 64 or n > 65536:
+    if not roles or not (kn.rw_min_m <= m <= 256) or n % 128 or k % 64:
         return False
     if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
         return False
     if n * k * 2 >= (1 << 31) or m * k * 2 >= (1 << 31):
         return False
-    role = "gate_up" if swiglu else ("down" if is_down_proj(n, k) else "proj")
+    role = "gate_up" if swiglu else ("down" if is_down_proj(n, k) else ("head" if n > 65536 else "proj"))
     return "all" in roles or role in roles
 
 
