@@ -56,7 +56,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, nargs="+", default=[256])
     ap.add_argument("--shapes", nargs="+", default=["qkv", "o", "gate_up", "down", "head"])
-    ap.add_argument("--ns", type=int, nargs="+", default=[3, 4, 5])
+    ap.add_argument("--ns", type=int, nargs="+", default=[0], help="ring depths (0: the row tile's default)")
     ap.add_argument("--splits", type=int, nargs="*", default=[])
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
@@ -79,7 +79,7 @@ def main():
             base = gemm.rw_splits(m, n, k, sw)
             for s in sorted({base} | set(a.splits)):
                 for ns in a.ns:
-                    for pol in a.policy:
+                    for pol in (a.policy if m > 128 else [0]):
                         v = ns | pol
                         impls[f"rw{ns}s{s}{'d' if pol else ''}"] = (
                             lambda w, s=s, v=v: gemm.linear_rw(x, w, splits=s, swiglu=sw, defer=defer, variant=v))

@@ -1,26 +1,28 @@
 // Register-weight decode GEMM for batch-sized M (<= 256): C[M,N] = A[M,K] . W[N,K]^T, bf16 in,
-// f32 accumulate.  The engine's decode projections (qkv, o, gate|up + SwiGLU, down) at B <= 256.
+// f32 accumulate.  The engine's decode projections (qkv, o, gate|up + SwiGLU, down, LM head).
 //
 // Why (profiles/round3_gemm_experiments.md): at M = 256 a decode projection sits on the ridge
-// between weight streaming and MFMA, and every LDS-staged design (gemm_wide, gemm_pp, gemm_gu) was
-// capped at the same ~48 GB/s per CU -- the weight bytes in flight per CU were bounded by the LDS
-// ring that also has to hold the (2x larger) activation tile.  Here the WEIGHTS never touch LDS:
+// between weight streaming and MFMA, and every LDS-staged design (gemm_wide, gemm_pp, and the
+// retired gemm_gu) was capped at the same ~48 GB/s per CU -- the weight bytes in flight per CU were
+// bounded by the LDS ring that also has to hold the (2x larger) activation tile.  Here the WEIGHTS
+// never touch LDS:
 //  * MFMA v_mfma_f32_32x32x16_bf16 with the weight as the A operand: lane l's A fragment is
 //    W[row l & 31][8 k-values] -- one 16-byte buffer load straight into 4 VGPRs per k-step (the
 //    K order inside a 64-deep K-tile is permuted so lane half h streams k 32h .. 32h + 31: the
 //    activation fragments use the same permutation, so the dot products are unchanged);
-//  * each of the 4 waves (one per SIMD) owns 32 weight rows x all 256 token rows: 8 accumulators of
-//    32 x 32 (128 registers), every weight fragment feeds 8 MFMAs, every activation fragment 1;
+//  * each of the 4 waves (one per SIMD) owns 32 weight rows x all BM token rows (BM = 64 / 128 /
+//    256 by M): BM / 32 accumulators of 32 x 32, every weight fragment feeds BM / 32 MFMAs;
 //  * only the activations (L2-resident, shared by the 4 waves) are staged, by LDS-DMA
 //    (buffer_load ... lds, 128-byte rows, 16-byte chunk swizzle c ^ ((row >> 1) & 7): conflict-free
-//    fragment reads), in an NS-slot ring of 32 KiB K-tiles: the whole 160 KiB of LDS holds
-//    activations, and the weight fragments of NS K-tiles ahead sit in NS + 1 register buffers;
+//    fragment reads), in an NS-slot ring of BM x 64 K-tiles; the weight fragments of the K-tiles in
+//    flight sit in NS register buffers (a smaller BM leaves LDS and registers for a deeper ring);
 //  * ONE barrier per K-tile, before its last k-step: every wave has read the K-tile into registers
 //    (its slot is re-staged from there), and the next K-tile has landed for every wave (counted
-//    vmcnt -- weights and activations of a K-tile are issued together, 12 VMEM ops per wave);
+//    vmcnt -- weights and activations of a K-tile are issued together, 4 + BM / 32 VMEM ops per wave);
 //  * per MFMA gap (24 free issue cycles behind a 32-cycle MFMA): 2 fragment reads of the next
-//    k-step in gaps 0-3, one VMEM op (weight fragment / LDS-DMA piece) in gaps 4-7, each MFMA
-//    waiting (counted lgkmcnt) only for the fragment it consumes;
+//    k-step in the first half of a k-step's gaps, the VMEM ops (weight fragments, LDS-DMA pieces)
+//    spread over the second halves, each MFMA waiting (counted lgkmcnt) only for the fragment it
+//    consumes;
 //  * epilogue straight from registers: a lane holds 4 consecutive output columns of one token row
 //    per 4-register group -> 8-byte stores of bf16 / f16 split-K slabs; SwiGLU: the wave's 32
 //    weight rows are 16 gate + 16 up rows of the same 16 outputs, so silu(g) * u is per lane;
@@ -38,9 +40,6 @@ namespace {
 typedef __attribute__((address_space(3))) void* lds_vptr_r;
 typedef int i32x4r __attribute__((ext_vector_type(4)));
 constexpr int RBK = 64;                 // K per tile (4 k-steps of 16)
-constexpr int RBM = 256;                // token rows per workgroup
-constexpr int RSLOT = RBM * RBK * 2;    // bytes per activation slot (32 KiB)
-constexpr int RG = 12;                  // VMEM ops per K-tile per wave: 4 weight fragments + 8 pieces
 
 template <int... I, class F>
 __device__ __forceinline__ void rw_for_impl(std::integer_sequence<int, I...>, F&& f) {
@@ -60,22 +59,15 @@ __device__ __forceinline__ void rw_vm() {
 // then tie the weight fragments w[0..3] the wait makes valid to an empty asm ("+v"): their loads
 // are inline asm the compiler does not track, so nothing may read them before this point.  The
 // counted waits take no operands and the tie is ONE statement after them: tied operands inside
-// the switch made hipcc merge the values through copies placed BEFORE the wait (copies of
+// the branches made hipcc merge the values through copies placed BEFORE the wait (copies of
 // registers still in flight).
-template <int MAXY>
+template <int MAXY, int RG>
 __device__ __forceinline__ void rw_wait_tiles(int younger, bf16x8 (&w)[4]) {
-  static_assert(MAXY >= 0 && MAXY <= 4 && MAXY * RG <= 63, "vmcnt range");
-  if (younger >= MAXY) {
-    rw_vm<MAXY * RG>();
-  } else if (younger <= 0) {
-    rw_vm<0>();
-  } else if (younger == 1) {
-    rw_vm<RG>();
-  } else if (younger == 2) {
-    if constexpr (MAXY > 2) rw_vm<2 * RG>();
-  } else {
-    if constexpr (MAXY > 3) rw_vm<3 * RG>();
-  }
+  static_assert(MAXY >= 0 && MAXY * RG <= 63, "vmcnt range");
+  younger = younger < 0 ? 0 : (younger > MAXY ? MAXY : younger);
+  rw_for<MAXY + 1>([&](auto y) {
+    if (younger == y.value) rw_vm<y.value * RG>();
+  });
   asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
 }
 
@@ -104,22 +96,30 @@ __device__ __forceinline__ void rw_lgkm(bf16x8& f) {
 }
 
 // the activation-fragment reads issued before MFMA mf of a k-step that are younger than fragment
-// mf of the current set: the rest of the current set (read 2 per gap in the previous k-step) +
-// the next set's reads issued in this k-step so far (2 per gap in gaps 0-3)
-constexpr int rw_younger(int mf) { return (7 - mf) + 2 * (mf < 4 ? mf : 4); }
+// mf of the current set: the rest of the current set (read 2 per gap in the first MFR / 2 gaps of
+// the previous k-step) + the next set's reads issued in this k-step so far
+constexpr int rw_younger(int mfr, int mf) { return (mfr - 1 - mf) + 2 * (mf < mfr / 2 ? mf : mfr / 2); }
 }  // namespace
 
 // MODE 0: C bf16 [M, N];  1: split-K slab P [S, M, N] (natural column order, also for SwiGLU
 // weights: the reducer applies silu(g) * u);  2: SwiGLU C [M, N / 2] from W = [Wg; Wu].
-// NS: activation ring slots (NS K-tiles of weights and activations in flight).  NT: weights
+// BM: token rows per workgroup (>= M).  NS: activation ring slots = weight register buffers; the
+// K-tiles t + 1 .. t + NS - 1 are in flight while K-tile t is multiplied.  NT: weights
 // nontemporal (read once per step).
-template <int NS, int MODE, bool SWROWS, bool NT>
+template <int BM, int NS, int MODE, bool SWROWS, bool NT>
 __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                          bf16* __restrict__ C, float* __restrict__ P, int M, int N,
                                                          int K, int kts, int nsplit) {
-  constexpr int NW = NS;                  // weight register buffers (K-tile u in buffer u mod NS)
-  static_assert(NS >= 3 && NS * RSLOT <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[NS * RSLOT];
+  constexpr int MFR = BM / 32;            // 32-row token fragments per wave (= LDS-DMA pieces per wave)
+  constexpr int AP = BM / 32;
+  constexpr int RG = 4 + AP;              // VMEM ops per K-tile per wave
+  constexpr int SLOT = BM * RBK * 2;      // bytes per activation slot
+  static_assert(BM == 64 || BM == 128 || BM == 256, "BM");
+  static_assert(NS >= 3 && NS * SLOT <= 160 * 1024 && (NS - 2) * RG <= 63, "ring");
+  // VMEM schedule: the RG ops of one K-tile (4 weight fragments, then AP pieces) spread over the
+  // NSL second-half gaps of a window's k-steps 0-2, in issue order
+  constexpr int NSL = 3 * (MFR / 2);
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -158,12 +158,12 @@ __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict_
       __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)((long)M * K * 2 - (long)kt0 * RBK * 2), 0x00020000);
   const uint32_t woff = (uint32_t)wrow_of(r) * (uint32_t)(K * 2) + (uint32_t)h * 64;
 
-  // LDS-DMA pieces: piece q of wave wv fills slot rows 8 pi .. 8 pi + 7 (pi = 8 wv + q), lane ->
+  // LDS-DMA pieces: piece q of wave wv fills slot rows 8 pi .. 8 pi + 7 (pi = AP wv + q), lane ->
   // (row 8 pi + lane / 8, physical chunk lane % 8) <- logical chunk (lane % 8) ^ swz(row)
-  uint32_t offA[8];
+  uint32_t offA[AP];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int row = 8 * (wv * 8 + q) + (lane >> 3);
+  for (int q = 0; q < AP; ++q) {
+    const int row = 8 * (wv * AP + q) + (lane >> 3);
     const int srow = row < M ? row : M - 1;
     offA[q] = (uint32_t)srow * (uint32_t)(K * 2) + (uint32_t)(((lane & 7) ^ ((row >> 1) & 7)) * 16);
   }
@@ -174,57 +174,59 @@ __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict_
 #pragma unroll
   for (int j = 0; j < 4; ++j) foff[j] = (uint32_t)(r * 128 + (((4 * h + j) ^ ((r >> 1) & 7)) * 16));
 
-  f32x16 acc[8];
+  f32x16 acc[MFR];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MFR; ++i)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-  bf16x8 wreg[NW][4];
-  bf16x8 fs0[8], fs1[8];
+  bf16x8 wreg[NS][4];
+  bf16x8 fs0[MFR], fs1[MFR];
 
   auto load_w = [&](bf16x8& dst, int t, int j) { rw_wload<NT>(dst, woff + j * 16, rsW, t * (RBK * 2)); };
   auto piece = [&](int slot, int t, int q) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_vptr_r)(smem + slot * RSLOT + (wv * 8 + q) * 1024), 16,
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_vptr_r)(smem + slot * SLOT + (wv * AP + q) * 1024), 16,
                                              (int)offA[q], t * (RBK * 2), 0, 0);
   };
-  auto reads2 = [&](bf16x8 (&dst)[8], uint32_t addr, auto g) {   // fragments 2g, 2g + 1 of a k-step
+  auto reads2 = [&](bf16x8 (&dst)[MFR], uint32_t addr, auto g) {   // fragments 2g, 2g + 1 of a k-step
     constexpr int G = decltype(g)::value;
     dst[2 * G] = rw_frag<(2 * G) * 4096>(addr);
     dst[2 * G + 1] = rw_frag<(2 * G + 1) * 4096>(addr);
   };
-  // one k-step: 8 MFMAs on fragment set `cur` with weight fragment `wf`; gaps 0-3 read the next
-  // k-step's fragments into `nxt` from LDS address `naddr` (if READ), gaps 4-7 run vm(g - 4)
-  auto kstep = [&](const bf16x8& wf, bf16x8 (&cur)[8], bf16x8 (&nxt)[8], uint32_t naddr, auto rd, auto waits,
+  // one k-step: MFR MFMAs on fragment set `cur` with weight fragment `wf`; gaps 0 .. MFR/2 - 1 read
+  // the next k-step's fragments into `nxt` from LDS address `naddr` (if READ), the other gaps run
+  // vm(gap - MFR / 2)
+  auto kstep = [&](const bf16x8& wf, bf16x8 (&cur)[MFR], bf16x8 (&nxt)[MFR], uint32_t naddr, auto rd, auto waits,
                    auto&& vm) {
     constexpr bool READ = decltype(rd)::value, WAIT = decltype(waits)::value;
-    rw_for<8>([&](auto mf) {
+    rw_for<MFR>([&](auto mf) {
       constexpr int MF = decltype(mf)::value;
-      if constexpr (WAIT) rw_lgkm<rw_younger(MF)>(cur[MF]);
+      if constexpr (WAIT) rw_lgkm<rw_younger(MFR, MF)>(cur[MF]);
       acc[MF] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, cur[MF], acc[MF], 0, 0, 0);
-      if constexpr (MF < 4) {
+      if constexpr (MF < MFR / 2) {
         if constexpr (READ) reads2(nxt, naddr, mf);
       } else {
-        vm(std::integral_constant<int, MF - 4>{});
+        vm(std::integral_constant<int, MF - MFR / 2>{});
       }
       __builtin_amdgcn_sched_barrier(0);
     });
   };
   auto no_vm = [](auto) {};
 
-  // ---- prologue: K-tiles 0 .. NS-2 (each: its 4 weight fragments, then its 8 LDS-DMA pieces).
-  // Straight-line: a K-tile past the slice (nt < NS - 1, tiny K only) is a dummy copy of K-tile
-  // nt - 1 into a buffer / slot nothing reads -- it only makes the waits below more conservative
+  // ---- prologue: K-tiles 0 .. NS-2 (each: its 4 weight fragments, then its AP LDS-DMA pieces).
+  // Straight-line: a K-tile past the slice (nt < NS - 1, short K slices only) is a dummy copy of
+  // K-tile nt - 1 into a buffer / slot nothing reads -- it only makes the waits below more
+  // conservative
   rw_for<NS - 1>([&](auto p) {
     const int tp = min((int)p.value, nt - 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) load_w(wreg[p.value][j], tp, j);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) piece(p.value, tp, q);
+    for (int q = 0; q < AP; ++q) piece(p.value, tp, q);
   });
-  rw_wait_tiles<NS - 2>(NS - 2, wreg[0]);
+  rw_wait_tiles<NS - 2, RG>(NS - 2, wreg[0]);
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  rw_for<4>([&](auto g) { reads2(fs0, lds0 + foff[0], g); });   // K-tile 0, k-step 0
+  rw_for<MFR / 2>([&](auto g) { reads2(fs0, lds0 + foff[0], g); });   // K-tile 0, k-step 0
   __builtin_amdgcn_sched_barrier(0);
 
   // ---- window t (I = t mod NS): the 4 k-steps of K-tile t (weight buffer I, slot t mod NS);
@@ -238,20 +240,30 @@ __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict_
   auto window = [&](int t, auto ic) {
     constexpr int I = decltype(ic)::value, IU = (I + NS - 1) % NS;
     const int s0 = t % NS, s1 = (t + 1) % NS, su = (t + NS - 1) % NS;
-    const uint32_t b0 = lds0 + (uint32_t)(s0 * RSLOT), b1 = lds0 + (uint32_t)(s1 * RSLOT);
+    const uint32_t b0 = lds0 + (uint32_t)(s0 * SLOT), b1 = lds0 + (uint32_t)(s1 * SLOT);
     const int tu = t + NS - 1;
     const bool issue = tu < nt;
-    kstep(wreg[I][0], fs0, fs1, b0 + foff[1], std::true_type{}, std::true_type{}, [&](auto g) {
-      if (issue) load_w(wreg[IU][decltype(g)::value], tu, decltype(g)::value);
-    });
-    kstep(wreg[I][1], fs1, fs0, b0 + foff[2], std::true_type{}, std::true_type{}, [&](auto g) {
-      if (issue) piece(su, tu, decltype(g)::value);
-    });
-    kstep(wreg[I][2], fs0, fs1, b0 + foff[3], std::true_type{}, std::true_type{}, [&](auto g) {
-      if (issue) piece(su, tu, 4 + decltype(g)::value);
-    });
+    // the VMEM ops whose schedule slot is (k-step j, second-half gap x)
+    auto ops = [&](auto jc, auto x) {
+      constexpr int SL = decltype(jc)::value * (MFR / 2) + decltype(x)::value;
+      rw_for<RG>([&](auto oc) {
+        constexpr int O = decltype(oc)::value;
+        if constexpr (O * NSL / RG == SL) {
+          if (issue) {
+            if constexpr (O < 4) load_w(wreg[IU][O], tu, O);
+            else piece(su, tu, O - 4);
+          }
+        }
+      });
+    };
+    kstep(wreg[I][0], fs0, fs1, b0 + foff[1], std::true_type{}, std::true_type{},
+          [&](auto x) { ops(std::integral_constant<int, 0>{}, x); });
+    kstep(wreg[I][1], fs1, fs0, b0 + foff[2], std::true_type{}, std::true_type{},
+          [&](auto x) { ops(std::integral_constant<int, 1>{}, x); });
+    kstep(wreg[I][2], fs0, fs1, b0 + foff[3], std::true_type{}, std::true_type{},
+          [&](auto x) { ops(std::integral_constant<int, 2>{}, x); });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    rw_wait_tiles<NS - 2>(nt - 2 - t, wreg[(I + 1) % NS]);
+    rw_wait_tiles<NS - 2, RG>(nt - 2 - t, wreg[(I + 1) % NS]);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     kstep(wreg[I][3], fs1, fs0, b1 + foff[0], std::true_type{}, std::false_type{}, no_vm);
@@ -267,7 +279,7 @@ __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict_
   // ---- epilogue: acc[mf] register 4 g + i = row 8 g + 4 h + i of the wave's 32 weight rows,
   // token mf * 32 + r
 #pragma unroll
-  for (int mf = 0; mf < 8; ++mf) {
+  for (int mf = 0; mf < MFR; ++mf) {
     const int m = mf * 32 + r;
     if (m >= M) continue;
     if constexpr (MODE == 2) {
@@ -307,21 +319,31 @@ __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict_
   }
 }
 
+static int rw_bm(int M) { return M <= 64 ? 64 : M <= 128 ? 128 : 256; }
+static int rw_default_ns(int bm) { return bm == 256 ? 4 : bm == 128 ? 6 : 8; }
+
 // mode 0: C = A W^T;  mode 1: SwiGLU, C[M, N/2] = silu(A Wg^T) * (A Wu^T) with W = [Wg; Wu];
 // mode 2: leave split-K partial slabs in ws (no reduce; S > 1 required).
-// variant: bits 0-3 ring slots NS (0 = 4; 3..5), bit 4: weights with the default cache policy
-// (else nontemporal).  Returns the effective number of K slices S.
+// variant: bits 0-3 ring slots NS (0 = the row tile's default: 4 / 6 / 8 at 256 / 128 / 64 rows;
+// 256 rows: 3..5, 128: 4 / 6 / 8, 64: 4 / 8), bit 4: weights with the default cache policy (else
+// nontemporal; 256-row tiles only), bits 8-9: row tile override (1 = 64, 2 = 128, 3 = 256).
+// Returns the effective number of K slices S.
 int gemm_rw(uintptr_t c, uintptr_t a, uintptr_t w, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream) {
-  DLLM_HOST_CHECK(M >= 1 && M <= RBM, "gemm_rw serves 1 <= M <= 256");
+  DLLM_HOST_CHECK(M >= 1 && M <= 256, "gemm_rw serves 1 <= M <= 256");
   DLLM_HOST_CHECK(K % RBK == 0 && K >= RBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(mode == 0 || mode == 1 || mode == 2, "mode");
   DLLM_HOST_CHECK(N % 128 == 0, "N must be a multiple of 128");
   DLLM_HOST_CHECK((long)N * K * 2 < (1L << 31) && (long)M * K * 2 < (1L << 31), "operands must be < 2 GiB");
   DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
-  const int ns = (variant & 15) ? (variant & 15) : 4;
-  DLLM_HOST_CHECK(ns >= 3 && ns <= 5, "ring slots 3..5");
-  const bool nt = (variant & 16) == 0;
+  const int bmo = (variant >> 8) & 3;
+  const int bm = bmo == 1 ? 64 : bmo == 2 ? 128 : bmo == 3 ? 256 : rw_bm(M);
+  DLLM_HOST_CHECK(M <= bm, "row tile override smaller than M");
+  const int ns = (variant & 15) ? (variant & 15) : rw_default_ns(bm);
+  DLLM_HOST_CHECK(bm != 256 || (ns >= 3 && ns <= 5), "ring slots at 256 rows: 3..5");
+  DLLM_HOST_CHECK(bm != 128 || ns == 4 || ns == 6 || ns == 8, "ring slots at 128 rows: 4, 6, 8");
+  DLLM_HOST_CHECK(bm != 64 || ns == 4 || ns == 8, "ring slots at 64 rows: 4, 8");
+  const bool nt = (variant & 16) == 0 || bm != 256;
   const bool swiglu = mode == 1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ktiles = K / RBK;
@@ -331,33 +353,39 @@ int gemm_rw(uintptr_t c, uintptr_t a, uintptr_t w, uintptr_t ws, long ws_floats,
   if (S > 1) DLLM_HOST_CHECK(ws != 0 && (long)S * M * N <= ws_floats, "split-K workspace too small");
   const int ntiles = swiglu ? (N / 2) / 64 : N / 128;
   const long grid = (long)ntiles * S;
-#define DLLM_RW_GO(NS_, MODE_, SW_, NT_)                                                                   \
-  hipLaunchKernelGGL((gemm_rw_kernel<NS_, MODE_, SW_, NT_>), dim3((unsigned)grid), dim3(256), 0, s,        \
+  const int kmode = S == 1 ? (swiglu ? 2 : 0) : 1;
+#define DLLM_RW_GO(BM_, NS_, MODE_, SW_, NT_)                                                               \
+  hipLaunchKernelGGL((gemm_rw_kernel<BM_, NS_, MODE_, SW_, NT_>), dim3((unsigned)grid), dim3(256), 0, s,    \
                      (const bf16*)a, (const bf16*)w, (bf16*)c, (float*)ws, M, N, K, kts, S)
-#define DLLM_RW_NS(MODE_, SW_, NT_)                        \
-  do {                                                     \
-    if (ns == 3) DLLM_RW_GO(3, MODE_, SW_, NT_);           \
-    else if (ns == 5) DLLM_RW_GO(5, MODE_, SW_, NT_);      \
-    else DLLM_RW_GO(4, MODE_, SW_, NT_);                   \
+#define DLLM_RW_MODES(BM_, NS_, NT_)                                          \
+  do {                                                                        \
+    if (kmode == 2) DLLM_RW_GO(BM_, NS_, 2, true, NT_);                       \
+    else if (kmode == 0) DLLM_RW_GO(BM_, NS_, 0, false, NT_);                 \
+    else if (swiglu) DLLM_RW_GO(BM_, NS_, 1, true, NT_);                      \
+    else DLLM_RW_GO(BM_, NS_, 1, false, NT_);                                 \
   } while (0)
-#define DLLM_RW_MODE(MODE_, SW_)                           \
-  do {                                                     \
-    if (nt) DLLM_RW_NS(MODE_, SW_, true);                  \
-    else DLLM_RW_NS(MODE_, SW_, false);                    \
-  } while (0)
-  if (S == 1) {
-    if (swiglu) DLLM_RW_MODE(2, true);
-    else DLLM_RW_MODE(0, false);
-    DLLM_HIP_CHECK(hipGetLastError());
-    return 1;
+  if (bm == 256) {
+    if (nt) {
+      if (ns == 3) DLLM_RW_MODES(256, 3, true);
+      else if (ns == 5) DLLM_RW_MODES(256, 5, true);
+      else DLLM_RW_MODES(256, 4, true);
+    } else {
+      if (ns == 3) DLLM_RW_MODES(256, 3, false);
+      else if (ns == 5) DLLM_RW_MODES(256, 5, false);
+      else DLLM_RW_MODES(256, 4, false);
+    }
+  } else if (bm == 128) {
+    if (ns == 4) DLLM_RW_MODES(128, 4, true);
+    else if (ns == 8) DLLM_RW_MODES(128, 8, true);
+    else DLLM_RW_MODES(128, 6, true);
+  } else {
+    if (ns == 4) DLLM_RW_MODES(64, 4, true);
+    else DLLM_RW_MODES(64, 8, true);
   }
-  if (swiglu) DLLM_RW_MODE(1, true);
-  else DLLM_RW_MODE(1, false);
-#undef DLLM_RW_MODE
-#undef DLLM_RW_NS
+#undef DLLM_RW_MODES
 #undef DLLM_RW_GO
   DLLM_HIP_CHECK(hipGetLastError());
-  if (mode == 2) return S;
+  if (S == 1 || mode == 2) return S;
   splitk_reduce_ex(c, ws, 0, S, M, N, swiglu ? 1 : 0, stream);
   return S;
 }

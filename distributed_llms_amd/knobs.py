@@ -47,7 +47,7 @@ class Knobs:
     # ring slots (K-tiles in flight)
     rw: str = "none"
     rw_min_m: int = 1
-    rw_ns: int = 4
+    rw_ns: int = 0                    # 0: the row tile's default (4 / 6 / 8 at 256 / 128 / 64 rows)
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
     # from this M up to 256, unsplit grids only unless sq_split
     sq: str = "all"

@@ -210,7 +210,9 @@ def linear_rw(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = 
     """Register-weight decode GEMM (csrc/kernels/gemm_rw.hip), M <= 256: weights stream straight
     into VGPRs as MFMA fragments, activations through an LDS-DMA ring; fused SwiGLU (``w`` =
     [Wg; Wu]) and split-K.  ``defer``: may return a :class:`SplitKPartial` (no SwiGLU).
-    ``variant``: bits 0-3 ring slots (0 = 4), bit 4 weights with the default cache policy."""
+    ``variant``: bits 0-3 ring slots (0 = the row tile's default), bit 4 weights with the default
+    cache policy (256-row tiles), bits 8-9 row tile override (1 = 64, 2 = 128, 3 = 256 rows; the
+    default is the smallest that holds M)."""
     k = x.shape[-1]
     n = w.shape[0]
     m = x.numel() // k

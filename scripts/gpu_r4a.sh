@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
 timeout -k 10 400 $T tests/test_gemm_rw_gpu.py > gpurun_out/r4a_rw_tests.log 2>&1 || { tail -30 gpurun_out/r4a_rw_tests.log; exit 1; }
 tail -2 gpurun_out/r4a_rw_tests.log
-timeout -k 10 300 python -u bench/rw_bench.py --rounds 3 > gpurun_out/r4a_rw_bench.log 2>&1 || { tail -30 gpurun_out/r4a_rw_bench.log; exit 1; }
+timeout -k 10 300 python -u bench/rw_bench.py --rounds 3 --ns 3 4 5 > gpurun_out/r4a_rw_bench.log 2>&1 || { tail -30 gpurun_out/r4a_rw_bench.log; exit 1; }
 cat gpurun_out/r4a_rw_bench.log
 timeout -k 10 400 $T tests/test_moe_gpu.py > gpurun_out/r4a_moe.log 2>&1 || { tail -30 gpurun_out/r4a_moe.log; exit 1; }
 tail -2 gpurun_out/r4a_moe.log

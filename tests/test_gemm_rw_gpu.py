@@ -14,11 +14,23 @@ def _bf(*s, scale=1.0):
     return (torch.randn(*s, device="cuda") * scale).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("m", [1, 31, 100, 255, 256])
+# ring depths each row tile is built with (csrc/kernels/gemm_rw.hip gemm_rw)
+NS_OF = {256: (3, 4, 5), 128: (4, 6, 8), 64: (4, 8)}
+
+
+def _ns(m, i):
+    bm = 64 if m <= 64 else 128 if m <= 128 else 256
+    if i >= len(NS_OF[bm]):
+        pytest.skip(f"{bm}-row tile has {len(NS_OF[bm])} ring depths")
+    return NS_OF[bm][i]
+
+
+@pytest.mark.parametrize("m", [1, 31, 64, 100, 128, 255, 256])
 @pytest.mark.parametrize("n,k,splits", [(6144, 4096, 1), (6144, 4096, 5), (4096, 14336, 8), (4096, 4096, 8),
                                         (1024, 512, 1), (256, 64, 1), (384, 192, 2)])
-@pytest.mark.parametrize("ns", [3, 4, 5])
-def test_rw_linear(cuda, m, n, k, splits, ns):
+@pytest.mark.parametrize("nsi", [0, 1, 2])
+def test_rw_linear(cuda, m, n, k, splits, nsi):
+    ns = _ns(m, nsi)
     torch.manual_seed(m * 7 + n + k + ns)
     x, w = _bf(m, k), _bf(n, k, scale=0.05)
     y = gemm.linear_rw(x, w, splits=splits, variant=ns)
@@ -27,8 +39,9 @@ def test_rw_linear(cuda, m, n, k, splits, ns):
 
 @pytest.mark.parametrize("m", [1, 77, 256])
 @pytest.mark.parametrize("inter,k,splits", [(14336, 4096, 1), (1024, 512, 1), (1024, 1024, 2), (64, 64, 1)])
-@pytest.mark.parametrize("ns", [3, 4, 5])
-def test_rw_swiglu(cuda, m, inter, k, splits, ns):
+@pytest.mark.parametrize("nsi", [0, 1, 2])
+def test_rw_swiglu(cuda, m, inter, k, splits, nsi):
+    ns = _ns(m, nsi)
     torch.manual_seed(m + inter + k + ns)
     x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
     y = gemm.linear_rw(x, w, splits=splits, swiglu=True, variant=ns)
@@ -81,6 +94,14 @@ def test_rw_graph_replay(cuda):
         g.replay()
         gu = x.float() @ w.float().t()
         torch.testing.assert_close(y.float(), F.silu(gu[:, :14336]) * gu[:, 14336:], atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("bm", [1, 2, 3])
+def test_rw_row_tile_override(cuda, bm):
+    """variant bits 8-9 force the 64 / 128 / 256-row tile for an M that fits it: same results."""
+    x, w = _bf(50, 4096), _bf(4096, 4096, scale=0.05)
+    y = gemm.linear_rw(x, w, splits=8, variant=bm << 8)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
 
 
 def test_rw_rejects_bad_shapes(cuda):
