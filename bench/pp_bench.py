@@ -125,6 +125,7 @@ def main():
                     v = vb | grp
                     impls[f"pp{bn}g{'S2' if grp & 64 else ''}"] = (lambda w, v=v: gemm.linear_pp(
                         x, w, splits=1, swiglu=sw, variant=v))
+            impls["pf"] = lambda w: gemm.linear_pf(x, w, swiglu=sw)   # persistent schedule 2
             graphs = {key: graph_of(f, [w], 2) for key, f in impls.items()}
             res = {key: [] for key in graphs}
             for _ in range(a.rounds):

@@ -718,4 +718,257 @@ void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintpt
   DLLM_HIP_CHECK(hipGetLastError());
 }
 
+// ---- Persistent prefill GEMM (gemm_pf): schedule 2's K-tile body, one workgroup per CU walking
+// its share of the 256 x 256 output tiles, the LDS-DMA pipeline CONTINUOUS across tile boundaries.
+//
+// Why (profiles/round3_gemm_experiments.md, per-CU timeline of schedule 2 at M = 8192): the loop
+// ran 92.5 % of the time -- every 256 x 256 tile paid a 4.3 us epilogue through an LDS image (the
+// ring cannot be restaged while the image occupies it), a prologue that waits for two K-tiles from
+// HBM, and a workgroup relaunch.  Here the pieces of the NEXT tile's first K-tiles are staged by the
+// current tile's last K-tiles exactly as any other K-tile (a tile boundary is invisible to the
+// ring), and the epilogue stores straight from the accumulators (a lane holds 4 consecutive output
+// columns of one row: 8-byte stores, 32 contiguous bytes per row and fragment, merged into full
+// lines in L2 by the same wave's neighbouring fragments), so no LDS, no barrier and no wait for the
+// ring is on the tile boundary -- only the stores' issue and the accumulator reset.
+//
+// Tile order: the grouped order of gemm_pp (8 row tiles x all column tiles per group), walked as
+// tile = w + i P by P = gridDim.x workgroups, w the XCD-aware rank (workgroup b runs on XCD b % 8;
+// w = (b % 8) (P / 8) + b / 8), so each XCD's L2 serves 32 consecutive tiles of the grouped order
+// (8 row tiles x 4 column tiles) at a time.
+// MODE 0: C bf16 [M, N];  2: SwiGLU C [M, N / 2] with B = [Bg; Bu] (row groups as pp_b_row).
+template <int MODE>
+__global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                         bf16* __restrict__ C, int M, int N, int K) {
+  constexpr int NW = 4, NWN = 2, BM = 256, BN = 256, TM = 128, TN = BN / NWN;
+  constexpr int RT = TM / 16, CT = TN / 16;            // 8 x 8 accumulators per wave
+  constexpr int SLOT = (BM + BN) * PBK, NB = 2;        // 2 x 64 KiB ring
+  constexpr int GA = BM * PBK * 2 / 1024 / NW, GB = BN * PBK * 2 / 1024 / NW, G = GA + GB;
+  constexpr bool SWIGLU = MODE == 2;
+  constexpr int OUTW = SWIGLU ? BN / 2 : BN;           // output tile width (elements)
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) bf16 smem[NB * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv / NWN, wn = wv % NWN;
+  const int ldc = SWIGLU ? N / 2 : N;
+  const int ntn = N / BN, mtiles = (M + BM - 1) / BM, tiles = ntn * mtiles;
+  const int P = gridDim.x;                             // a multiple of 8 (host)
+  const int w = (int)(blockIdx.x & 7) * (P >> 3) + (int)(blockIdx.x >> 3);
+  const int mine = w < tiles ? (tiles - 1 - w) / P + 1 : 0;
+  if (mine == 0) return;                               // uniform: before any load or barrier
+  const int nt = K / PBK, per = 8 * ntn;
+  auto tile_mn = [&](int i, int& m_t, int& n_t) {      // my i-th tile, grouped order
+    const int tau = w + i * P, g = tau / per, first = g * 8, gsz = min(mtiles - first, 8), q = tau - g * per;
+    m_t = first + q % gsz;
+    n_t = q / gsz;
+  };
+
+  // ---- staging side: tile s_i's K-tile s_kt; per-lane A row offsets of that tile (rows past M
+  // clamp to M - 1), B rows through the SGPR offset (uniform per piece)
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)(unsigned)((long)M * K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)(unsigned)((long)N * K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsC =
+      __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, (int)(unsigned)((long)M * ldc * 2), 0x00020000);
+  uint32_t chunk_q[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) chunk_q[par] = (uint32_t)(pswz(8 * par + (lane >> 3), lane & 7) * 16);
+  uint32_t offB[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) offB[par] = (uint32_t)(lane >> 3) * (uint32_t)(K * 2) + chunk_q[par];
+  uint32_t offA[GA];
+  int s_i = 0, s_kt = 0, s_n = 0;
+  auto set_stage = [&](int i) {
+    int m_t, n_t;
+    tile_mn(i, m_t, n_t);
+    s_n = n_t;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int q = wv * GA + j, r = 8 * q + (lane >> 3);
+      offA[j] = (uint32_t)min(m_t * BM + r, M - 1) * (uint32_t)(K * 2) + chunk_q[q & 1];
+    }
+  };
+  // piece p of the staging K-tile into ring slot `slot`
+  auto piece = [&](int slot, int p) {
+    bf16* base = smem + slot * SLOT;
+    if (p < GA) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_vptr_p)(base + (wv * GA + p) * 512), 16, (int)offA[p],
+                                               s_kt * PBK * 2, 0, 0);
+    } else {
+      const int q = wv * GB + p - GA;
+      const uint32_t brow = (uint32_t)pp_b_row<BN, SWIGLU>(8 * q, s_n, N / 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_vptr_p)(base + BM * PBK + q * 512), 16, (int)offB[q & 1],
+                                               (int)(brow * (uint32_t)(K * 2) + (uint32_t)(s_kt * PBK * 2)), 0, 0);
+    }
+  };
+  // next staging K-tile; past my last tile: K-tile nt - 1 of it again (a DUMMY piece into a slot
+  // nobody reads again, so every K-tile issues exactly G pieces: static vmcnt counts)
+  auto advance = [&]() {
+    if (++s_kt == nt) {
+      if (s_i + 1 < mine) {
+        ++s_i;
+        s_kt = 0;
+        set_stage(s_i);
+      } else {
+        s_kt = nt - 1;
+      }
+    }
+  };
+
+  const uint32_t lds_base = (uint32_t)(size_t)(lds_vptr_p)smem;
+  uint32_t lane_off[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+    lane_off[kh] = (uint32_t)((lane & 15) * 128 + ((4 * kh + (lane >> 4)) ^ (((lane & 15) >> 1) & 7)) * 16);
+  const uint32_t a_off = (uint32_t)(wm * TM * 128), b_off = (uint32_t)(BM * 128 + wn * TN * 128);
+
+  f32x4 acc[RT][CT];
+  bf16x8 fa0[RT], fb0[CT], fa1[RT], fb1[CT];
+  constexpr int NMF = RT * CT, NR = RT + CT;
+  constexpr int IB1 = 2 * NR + 8 < NMF - 1 ? 2 * NR + 8 : NMF - 1;
+  constexpr int GE = (2 * NMF - 4 - IB1 - 1) / G > 1 ? (2 * NMF - 4 - IB1 - 1) / G : 1;
+  constexpr int IB3 = 2 * NMF - 8 - 2 * NR > NMF ? 2 * NMF - 8 - 2 * NR : NMF;
+  constexpr int PB3 = (IB3 - IB1 - 1) / GE + 1 < G ? (IB3 - IB1 - 1) / GE + 1 : G;
+  constexpr int VC = (NB - 2) * G + PB3;
+  static_assert(IB1 + 1 + GE * (G - 1) < 2 * NMF && IB3 + 1 + 2 * (NR - 1) < 2 * NMF, "schedule 2 fits a K-tile");
+  static_assert(VC <= 63, "vmcnt");
+  auto rd0 = [&](uint32_t base, auto mc) {
+    constexpr int m = decltype(mc)::value;
+    if constexpr (m < CT) fb0[m] = pp_frag<m * 16 * 128>(base + b_off);
+    else fa0[m - CT] = pp_frag<(m - CT) * 16 * 128>(base + a_off);
+  };
+  auto rd1 = [&](uint32_t base, auto mc) {
+    constexpr int m = decltype(mc)::value;
+    if constexpr (m < CT) fb1[m] = pp_frag<m * 16 * 128>(base + b_off);
+    else fa1[m - CT] = pp_frag<(m - CT) * 16 * 128>(base + a_off);
+  };
+
+  // prologue: the first NB K-tiles of my first tile in flight, K-tile 0 landed, its K-half 0 read
+  set_stage(0);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+#pragma unroll
+    for (int p = 0; p < G; ++p) piece(j, p);
+    advance();
+  }
+  pp_vm<(NB - 1) * G>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  pp_static_for<NR>([&](auto mc) { rd0(lds_base + lane_off[0], mc); });
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int lr = lane & 15, lq = lane >> 4;
+  int slot = 0;
+  for (int ti = 0; ti < mine; ++ti) {
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < nt; ++t) {
+      // schedule 2's K-tile (gemm_pp_kernel): set-1 reads from the start, barrier after MFMA IB1
+      // (slot free), pieces of the staging K-tile one every GE MFMAs, counted vmcnt + barrier after
+      // MFMA IB3 (next K-tile landed -- across a tile boundary too), next K-half 0 reads
+      const int nslot = slot == NB - 1 ? 0 : slot + 1;
+      const uint32_t base1 = lds_base + (uint32_t)(slot * SLOT * 2) + lane_off[1];
+      const uint32_t base0 = lds_base + (uint32_t)(nslot * SLOT * 2) + lane_off[0];
+      pp_static_for<2 * NMF>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, h = i / NMF, j = i % NMF, r = j / CT, c = j % CT;
+        if constexpr (h == 0 && c == 0) {
+          constexpr int w0 = (RT - 1 - r) + (j / 2 < NR ? j / 2 : NR);
+          pp_lgkm<(w0 > 15 ? 15 : w0)>();
+        }
+        if constexpr (h == 0)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[c], fa0[r], acc[r][c], 0, 0, 0);
+        else
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[c], fa1[r], acc[r][c], 0, 0, 0);
+        if constexpr (i % 2 == 1 && i / 2 < NR) rd1(base1, std::integral_constant<int, i / 2>{});
+        if constexpr (i == IB1) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (i > IB1 && (i - IB1 - 1) % GE == 0 && (i - IB1 - 1) / GE < G) piece(slot, (i - IB1 - 1) / GE);
+        if constexpr (i == IB3) {
+          pp_vm<VC>();
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (i > IB3 && (i - IB3 - 1) % 2 == 0 && (i - IB3 - 1) / 2 < NR)
+          rd0(base0, std::integral_constant<int, (i - IB3 - 1) / 2>{});
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      advance();
+      slot = nslot;
+    }
+    // epilogue straight from the accumulators: acc[r][c] lane l = C[row wm TM + 16 r + (l & 15)]
+    // [col wn TN + 16 c + 4 (l >> 4) + v]; SwiGLU: fragments 2 cp (gate) and 2 cp + 1 (up) hold the
+    // same output columns.  Buffer stores, rows past M dropped by the range check (offset
+    // 0x80000000): straight-line, no branch to hoist accumulator reads over
+    int m_t, n_t;
+    tile_mn(ti, m_t, n_t);
+    const uint32_t colb = (uint32_t)(n_t * OUTW + wn * (OUTW / NWN) + 4 * lq) * 2;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      // pin row r's accumulators in AGPRs up to here: hipcc would otherwise copy all 256 to VGPRs
+      // at the K loop's exit (and spill, draining the pipeline with vmcnt(0) waits)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) asm volatile("" : "+a"(acc[r][c]));
+      const int row = m_t * BM + wm * TM + r * 16 + lr;
+      const uint32_t vo = row < M ? (uint32_t)row * (uint32_t)(ldc * 2) + colb : 0x80000000u;
+      if constexpr (SWIGLU) {
+#pragma unroll
+        for (int cp = 0; cp < CT / 2; ++cp) {
+          const f32x4 g = acc[r][2 * cp], u = acc[r][2 * cp + 1];
+          bf16x4 h;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) h[v] = f2bf(silu_f(g[v]) * u[v]);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rsC, (int)(vo + cp * 32), 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          bf16x4 h;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) h[v] = f2bf(acc[r][c][v]);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rsC, (int)(vo + c * 32), 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // the dummy pieces of the last K-tiles must land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Persistent prefill GEMM: C = A B^T (mode 0) or SwiGLU (mode 1, C [M, N / 2], B = [Bg; Bu]),
+// 256 x 256 tiles, grid = min(tiles, CUs) rounded up to a multiple of 8.
+void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mode, uintptr_t stream) {
+  DLLM_HOST_CHECK(M >= 1, "M >= 1");
+  DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
+  DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
+  DLLM_HOST_CHECK((long)M * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32) && (long)M * N * 2 < (1L << 31),
+                  "operands must be < 4 GiB, the output < 2 GiB");
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    DLLM_HIP_CHECK(hipGetDevice(&dev));
+    DLLM_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    cus = n > 0 ? n : 256;
+  }
+  const long tiles = (long)(N / 256) * ((M + 255) / 256);
+  DLLM_HOST_CHECK(tiles < (1L << 30), "tiles");
+  const long grid = ((tiles < cus ? tiles : cus) + 7) / 8 * 8;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (mode == 1)
+    hipLaunchKernelGGL((gemm_pf_kernel<2>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, (const bf16*)b,
+                       (bf16*)c, M, N, K);
+  else
+    hipLaunchKernelGGL((gemm_pf_kernel<0>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, (const bf16*)b,
+                       (bf16*)c, M, N, K);
+  DLLM_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace dllm

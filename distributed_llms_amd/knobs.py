@@ -18,6 +18,7 @@ DLLM_TUNABLEOP_FILE.
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import json
 import os
@@ -60,6 +61,10 @@ class Knobs:
     # the plain projections still trail hipBLASLt (1434-1448 vs 1546-1631), so off
     pp_swiglu_min_m: int = 2048
     pp_proj_min_m: int = 0
+    # the prefill GEMMs above (pp_swiglu_min_m / pp_proj_min_m) on the persistent form of schedule
+    # 2 (gemm_pf: one workgroup per CU, the LDS-DMA pipeline continuous across output tiles, the
+    # epilogue stored straight from the accumulators) instead of one workgroup per tile
+    pp_persistent: bool = False
     # decode LM head (N > 65536) at pp_head_min_m <= M <= 256 on gemm_pp schedule 2 with nontemporal
     # weights: 230 vs 265 us for gemm_sq at M = 256 (Llama-3-8B); 0 = off
     pp_head_min_m: int = 225
@@ -114,6 +119,17 @@ def update(overrides: Optional[Mapping[str, Any]] = None, **kw) -> Knobs:
     for k, v in items.items():
         setattr(K, k, _coerce(k, v))
     return K
+
+
+@contextlib.contextmanager
+def override(**kw):
+    """Temporarily apply overrides (restored on exit, also on an exception)."""
+    saved = dataclasses.asdict(K)
+    update(kw)
+    try:
+        yield K
+    finally:
+        update(saved)
 
 
 def reset() -> Knobs:

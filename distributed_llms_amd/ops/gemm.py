@@ -97,6 +97,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
     if bias is None and _use_pp(m, n, k, x, w, knobs.K.pp_proj_min_m):
+        if kn.pp_persistent and m * n * 2 < (1 << 31):
+            return linear_pf(x, w)
         return linear_pp(x, w, splits=1, variant=PP_PREFILL_VARIANT)
     return F.linear(x, w, bias)
 
@@ -271,6 +273,23 @@ def linear_pp(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = 
     return y
 
 
+def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
+    """Persistent prefill GEMM (gemm_pf in csrc/kernels/gemm_pp.hip): schedule 2's 256 x 256 tiles,
+    one workgroup per CU walking its tiles with the LDS-DMA pipeline running across tile
+    boundaries; optional fused SwiGLU (``w`` = [Wg; Wu], y [M, N / 2])."""
+    k = x.shape[-1]
+    n = w.shape[0]
+    m = x.numel() // k
+    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
+        raise ValueError("linear_pf: bf16 contiguous operands")
+    if n % 256 or k % 64:
+        raise ValueError("linear_pf: N % 256 and K % 64")
+    y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
+    _ext.kernels().gemm_pf(y.data_ptr(), x.data_ptr(), w.data_ptr(), m, n, k, 1 if swiglu else 0,
+                           torch.cuda.current_stream().cuda_stream)
+    return y
+
+
 # 256 x 256-tile decode GEMM (gemm_sq.hip) for 128 < M <= 256: a third fewer staged bytes per FLOP
 # than the wide kernel's 256 x 128 tile.  Measured (profiles/wide_gemm.md, "256 x 256 tile"): it
 # wins only where the grid needs no K split -- the LM head (1.05x) and the 70B MLP gate|up (1.07x);
@@ -341,5 +360,7 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Te
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
     if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):
+        if knobs.K.pp_persistent and m * n * 2 < (1 << 31):
+            return linear_pf(x, w_gate_up, swiglu=True)
         return linear_pp(x, w_gate_up, splits=1, swiglu=True, variant=PP_PREFILL_VARIANT)
     return None

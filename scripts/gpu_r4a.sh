@@ -1,15 +1,24 @@
 #!/bin/bash
 # Round 4, first GPU pass: new kernels' numerics, the RCCL transport stand-in on one GPU, then the
-# register-weight GEMM bench.  Each step under its own time limit; stop at the first failure.
+# register-weight GEMM bench.  Each step under its own time limit.  A failing test step is
+# reported and the next step runs; a time limit, abort or crash (124 / 137 / 134 / 139) ends the call.
 set -o pipefail
 mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
-timeout -k 10 400 $T tests/test_gemm_rw_gpu.py > gpurun_out/r4a_rw_tests.log 2>&1 || { tail -30 gpurun_out/r4a_rw_tests.log; exit 1; }
-tail -2 gpurun_out/r4a_rw_tests.log
-timeout -k 10 300 python -u bench/rw_bench.py --rounds 3 --ns 3 4 5 > gpurun_out/r4a_rw_bench.log 2>&1 || { tail -30 gpurun_out/r4a_rw_bench.log; exit 1; }
-cat gpurun_out/r4a_rw_bench.log
-timeout -k 10 400 $T tests/test_moe_gpu.py > gpurun_out/r4a_moe.log 2>&1 || { tail -30 gpurun_out/r4a_moe.log; exit 1; }
-tail -2 gpurun_out/r4a_moe.log
-timeout -k 10 300 $T tests/test_pipeline_gpu.py -k standin > gpurun_out/r4a_standin.log 2>&1 || { tail -30 gpurun_out/r4a_standin.log; exit 1; }
-tail -2 gpurun_out/r4a_standin.log
-AB_RUNS="base: rw:rw=all base2: rw2:rw=all" bash scripts/gpu_ab_knobs.sh || exit 1
+step() {   # step <log> <limit> <command...>
+  local log=$1 lim=$2; shift 2
+  timeout -k 10 $lim "$@" > gpurun_out/$log 2>&1
+  local rc=$?
+  tail -${TAILN:-3} gpurun_out/$log
+  case $rc in
+    0) ;;
+    124|137|134|139) echo "STOP: $log rc=$rc"; exit $rc ;;
+    *) echo "FAILED: $log rc=$rc" ;;
+  esac
+}
+step r4a_pf_tests.log 300 $T tests/test_gemm_gpu.py -k "pf_"
+TAILN=40 step r4a_pf_bench.log 300 python -u bench/pp_bench.py --no-decode --prefill 32768 8192 --rounds 2
+step r4a_rw_tests.log 400 $T tests/test_gemm_rw_gpu.py
+TAILN=60 step r4a_rw_bench.log 300 python -u bench/rw_bench.py --rounds 3 --ns 3 4 5
+step r4a_moe.log 400 $T tests/test_moe_gpu.py
+step r4a_standin.log 300 $T tests/test_pipeline_gpu.py -k standin

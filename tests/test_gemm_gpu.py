@@ -308,6 +308,49 @@ def test_pp_swiglu(cuda, m, inter, k, splits, variant):
     torch.testing.assert_close(y.float(), ref, atol=6e-2, rtol=3e-2)
 
 
+# ---- gemm_pf: persistent schedule-2 prefill kernel (tiles per workgroup > 1, row tails, tiny grids)
+@pytest.mark.parametrize("m", [1, 77, 256, 300, 2048, 4100, 9000])
+@pytest.mark.parametrize("n,k", [(6144, 4096), (4096, 14336), (512, 192), (256, 64), (1024, 128)])
+def test_pf_linear(cuda, m, n, k):
+    torch.manual_seed(m + n + k)
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear_pf(x, w)
+    ref = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m", [64, 1000, 4096])
+@pytest.mark.parametrize("inter,k", [(14336, 4096), (384, 256), (128, 64)])
+def test_pf_swiglu(cuda, m, inter, k):
+    torch.manual_seed(m * 3 + inter)
+    x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
+    y = gemm.linear_pf(x, w, swiglu=True)
+    gu = x.float() @ w.float().t()
+    ref = F.silu(gu[:, :inter]) * gu[:, inter:]
+    torch.testing.assert_close(y.float(), ref, atol=6e-2, rtol=3e-2)
+
+
+def test_pf_matches_pp_schedule2_bit_exact(cuda):
+    """Same K-tile body and accumulation order as gemm_pp schedule 2: identical bits, plain and
+    SwiGLU (the SwiGLU of gemm_pp rounds gate / up to bf16 first, so only the plain form is exact)."""
+    x, w = _bf(5000, 4096), _bf(6144, 4096, scale=0.05)
+    assert torch.equal(gemm.linear_pf(x, w), gemm.linear_pp(x, w, splits=1, variant=gemm.PP_PREFILL_VARIANT))
+
+
+def test_pf_dispatch_and_graph(cuda):
+    from distributed_llms_amd import knobs
+    x, w = _bf(4096, 4096), _bf(4096, 4096, scale=0.05)
+    with knobs.override(pp_proj_min_m=2048, pp_persistent=True):
+        y0 = gemm.linear(x, w)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            y = gemm.linear(x, w)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
+
+
 def test_pp_deferred_splitk_matches_materialized_and_wide(cuda):
     x, w = _bf(256, 14336), _bf(4096, 14336, scale=0.05)
     p = gemm.linear_pp(x, w, splits=16, defer=True)

@@ -61,3 +61,32 @@ def test_rw_main_loop_has_no_register_copies(rw_asm):
         copies = [l for l in loop if l.startswith(("v_mov_b", "v_accvgpr_mov", "v_accvgpr_write", "v_accvgpr_read"))]
         assert not copies, (name, copies[:4])
         assert sum(l.startswith("v_mfma_f32_32x32x16_bf16") for l in loop) >= 32
+
+
+@pytest.fixture(scope="module")
+def pp_asm(tmp_path_factory):
+    src = ROOT / "distributed_llms_amd" / "csrc" / "kernels" / "gemm_pp.hip"
+    out = tmp_path_factory.mktemp("asm") / "pp.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "--offload-device-only", "-S",
+                    str(src), f"-I{src.parent}", "-o", str(out)], check=True, capture_output=True, timeout=900)
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_pf_persistent_kernel_keeps_the_pipeline_full(pp_asm):
+    """gemm_pf (persistent schedule 2): no scratch spills (a spill reload in the tile loop waits on
+    vmcnt, i.e. drains the LDS-DMA pipeline the persistent form exists to keep full), and no
+    vmcnt(0) anywhere before the final drain -- the tile-boundary epilogue included."""
+    s = pp_asm.read_text()
+    names = re.findall(r"^(_ZN4dllm14gemm_pf_kernel\w+):", s, re.M)
+    assert len(names) == 2
+    for name in names:
+        start = s.index(name + ":")
+        body = s[start: s.index(".Lfunc_end", start)]
+        meta = s[s.index(".amdhsa_kernel " + name):]
+        scratch = int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", meta).group(1))
+        assert scratch == 0, (name, scratch)
+        assert "scratch_" not in body
+        waits = re.findall(r"s_waitcnt vmcnt\((\d+)\)", body)
+        assert waits.count("0") <= 1, (name, waits)
+        assert body.count("v_mfma_f32_16x16x32_bf16") >= 128
