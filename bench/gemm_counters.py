@@ -1,6 +1,7 @@
-"""GEMM kernels for rocprofv3 counter passes (scripts/gpu_gemm_counters.sh): the ping-pong
-kernel and hipBLASLt on one prefill shape, the wide and ping-pong kernels on the decode MLP
-up projection, each a few dispatches."""
+"""GEMM kernels for rocprofv3 counter passes (scripts/gpu_gemm_counters.sh), a few dispatches
+each.  GCTR=decode: the decode MLP gate|up (M = 256, SwiGLU) on gemm_wide and on gemm_rw (default
+and nontemporal weight policy), the o projection (split-K) on both.  GCTR=prefill: a prefill
+projection (T = 8192, N = 6144, K = 4096) on gemm_pf, gemm_pp schedule 2 and hipBLASLt."""
 import os
 import sys
 
@@ -15,18 +16,23 @@ from distributed_llms_amd.ops import gemm
 def main():
     torch.manual_seed(0)
     bf = lambda *s, sc=1.0: (torch.randn(*s, device="cuda") * sc).to(torch.bfloat16)   # noqa: E731
-    var = int(os.environ.get("PP_VAR", "4"))
-    x, w = bf(8192, 4096), bf(14336, 4096, sc=0.02)
-    xd, wd = bf(256, 4096), bf(28672, 4096, sc=0.02)
-    decode_only = os.environ.get("DECODE_ONLY") == "1"
-    for _ in range(4):
-        if not decode_only:
-            gemm.linear_pp(x, w, splits=1, variant=var)
+    mode = os.environ.get("GCTR", "decode")
+    if mode == "decode":
+        xd = bf(256, 4096)
+        wgu = [bf(28672, 4096, sc=0.02) for _ in range(4)]    # > L2 / MALL reuse between calls
+        wo = [bf(4096, 4096, sc=0.02) for _ in range(4)]
+        for i in range(4):
+            gemm.linear_wide(xd, wgu[i % 4], swiglu=True)
+            gemm.linear_rw(xd, wgu[(i + 1) % 4], swiglu=True, variant=16 | 4)
+            gemm.linear_rw(xd, wgu[(i + 2) % 4], swiglu=True, variant=4)
+            gemm.linear_wide(xd, wo[i % 4], defer=True)
+            gemm.linear_rw(xd, wo[(i + 1) % 4], defer=True, variant=16 | 4)
+    else:
+        x, w = bf(8192, 4096), bf(6144, 4096, sc=0.02)
+        for _ in range(4):
+            gemm.linear_pf(x, w)
+            gemm.linear_pp(x, w, splits=1, variant=gemm.PP_PREFILL_VARIANT)
             F.linear(x, w)
-            gemm.linear_pp(xd, wd, splits=1, swiglu=True, variant=1 | 2)
-        gemm.linear_wide(xd, wd, swiglu=True)
-        gemm.linear_gate_up56(xd, wd, variant=0)
-        gemm.linear_gate_up56(xd, wd, variant=1)
     torch.cuda.synchronize()
 
 

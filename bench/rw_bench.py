@@ -4,7 +4,7 @@ Each implementation runs as the engine runs it (qkv materialised, o / down defer
 gate|up with the SwiGLU) inside one HIP graph that rotates through > 768 MB of weight copies, so
 every call streams its weight from HBM as a decode step does.  Interleaved rounds, min over rounds.
 
-    python bench/rw_bench.py [--m 256] [--shapes qkv o gate_up down] [--ns 3 4 5]
+    python bench/rw_bench.py [--m 256] [--shapes qkv o gate_up down] [--ns 3 4 5] [--packed 0 1]
 """
 import argparse
 import os
@@ -60,7 +60,7 @@ def main():
     ap.add_argument("--splits", type=int, nargs="*", default=[])
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--policy", type=int, nargs="+", default=[0, 16])
+    ap.add_argument("--packed", type=int, nargs="+", default=[0, 1], help="0: nn.Linear layout, 1: pack_rw")
     a = ap.parse_args()
     torch.manual_seed(0)
     for name in a.shapes:
@@ -68,23 +68,25 @@ def main():
         defer = role == "defer"
         copies = max(2, -(-(768 << 20) // (n * k * 2)))
         ws = [(torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(copies)]
+        wps = [gemm.pack_rw(w, sw) for w in ws] if 1 in a.packed else []
         for m in a.m:
             x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
             impls = {}
             if name == "head":       # the engine's LM head today: gemm_pp schedule 2, nt weights
-                impls["wide"] = lambda w: gemm.linear_pp(x, w, splits=1, variant=gemm.PP_HEAD_VARIANT)
+                impls["wide"] = (lambda w: gemm.linear_pp(x, w, splits=1, variant=gemm.PP_HEAD_VARIANT), ws)
             elif m <= 512:
-                impls["wide"] = (lambda w: gemm.linear_wide(x, w, swiglu=True)) if sw else \
-                    (lambda w: gemm.linear_wide(x, w, defer=defer))
+                impls["wide"] = ((lambda w: gemm.linear_wide(x, w, swiglu=True)) if sw else
+                                 (lambda w: gemm.linear_wide(x, w, defer=defer)), ws)
             base = gemm.rw_splits(m, n, k, sw)
             for s in sorted({base} | set(a.splits)):
                 for ns in a.ns:
-                    for pol in (a.policy if m > 128 else [0]):
-                        v = ns | pol
-                        impls[f"rw{ns}s{s}{'d' if pol else ''}"] = (
-                            lambda w, s=s, v=v: gemm.linear_rw(x, w, splits=s, swiglu=sw, defer=defer, variant=v))
+                    for pk in a.packed:
+                        impls[f"rw{ns}s{s}{'p' if pk else ''}"] = (
+                            lambda w, s=s, ns=ns, pk=pk: gemm.linear_rw(x, w, splits=s, swiglu=sw, defer=defer,
+                                                                        variant=ns, packed=bool(pk)),
+                            wps if pk else ws)
             reps = max(copies, 8)
-            graphs = {key: graph_of(f, ws, reps) for key, f in impls.items()}
+            graphs = {key: graph_of(f, wl, reps) for key, (f, wl) in impls.items()}
             res = {key: [] for key in graphs}
             for _ in range(a.rounds):
                 for key, g in graphs.items():
@@ -96,7 +98,7 @@ def main():
                   + f" | best {best} {t[best]:.1f} us = {wb / t[best] / 1e6:.2f} TB/s"
                   + (f" ({t['wide'] / t[best]:.2f}x wide)" if "wide" in t else ""), flush=True)
             del graphs
-        del ws
+        del ws, wps
         torch.cuda.empty_cache()
 
 

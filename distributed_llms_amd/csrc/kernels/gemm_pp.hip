@@ -746,6 +746,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   constexpr bool SWIGLU = MODE == 2;
   constexpr int OUTW = SWIGLU ? BN / 2 : BN;           // output tile width (elements)
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) bf16 smem[NB * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -865,7 +866,10 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
 #pragma unroll
     for (int i = 0; i < RT; ++i)
 #pragma unroll
-      for (int j = 0; j < CT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < CT; ++j) {
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        asm volatile("" : "+a"(acc[i][j]));            // zeroed in place, in AGPRs
+      }
     for (int t = 0; t < nt; ++t) {
       // schedule 2's K-tile (gemm_pp_kernel): set-1 reads from the start, barrier after MFMA IB1
       // (slot free), pieces of the staging K-tile one every GE MFMAs, counted vmcnt + barrier after
@@ -903,12 +907,15 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
       slot = nslot;
     }
     // epilogue straight from the accumulators: acc[r][c] lane l = C[row wm TM + 16 r + (l & 15)]
-    // [col wn TN + 16 c + 4 (l >> 4) + v]; SwiGLU: fragments 2 cp (gate) and 2 cp + 1 (up) hold the
-    // same output columns.  Buffer stores, rows past M dropped by the range check (offset
-    // 0x80000000): straight-line, no branch to hoist accumulator reads over
+    // [col wn TN + 16 c + 4 (l >> 4) + v] (SwiGLU: fragments 2 cp (gate) and 2 cp + 1 (up) hold the
+    // same output columns).  Two fragments' bf16 quads per lane are exchanged between 16-lane rows
+    // (v_permlane16_swap: row 1 <-> row 0's partner, row 3 <-> row 2's) so that every lane holds 8
+    // consecutive columns: 16-byte stores, a row's 16 lanes covering 64 contiguous bytes.  Buffer
+    // stores, rows past M dropped by the range check (offset 0x80000000): no branch to hoist
+    // accumulator reads over.
     int m_t, n_t;
     tile_mn(ti, m_t, n_t);
-    const uint32_t colb = (uint32_t)(n_t * OUTW + wn * (OUTW / NWN) + 4 * lq) * 2;
+    const uint32_t colb = (uint32_t)(n_t * OUTW + wn * (OUTW / NWN) + 16 * (lq & 1) + 8 * (lq >> 1)) * 2;
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       // pin row r's accumulators in AGPRs up to here: hipcc would otherwise copy all 256 to VGPRs
@@ -917,23 +924,32 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
       for (int c = 0; c < CT; ++c) asm volatile("" : "+a"(acc[r][c]));
       const int row = m_t * BM + wm * TM + r * 16 + lr;
       const uint32_t vo = row < M ? (uint32_t)row * (uint32_t)(ldc * 2) + colb : 0x80000000u;
-      if constexpr (SWIGLU) {
+      constexpr int NQ = SWIGLU ? CT / 2 : CT;         // bf16 quads per lane in this row group
+      u32x2 q[NQ];
 #pragma unroll
-        for (int cp = 0; cp < CT / 2; ++cp) {
-          const f32x4 g = acc[r][2 * cp], u = acc[r][2 * cp + 1];
-          bf16x4 h;
+      for (int i = 0; i < NQ; ++i) {
+        bf16x4 hq;
+        if constexpr (SWIGLU) {
+          const f32x4 g = acc[r][2 * i], u = acc[r][2 * i + 1];
 #pragma unroll
-          for (int v = 0; v < 4; ++v) h[v] = f2bf(silu_f(g[v]) * u[v]);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rsC, (int)(vo + cp * 32), 0, 0);
+          for (int v = 0; v < 4; ++v) hq[v] = f2bf(silu_f(g[v]) * u[v]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) hq[v] = f2bf(acc[r][i][v]);
         }
-      } else {
+        q[i] = __builtin_bit_cast(u32x2, hq);
+      }
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          bf16x4 h;
+      for (int pr = 0; pr < NQ / 2; ++pr) {
+        u32x2 x = q[2 * pr], y = q[2 * pr + 1];
 #pragma unroll
-          for (int v = 0; v < 4; ++v) h[v] = f2bf(acc[r][c][v]);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rsC, (int)(vo + c * 32), 0, 0);
+        for (int d = 0; d < 2; ++d) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
+          x[d] = sw[0];
+          y[d] = sw[1];
         }
+        const u32x4 o = {x[0], x[1], y[0], y[1]};
+        __builtin_amdgcn_raw_buffer_store_b128(o, rsC, (int)(vo + pr * 64), 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }

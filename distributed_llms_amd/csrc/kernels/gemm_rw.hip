@@ -7,9 +7,10 @@
 // bounded by the LDS ring that also has to hold the (2x larger) activation tile.  Here the WEIGHTS
 // never touch LDS:
 //  * MFMA v_mfma_f32_32x32x16_bf16 with the weight as the A operand: lane l's A fragment is
-//    W[row l & 31][8 k-values] -- one 16-byte buffer load straight into 4 VGPRs per k-step (the
-//    K order inside a 64-deep K-tile is permuted so lane half h streams k 32h .. 32h + 31: the
-//    activation fragments use the same permutation, so the dot products are unchanged);
+//    W[row l & 31][k 16 j + 8 (l >> 5) ..+ 8] at k-step j -- one 16-byte buffer load straight into
+//    4 VGPRs (default cache policy: nontemporal loads doubled the L2 requests, 106 vs 82 us on the
+//    8B gate|up); from the nn.Linear layout that is 64 lanes in 64 rows, so the packed
+//    fragment-major layout (PK below) is the fast form;
 //  * each of the 4 waves (one per SIMD) owns 32 weight rows x all BM token rows (BM = 64 / 128 /
 //    256 by M): BM / 32 accumulators of 32 x 32, every weight fragment feeds BM / 32 MFMAs;
 //  * only the activations (L2-resident, shared by the 4 waves) are staged, by LDS-DMA
@@ -74,12 +75,8 @@ __device__ __forceinline__ void rw_wait_tiles(int younger, bf16x8 (&w)[4]) {
 // one weight fragment: 16 bytes per lane straight into VGPRs (buffer_load_dwordx4, voffset +
 // soffset), in inline asm so that hipcc inserts no vmcnt waits of its own (its loop-carried
 // scoreboard falls back to vmcnt(0)); validity comes from rw_wait_tiles
-template <bool NT>
 __device__ __forceinline__ void rw_wload(bf16x8& dst, uint32_t voff, const i32x4r& rs, int soff) {
-  if constexpr (NT)
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen nt" : "=v"(dst) : "v"(voff), "s"(rs), "s"(soff));
-  else
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(dst) : "v"(voff), "s"(rs), "s"(soff));
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(dst) : "v"(voff), "s"(rs), "s"(soff));
 }
 
 template <int OFF>
@@ -104,9 +101,15 @@ constexpr int rw_younger(int mfr, int mf) { return (mfr - 1 - mf) + 2 * (mf < mf
 // MODE 0: C bf16 [M, N];  1: split-K slab P [S, M, N] (natural column order, also for SwiGLU
 // weights: the reducer applies silu(g) * u);  2: SwiGLU C [M, N / 2] from W = [Wg; Wu].
 // BM: token rows per workgroup (>= M).  NS: activation ring slots = weight register buffers; the
-// K-tiles t + 1 .. t + NS - 1 are in flight while K-tile t is multiplied.  NT: weights
-// nontemporal (read once per step).
-template <int BM, int NS, int MODE, bool SWROWS, bool NT>
+// K-tiles t + 1 .. t + NS - 1 are in flight while K-tile t is multiplied.
+// PK: W is stored FRAGMENT-MAJOR (ops/gemm.py pack_rw): 32-row group g, K-tile t, k-step j, lane L
+// -> 16 bytes at ((g KT + t) 4 + j) 64 + L (16-byte units) = W[32 g + (L & 31)][64 t + 16 j +
+// 8 (L >> 5) ..+ 8] (SwiGLU: group g = gate rows 16 g .. 16 g + 15, then the same up rows), so a
+// wave's weight load is ONE contiguous KiB.  In the nn.Linear layout the 64 lanes of a load hit 64
+// different 64-byte segments (rows 2 K bytes apart): 4x the L1 tag lookups of a coalesced load, and
+// the L1 -- not HBM -- set the pace (profiles/round4_gemm_counters.md: TA stalled on it 25 M cycles
+// vs 1 M for gemm_wide).
+template <int BM, int NS, int MODE, bool SWROWS, bool PK>
 __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                                          bf16* __restrict__ C, float* __restrict__ P, int M, int N,
                                                          int K, int kts, int nsplit) {
@@ -148,15 +151,16 @@ __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict_
   const char* Ab = reinterpret_cast<const char*>(A) + (size_t)kt0 * RBK * 2;
   i32x4r rsW;   // buffer descriptor of the weight slice: base, stride 0, byte range, raw dword format
   {
-    const uint64_t wa = (uint64_t)(size_t)Wb;
+    const uint64_t wa = (uint64_t)(size_t)(PK ? reinterpret_cast<const char*>(W) : Wb);
     rsW[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)wa);
     rsW[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(wa >> 32) & 0xffff);
-    rsW[2] = __builtin_amdgcn_readfirstlane((int)((long)N * K * 2 - (long)kt0 * RBK * 2));
+    rsW[2] = __builtin_amdgcn_readfirstlane((int)((long)N * K * 2 - (PK ? 0L : (long)kt0 * RBK * 2)));
     rsW[3] = 0x00020000;
   }
   const __amdgpu_buffer_rsrc_t rsA =
       __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)((long)M * K * 2 - (long)kt0 * RBK * 2), 0x00020000);
-  const uint32_t woff = (uint32_t)wrow_of(r) * (uint32_t)(K * 2) + (uint32_t)h * 64;
+  const uint32_t woff = PK ? (uint32_t)(n_t * 4 + wv) * (uint32_t)(K / RBK * 4096) + (uint32_t)lane * 16
+                           : (uint32_t)wrow_of(r) * (uint32_t)(K * 2) + (uint32_t)h * 16;
 
   // LDS-DMA pieces: piece q of wave wv fills slot rows 8 pi .. 8 pi + 7 (pi = AP wv + q), lane ->
   // (row 8 pi + lane / 8, physical chunk lane % 8) <- logical chunk (lane % 8) ^ swz(row)
@@ -168,11 +172,11 @@ __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict_
     offA[q] = (uint32_t)srow * (uint32_t)(K * 2) + (uint32_t)(((lane & 7) ^ ((row >> 1) & 7)) * 16);
   }
   // fragment read offsets (bytes, within a slot) of k-step j: token row r of each 32-row m-frag
-  // (the m-frag is the immediate offset 4096 mf), logical chunk 4 h + j
+  // (the m-frag is the immediate offset 4096 mf), logical chunk 2 j + h
   const uint32_t lds0 = (uint32_t)(size_t)(lds_vptr_r)smem;
   uint32_t foff[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) foff[j] = (uint32_t)(r * 128 + (((4 * h + j) ^ ((r >> 1) & 7)) * 16));
+  for (int j = 0; j < 4; ++j) foff[j] = (uint32_t)(r * 128 + (((2 * j + h) ^ ((r >> 1) & 7)) * 16));
 
   f32x16 acc[MFR];
 #pragma unroll
@@ -182,7 +186,10 @@ __global__ void __launch_bounds__(256, 1) gemm_rw_kernel(const bf16* __restrict_
   bf16x8 wreg[NS][4];
   bf16x8 fs0[MFR], fs1[MFR];
 
-  auto load_w = [&](bf16x8& dst, int t, int j) { rw_wload<NT>(dst, woff + j * 16, rsW, t * (RBK * 2)); };
+  auto load_w = [&](bf16x8& dst, int t, int j) {
+    if constexpr (PK) rw_wload(dst, woff + j * 1024, rsW, (kt0 + t) * 4096);
+    else rw_wload(dst, woff + j * 32, rsW, t * (RBK * 2));
+  };
   auto piece = [&](int slot, int t, int q) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_vptr_r)(smem + slot * SLOT + (wv * AP + q) * 1024), 16,
                                              (int)offA[q], t * (RBK * 2), 0, 0);
@@ -325,8 +332,8 @@ static int rw_default_ns(int bm) { return bm == 256 ? 4 : bm == 128 ? 6 : 8; }
 // mode 0: C = A W^T;  mode 1: SwiGLU, C[M, N/2] = silu(A Wg^T) * (A Wu^T) with W = [Wg; Wu];
 // mode 2: leave split-K partial slabs in ws (no reduce; S > 1 required).
 // variant: bits 0-3 ring slots NS (0 = the row tile's default: 4 / 6 / 8 at 256 / 128 / 64 rows;
-// 256 rows: 3..5, 128: 4 / 6 / 8, 64: 4 / 8), bit 4: weights with the default cache policy (else
-// nontemporal; 256-row tiles only), bits 8-9: row tile override (1 = 64, 2 = 128, 3 = 256).
+// 256 rows: 3..5, 128: 4 / 6 / 8, 64: 4 / 8), bit 4: W is fragment-major packed (see PK), bits
+// 8-9: row tile override (1 = 64, 2 = 128, 3 = 256).
 // Returns the effective number of K slices S.
 int gemm_rw(uintptr_t c, uintptr_t a, uintptr_t w, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream) {
@@ -343,7 +350,7 @@ int gemm_rw(uintptr_t c, uintptr_t a, uintptr_t w, uintptr_t ws, long ws_floats,
   DLLM_HOST_CHECK(bm != 256 || (ns >= 3 && ns <= 5), "ring slots at 256 rows: 3..5");
   DLLM_HOST_CHECK(bm != 128 || ns == 4 || ns == 6 || ns == 8, "ring slots at 128 rows: 4, 6, 8");
   DLLM_HOST_CHECK(bm != 64 || ns == 4 || ns == 8, "ring slots at 64 rows: 4, 8");
-  const bool nt = (variant & 16) == 0 || bm != 256;
+  const bool pk = (variant & 16) != 0;
   const bool swiglu = mode == 1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ktiles = K / RBK;
@@ -354,35 +361,35 @@ int gemm_rw(uintptr_t c, uintptr_t a, uintptr_t w, uintptr_t ws, long ws_floats,
   const int ntiles = swiglu ? (N / 2) / 64 : N / 128;
   const long grid = (long)ntiles * S;
   const int kmode = S == 1 ? (swiglu ? 2 : 0) : 1;
-#define DLLM_RW_GO(BM_, NS_, MODE_, SW_, NT_)                                                               \
-  hipLaunchKernelGGL((gemm_rw_kernel<BM_, NS_, MODE_, SW_, NT_>), dim3((unsigned)grid), dim3(256), 0, s,    \
+#define DLLM_RW_GO(BM_, NS_, MODE_, SW_, PK_)                                                               \
+  hipLaunchKernelGGL((gemm_rw_kernel<BM_, NS_, MODE_, SW_, PK_>), dim3((unsigned)grid), dim3(256), 0, s,    \
                      (const bf16*)a, (const bf16*)w, (bf16*)c, (float*)ws, M, N, K, kts, S)
-#define DLLM_RW_MODES(BM_, NS_, NT_)                                          \
+#define DLLM_RW_MODES1(BM_, NS_, PK_)                                         \
   do {                                                                        \
-    if (kmode == 2) DLLM_RW_GO(BM_, NS_, 2, true, NT_);                       \
-    else if (kmode == 0) DLLM_RW_GO(BM_, NS_, 0, false, NT_);                 \
-    else if (swiglu) DLLM_RW_GO(BM_, NS_, 1, true, NT_);                      \
-    else DLLM_RW_GO(BM_, NS_, 1, false, NT_);                                 \
+    if (kmode == 2) DLLM_RW_GO(BM_, NS_, 2, true, PK_);                       \
+    else if (kmode == 0) DLLM_RW_GO(BM_, NS_, 0, false, PK_);                 \
+    else if (swiglu) DLLM_RW_GO(BM_, NS_, 1, true, PK_);                      \
+    else DLLM_RW_GO(BM_, NS_, 1, false, PK_);                                 \
+  } while (0)
+#define DLLM_RW_MODES(BM_, NS_)                                               \
+  do {                                                                        \
+    if (pk) DLLM_RW_MODES1(BM_, NS_, true);                                   \
+    else DLLM_RW_MODES1(BM_, NS_, false);                                     \
   } while (0)
   if (bm == 256) {
-    if (nt) {
-      if (ns == 3) DLLM_RW_MODES(256, 3, true);
-      else if (ns == 5) DLLM_RW_MODES(256, 5, true);
-      else DLLM_RW_MODES(256, 4, true);
-    } else {
-      if (ns == 3) DLLM_RW_MODES(256, 3, false);
-      else if (ns == 5) DLLM_RW_MODES(256, 5, false);
-      else DLLM_RW_MODES(256, 4, false);
-    }
+    if (ns == 3) DLLM_RW_MODES(256, 3);
+    else if (ns == 5) DLLM_RW_MODES(256, 5);
+    else DLLM_RW_MODES(256, 4);
   } else if (bm == 128) {
-    if (ns == 4) DLLM_RW_MODES(128, 4, true);
-    else if (ns == 8) DLLM_RW_MODES(128, 8, true);
-    else DLLM_RW_MODES(128, 6, true);
+    if (ns == 4) DLLM_RW_MODES(128, 4);
+    else if (ns == 8) DLLM_RW_MODES(128, 8);
+    else DLLM_RW_MODES(128, 6);
   } else {
-    if (ns == 4) DLLM_RW_MODES(64, 4, true);
-    else DLLM_RW_MODES(64, 8, true);
+    if (ns == 4) DLLM_RW_MODES(64, 4);
+    else DLLM_RW_MODES(64, 8);
   }
 #undef DLLM_RW_MODES
+#undef DLLM_RW_MODES1
 #undef DLLM_RW_GO
   DLLM_HIP_CHECK(hipGetLastError());
   if (S == 1 || mode == 2) return S;

@@ -207,14 +207,29 @@ def rw_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 25
     return max(1, min(round(target_wgs / max(1, tiles)), (k // 64) // 4, 16))
 
 
+def pack_rw(w: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
+    """``w`` [N, K] (nn.Linear layout; SwiGLU: [Wg; Wu]) -> the fragment-major layout gemm_rw's
+    packed form streams (csrc/kernels/gemm_rw.hip, PK): for 32-row group g, 64-deep K-tile t,
+    16-deep k-step j and lane L, 8 elements W[32 g + L % 32][64 t + 16 j + 8 (L // 32) ..+ 8] -- one
+    contiguous KiB per (g, t, j), the MFMA A fragment of a wave.  SwiGLU groups hold gate rows
+    16 g .. 16 g + 15 then the same up rows.  Same shape and dtype; a different element order."""
+    n, k = w.shape
+    if n % 32 or k % 64 or (swiglu and n % 64):
+        raise ValueError(f"pack_rw: N {n} % 32 (SwiGLU: % 64), K {k} % 64")
+    if swiglu:   # [Wg; Wu] -> per 16-row output group: 16 gate rows, then its 16 up rows
+        w = w.view(2, n // 32, 16, k).transpose(0, 1).reshape(n, k)
+    # (g, r, t, j, h, e) -> (g, t, j, h, r, e): lane L = 32 h + r
+    return w.reshape(n // 32, 32, k // 64, 4, 2, 8).permute(0, 2, 3, 4, 1, 5).contiguous().view(n, k)
+
+
 def linear_rw(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = False, defer: bool = False,
-              variant: int = 0):
+              variant: int = 0, packed: bool = False):
     """Register-weight decode GEMM (csrc/kernels/gemm_rw.hip), M <= 256: weights stream straight
     into VGPRs as MFMA fragments, activations through an LDS-DMA ring; fused SwiGLU (``w`` =
     [Wg; Wu]) and split-K.  ``defer``: may return a :class:`SplitKPartial` (no SwiGLU).
-    ``variant``: bits 0-3 ring slots (0 = the row tile's default), bit 4 weights with the default
-    cache policy (256-row tiles), bits 8-9 row tile override (1 = 64, 2 = 128, 3 = 256 rows; the
-    default is the smallest that holds M)."""
+    ``packed``: ``w`` is :func:`pack_rw`'s fragment-major layout (coalesced weight loads).
+    ``variant``: bits 0-3 ring slots (0 = the row tile's default), bits 8-9 row tile override
+    (1 = 64, 2 = 128, 3 = 256 rows; the default is the smallest that holds M)."""
     k = x.shape[-1]
     n = w.shape[0]
     m = x.numel() // k
@@ -227,6 +242,7 @@ def linear_rw(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = 
     if s > 1 and s * m * n > ws.numel():
         s = max(1, ws.numel() // (m * n))
     stream = torch.cuda.current_stream().cuda_stream
+    variant = (variant & ~16) | (16 if packed else 0)
     if defer and not swiglu and s > 1:
         se = _ext.kernels().gemm_rw(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, variant,
                                     stream)

@@ -103,7 +103,10 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
         extra["stage_busy_frac"] = busy
         kinds = sorted({i["transport"] for i in info})
         extra["transport"] = kinds[0] if len(kinds) == 1 else kinds
-        # every native RCCL communicator appears on both of its ranks: count them once
+        # every native RCCL communicator appears on both of its ranks: count them once.  The
+        # pipeline data plane is built from 2-rank EDGE communicators (stage s <-> s + 1, plus
+        # the ids ring closure last -> first), so rccl_comm_nranks is [2] at any N -- the number
+        # of edges (rccl_comms) and of ranks on them (rccl_ranks) is what grows with N
         extra["rccl_comms"] = sum(len(i["rccl_comm_ranks"]) for i in info) // 2
         extra["rccl_ranks"] = sum(1 for i in info if i["rccl_comm_ranks"])
         extra["rccl_comm_nranks"] = sorted({n for i in info for n in i["rccl_comm_ranks"]})

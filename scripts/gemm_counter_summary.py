@@ -19,7 +19,7 @@ def short(n):
     m = re.match(r"_ZN4dllm(\d+)", n)
     if m:
         ln, rest = int(m.group(1)), n[m.end():]
-        targs = re.findall(r"Li(\d+)E", rest[ln:ln + 60])
+        targs = re.findall(r"L[ib](\d+)E", rest[ln:ln + 60])
         return rest[:ln] + ("<" + ",".join(targs) + ">" if targs else "")
     return n[:48]
 

@@ -50,13 +50,21 @@ def test_rw_swiglu(cuda, m, inter, k, splits, nsi):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("variant", [4, 16 | 4])
-def test_rw_cache_policy_bit_exact(cuda, variant):
-    """The nontemporal and default-policy weight loads produce identical results."""
-    x, w = _bf(256, 4096), _bf(6144, 4096, scale=0.05)
-    a = gemm.linear_rw(x, w, splits=5, variant=4)
-    b = gemm.linear_rw(x, w, splits=5, variant=variant)
+@pytest.mark.parametrize("m", [1, 100, 256])
+@pytest.mark.parametrize("n,k,splits,swiglu", [(6144, 4096, 5, False), (4096, 14336, 8, False), (28672, 4096, 1, True),
+                                               (1024, 512, 1, True), (384, 192, 2, False), (1024, 1024, 2, True)])
+@pytest.mark.parametrize("nsi", [0, 1])
+def test_rw_packed_bit_exact(cuda, m, n, k, splits, swiglu, nsi):
+    """Fragment-major packed weights (gemm.pack_rw) give the same bits as the nn.Linear layout:
+    the same fragments in the same registers, only the load addresses differ."""
+    ns = _ns(m, nsi)
+    torch.manual_seed(m + n + k + ns)
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    a = gemm.linear_rw(x, w, splits=splits, swiglu=swiglu, variant=ns)
+    b = gemm.linear_rw(x, gemm.pack_rw(w, swiglu), splits=splits, swiglu=swiglu, variant=ns, packed=True)
     assert torch.equal(a, b)
+    if not swiglu:
+        torch.testing.assert_close(b.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("m,n,k", [(256, 4096, 14336), (200, 4096, 4096), (64, 1024, 8192)])

@@ -35,7 +35,7 @@ def test_rw_kernels_have_no_async_load_hazards(rw_asm):
     res = subprocess.run([sys.executable, str(ROOT / "scripts" / "check_async_loads.py"), str(rw_asm)],
                          check=True, capture_output=True, text=True).stdout
     lines = [l for l in res.splitlines() if "hazards" in l]
-    assert len(lines) == 44, res                 # 256 rows: 3 rings x 4 modes x 2 policies; 128: 3 x 4; 64: 2 x 4
+    assert len(lines) == 64, res                 # (3 + 3 + 2 ring depths) x 4 modes x 2 weight layouts
     for l in lines:
         assert re.search(r"hazards 0 ", l), res
         waits = [int(x) for x in re.findall(r"\d+", l.split("vmcnt", 1)[1])]
