@@ -230,67 +230,16 @@ __device__ __forceinline__ void rope_rotate(bf16x8 (&f)[D / 32], const float* cs
   }
 }
 
-// SEP (fused only): the KV append runs in its own workgroups -- the grid's last x index -- instead
-// of inside the attention waves, so no attention wave ends waiting for its cache stores to be
-// acknowledged.  An append wave re-derives the new k (RoPE) and v from the qkv row, writes the K
-// row, and rewrites the new key's whole V^T group tile (2 KiB: 16 full lines, the other 7 keys
-// read back and stored unchanged).  Attention waves that read that tile concurrently patch the
-// new key in registers as before: every byte they may observe either way is the same.
-template <int D, int PARTS>
-__device__ __forceinline__ void decode_append(bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
-                                              const int32_t* __restrict__ seq_lens, const RopeArgs& ra, int b,
-                                              int kvh, int hq, int hkv, int lane) {
-  const int r = lane & 15, g = lane >> 4;
-  if (seq_lens[b] <= 0) return;
-  const int width = (hq + 2 * hkv) * D;
-  const int ko = (hq + kvh) * D, vo = (hq + hkv + kvh) * D;
-  bf16x8 kn[D / 32];
-#pragma unroll
-  for (int ks = 0; ks < D / 32; ++ks) kn[ks] = qkv_load8<PARTS>(ra, b, width, ko + ks * 32 + 8 * g);
-  // lane (r, g) rewrites V^T rows d = (2g + i) * 16 + r of the group tile (i = 0, 1; D = 128) --
-  // D / 64 rows per lane
-  constexpr int VR = D / 64;
-  bf16 vn[VR];
-#pragma unroll
-  for (int i = 0; i < VR; ++i) vn[i] = qkv_load1<PARTS>(ra, b, width, vo + (VR * g + i) * 16 + r);
-  const int slot = ra.slots[b];
-  const int blk = slot / kBS, off = slot % kBS;
-  const size_t base = ((size_t)blk * hkv + kvh) * kBS * D;
-  bf16* tile = v_cache + base + (size_t)(off >> 3) * 8 * D;
-  bf16x8 rows[VR];
-#pragma unroll
-  for (int i = 0; i < VR; ++i) rows[i] = *reinterpret_cast<const bf16x8*>(tile + ((VR * g + i) * 16 + r) * 8);
-  const float* cs = ra.cos_sin ? ra.cos_sin + (size_t)ra.positions[b] * D : nullptr;
-  rope_rotate<D, true>(kn, cs, g);
-  if (r == 0) {
-#pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks)
-      *reinterpret_cast<bf16x8*>(k_cache + base + (size_t)krow32(off) * D + ks * 32 + 8 * g) = kn[ks];
-  }
-#pragma unroll
-  for (int i = 0; i < VR; ++i) {
-    rows[i][off & 7] = vn[i];
-    *reinterpret_cast<bf16x8*>(tile + ((VR * g + i) * 16 + r) * 8) = rows[i];
-  }
-}
-
-template <int D, int WPB, bool FUSED, int PARTS = 0, bool SEP = false>
+template <int D, int WPB, bool FUSED, int PARTS = 0>
 __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg: min waves per SIMD
     bf16* __restrict__ out, const bf16* __restrict__ q, bf16* __restrict__ k_cache,
     bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
     const int32_t* __restrict__ seq_lens, float* __restrict__ part_o, float* __restrict__ part_ml,
     int hq, int hkv, int max_blocks, int split_len, float scale_log2, RopeArgs ra) {
-  static_assert(!SEP || (FUSED && kVFullLines), "separate append: fused decode, whole-line V^T layout");
   const int split = blockIdx.x, b = blockIdx.z;
   const int lane = threadIdx.x & 63;
   const int kvh = blockIdx.y * WPB + (threadIdx.x >> 6);
-  const int nsplit = SEP ? gridDim.x - 1 : gridDim.x;
-  if constexpr (SEP) {
-    if (split == nsplit) {                            // the append workgroup of (kv heads, sequence)
-      decode_append<D, PARTS>(k_cache, v_cache, seq_lens, ra, b, kvh, hq, hkv, lane);
-      return;
-    }
-  }
+  const int nsplit = gridDim.x;
   const int G = hq / hkv;
   const int r = lane & 15, g = lane >> 4;
   const int ctx = seq_lens[b];
@@ -371,7 +320,7 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
       // [D][8] V^T tile (2 KiB, 16 full 128-B lines) with the new key patched in -- no partially
       // written lines to read-modify-write.  This is the sequence's last chunk: no KV load follows
       // whose vmcnt wait would include these stores.
-      if (vcol && owns_new && !SEP) {
+      if (vcol && owns_new) {
 #pragma unroll
         for (int dt = 0; dt < D / 16; ++dt)
           *reinterpret_cast<bf16x8*>(v_cache + cbase + g * 8 * D + (dt * 16 + r) * 8) = c.v[dt];
@@ -414,7 +363,7 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     }
   }
   finish_rope();   // no cache chunk in this split
-  if (owns_new && !SEP) {
+  if (owns_new) {
     // append k (row krow32(off)) and v (its [4][D][8] V^T slots) to the paged cache only now, after the
     // last KV load: stores count in vmcnt in issue order, so stores issued before the KV stream
     // made every later chunk wait for their (scattered 2-byte V^T) write acknowledgements
@@ -778,7 +727,7 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
 static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache, uintptr_t block_tables,
                           uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml, int batch, int hq, int hkv, int d,
                           int block_size, int max_blocks, int num_splits, int split_len, float scale, RopeArgs ra,
-                          bool fused, uintptr_t stream, int flags = 0) {
+                          bool fused, uintptr_t stream) {
   DLLM_HOST_CHECK(block_size == kBS, "paged attention requires block_size 32");
   DLLM_HOST_CHECK(hq % hkv == 0 && hq / hkv <= 16, "GQA group size must be <= 16");
   DLLM_HOST_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
@@ -793,9 +742,7 @@ static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr
   const float sl2 = scale * 1.4426950408889634f;
   // one wave per kv head; pack up to 4 heads (independent waves) per workgroup
   const int wpb = hkv % 4 == 0 ? 4 : hkv % 2 == 0 ? 2 : 1;
-  // flags bit 0: the KV append in its own workgroups (SEP; fused, head_dim 128 only)
-  const bool sep = fused && (flags & 1) && d == 128;
-  dim3 grid(num_splits + (sep ? 1 : 0), hkv / wpb, batch);
+  dim3 grid(num_splits, hkv / wpb, batch);
   auto go = [&](auto kern, int threads) {
     hipLaunchKernelGGL(kern, grid, dim3(threads), 0, s, (bf16*)out, (const bf16*)q, (bf16*)k_cache, (bf16*)v_cache,
                        (const int32_t*)block_tables, (const int32_t*)seq_lens, (float*)part_o, (float*)part_ml, hq,
@@ -807,23 +754,8 @@ static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr
     else if (wpb == 2) go(attn_decode_kernel<DD, 2, FF, PP>, 128);    \
     else go(attn_decode_kernel<DD, 1, FF, PP>, 64);                   \
   } while (0)
-#define DLLM_DECS(PP)                                                         \
-  do {                                                                        \
-    if (wpb == 4) go(attn_decode_kernel<128, 4, true, PP, true>, 256);        \
-    else if (wpb == 2) go(attn_decode_kernel<128, 2, true, PP, true>, 128);   \
-    else go(attn_decode_kernel<128, 1, true, PP, true>, 64);                  \
-  } while (0)
   const bool parts = fused && ra.part != nullptr;
-  if (sep) {
-    if (parts) {
-      if (ra.nparts == 5) DLLM_DECS(5);
-      else if (ra.nparts == 4) DLLM_DECS(4);
-      else if (ra.nparts == 8) DLLM_DECS(8);
-      else DLLM_DECS(-1);
-    } else {
-      DLLM_DECS(0);
-    }
-  } else if (d == 128) {
+  if (d == 128) {
     if (parts) {
       if (ra.nparts == 5) DLLM_DEC(128, true, 5);
       else if (ra.nparts == 4) DLLM_DEC(128, true, 4);
@@ -834,7 +766,6 @@ static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr
     if (parts) DLLM_DEC(64, true, -1); else if (fused) DLLM_DEC(64, true, 0); else DLLM_DEC(64, false, 0);
   }
 #undef DLLM_DEC
-#undef DLLM_DECS
   DLLM_HIP_CHECK(hipGetLastError());
   if (num_splits > 1) {
     if (d == 128)
@@ -860,11 +791,11 @@ void paged_attention_decode_rope(uintptr_t out, uintptr_t qkv, uintptr_t positio
                                  uintptr_t k_cache, uintptr_t v_cache, uintptr_t block_tables, uintptr_t seq_lens,
                                  uintptr_t part_o, uintptr_t part_ml, int batch, int hq, int hkv, int d,
                                  int block_size, int max_blocks, int num_splits, int split_len, float scale,
-                                 uintptr_t qkv_part, int qkv_nparts, long qkv_slab, uintptr_t stream, int flags) {
+                                 uintptr_t qkv_part, int qkv_nparts, long qkv_slab, uintptr_t stream) {
   RopeArgs ra{(const bf16*)qkv, (const int32_t*)positions, (const float*)cos_sin, (const int32_t*)slots,
               (const float*)qkv_part, qkv_nparts, qkv_slab};
   decode_launch(out, 0, k_cache, v_cache, block_tables, seq_lens, part_o, part_ml, batch, hq, hkv, d, block_size,
-                max_blocks, num_splits, split_len, scale, ra, true, stream, flags);
+                max_blocks, num_splits, split_len, scale, ra, true, stream);
 }
 
 template <int D>

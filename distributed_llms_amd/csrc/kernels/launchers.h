@@ -63,7 +63,7 @@ void paged_attention_decode_rope(uintptr_t out, uintptr_t qkv, uintptr_t positio
                                  uintptr_t k_cache, uintptr_t v_cache, uintptr_t block_tables, uintptr_t seq_lens,
                                  uintptr_t part_o, uintptr_t part_ml, int batch, int hq, int hkv, int d,
                                  int block_size, int max_blocks, int num_splits, int split_len, float scale,
-                                 uintptr_t qkv_part, int qkv_nparts, long qkv_slab, uintptr_t stream, int flags);
+                                 uintptr_t qkv_part, int qkv_nparts, long qkv_slab, uintptr_t stream);
 void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
                              uintptr_t block_tables, uintptr_t cu_seqlens_q, uintptr_t seq_lens, int batch,
                              int hq, int hkv, int d, int block_size, int max_blocks, int max_q_len, float scale,

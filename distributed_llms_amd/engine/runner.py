@@ -12,7 +12,6 @@ import torch
 from .. import knobs
 from ..config import EngineConfig, ModelConfig, pipeline_slots
 from ..models.stage import KVCache, ModelStage
-from ..ops.tuning import enable_tuned_gemms
 from ..utils.tracing import get_tracer
 from .batch import HostBatch, to_device_meta
 from .graphs import DecodeGraphRunner
@@ -58,8 +57,6 @@ class StageRunner:
         knobs.reset()
         if ecfg.kernel_knobs:
             knobs.update(ecfg.kernel_knobs)
-        if stage.device.type == "cuda":
-            enable_tuned_gemms()          # before any graph capture fixes the GEMM solutions
         self.block_size = ecfg.kv_block_size
         nb = num_blocks or plan_kv_blocks(stage.cfg, stage.num_layers, ecfg, stage.device, stage.hkv)
         stage.allocate_kv(nb, self.block_size)

@@ -13,8 +13,7 @@ captured before an update keep the dispatch they were captured with).
 
 Environment variables the package still reads (all documented in README "Environment"):
 DLLM_KNOBS, DLLM_TRACE, DLLM_ROCTX, DLLM_JSON_LOGS, DLLM_DEVICE, DLLM_DIST_ADDR, DLLM_TRANSPORT,
-DLLM_SHARE_GPU, DLLM_DATA_BACKEND, DLLM_PP_UNITS, DLLM_PP_FINE, DLLM_OFFLOAD_ARCH, DLLM_PART_TYPE,
-DLLM_TUNABLEOP_FILE.
+DLLM_SHARE_GPU, DLLM_DATA_BACKEND, DLLM_PP_UNITS, DLLM_PP_FINE, DLLM_OFFLOAD_ARCH, DLLM_PART_TYPE.
 """
 from __future__ import annotations
 
@@ -55,16 +54,16 @@ class Knobs:
     sq_min_m: int = 225
     sq_split: bool = False
     sq_variant: int = 4
-    # prefill-sized GEMMs on gemm_pp.hip (256 x 256 tiles, schedule 2, grouped tile order) from this
-    # M instead of hipBLASLt; 0 = off.  gate|up with the SwiGLU fused into the epilogue:
-    # 1444 vs 1382 TFLOP/s for hipBLASLt + silu_mul at T = 32768 (profiles/round3_gemm_experiments.md);
-    # the plain projections still trail hipBLASLt (1434-1448 vs 1546-1631), so off
-    pp_swiglu_min_m: int = 2048
-    pp_proj_min_m: int = 0
-    # the prefill GEMMs above (pp_swiglu_min_m / pp_proj_min_m) on the persistent form of schedule
-    # 2 (gemm_pf: one workgroup per CU, the LDS-DMA pipeline continuous across output tiles, the
-    # epilogue stored straight from the accumulators) instead of one workgroup per tile
-    pp_persistent: bool = False
+    # prefill-sized GEMMs (above the decode kernels' ranges) on the hand-written 256 x 256 kernels
+    # instead of hipBLASLt, from this M (0 = hipBLASLt): the persistent schedule-2 kernel gemm_pf
+    # (pp_persistent; else gemm_pp schedule 2).  At T = 32768 (profiles/round4_gemm_counters.md):
+    # gate|up + SwiGLU 1396 TFLOP/s vs 1345 for hipBLASLt + silu_mul; qkv / o / down 1415-1474 vs
+    # hipBLASLt's 1511-1591.  In-engine (Llama-3-8B B = 256, two interleaved pairs): every prefill
+    # GEMM hand-written 27,532 / 27,513 tok/s vs 27,792 / 27,753 with hipBLASLt on qkv / o / down
+    # (-0.9 %) -- taken, so that no vendor GEMM runs in the forward path
+    pp_swiglu_min_m: int = 257
+    pp_proj_min_m: int = 257
+    pp_persistent: bool = True
     # decode LM head (N > 65536) at pp_head_min_m <= M <= 256 on gemm_pp schedule 2 with nontemporal
     # weights: 230 vs 265 us for gemm_sq at M = 256 (Llama-3-8B); 0 = off
     pp_head_min_m: int = 225
@@ -73,9 +72,6 @@ class Knobs:
     prefill_attn: int = 4             # prefill kernel version 1..5 (4: LDS-shared K/V tiles)
     # ---- model / engine
     fused_rope: bool = True           # decode: RoPE + KV append fused into attention
-    # fused decode: the KV append in workgroups of its own (no attention wave waits on its cache
-    # stores) instead of inside the attention waves
-    attn_append_sep: bool = False
     # split-K qkv partials summed inside the fused RoPE + attention kernel (no splitk_reduce launch):
     # +0.2-0.6 % tok/s in 4 of 4 interleaved in-engine pairs on two boxes (round 3,
     # profiles/round3_gemm_experiments.md; a round-2 build measured -3 %)
@@ -92,8 +88,6 @@ class Knobs:
     # ---- FP8 W8A8 (ops/quant.py)
     fp8_bm128: bool = True
     fp8_group_m: int = 4096
-    # ---- hipBLASLt (ops/tuning.py)
-    tunableop: bool = True            # load the shipped TunableOp solution table
 
 
 K = Knobs()

@@ -325,7 +325,7 @@ def paged_attention_decode_rope(qkv, positions, cos_sin, k_cache, v_cache, slot_
         slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), seq_lens.data_ptr(),
         po, pml, b, hq, hkv, d, bs, max_blocks, splits, split_len, float(scale),
         0 if part is None else part.ws.data_ptr(), 0 if part is None else part.splits,
-        0 if part is None else part.m * part.n, _stream(), 1 if knobs.K.attn_append_sep else 0)
+        0 if part is None else part.m * part.n, _stream())
     return out
 
 

@@ -14,11 +14,12 @@ the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..
   with the 256 x 256 tile (gemm_sq.hip) taking unsplit grids at 225 <= M <= 256 (70B gate|up);
 * the decode LM head at 225 <= M <= 256: gemm_pp.hip schedule 2 with nontemporal weights
   (knobs.pp_head_min_m);
-* prefill gate|up (M >= knobs.pp_swiglu_min_m): gemm_pp.hip, the 4-wave 256 x 256-tile kernel
-  (schedule 2) with the SwiGLU fused into its epilogue -- faster than hipBLASLt + silu_mul
-  (profiles/round3_gemm_experiments.md);
-* everything else (prefill qkv / o / down, M above the cutovers): hipBLASLt via torch (TunableOp
-  table in tuning/), chosen purely by shape (knobs.pp_proj_min_m moves them to gemm_pp).
+* prefill (M >= knobs.pp_swiglu_min_m / pp_proj_min_m, above the decode ranges): the 4-wave
+  256 x 256-tile schedule-2 kernel in its persistent form (gemm_pf in gemm_pp.hip, knobs.pp_persistent)
+  -- gate|up with the SwiGLU fused into its epilogue, qkv / o / down plain
+  (profiles/round4_gemm_counters.md);
+* what none of them takes (a bias, N not a multiple of 256, fp32 on CPU, operands >= 4 GiB):
+  torch's F.linear.
 
 The role is inferred from the shape: "down" = K >= 8192 and K > N, so the square / widening
 K = 8192 projections of 70B-class models (qkv 8192 -> 10240, o 8192 -> 8192) stay "proj".
@@ -376,7 +377,7 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Te
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
     if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):
-        if knobs.K.pp_persistent and m * n * 2 < (1 << 31):
+        if knobs.K.pp_persistent and m * (n // 2) * 2 < (1 << 31):
             return linear_pf(x, w_gate_up, swiglu=True)
         return linear_pp(x, w_gate_up, splits=1, swiglu=True, variant=PP_PREFILL_VARIANT)
     return None

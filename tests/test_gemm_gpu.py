@@ -43,9 +43,10 @@ def test_small_m_swiglu(cuda, m, inter, k):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
-def test_large_m_uses_library_gemm(cuda):
+def test_large_m_uses_hand_written_prefill_gemm(cuda):
     x, w = _bf(300, 512), _bf(256, 512, scale=0.05)
     assert not gemm._use_wide(300, 256, 512, x, w)
+    assert gemm._use_pp(300, 256, 512, x, w, gemm.knobs.K.pp_proj_min_m)
     y = ops.linear(x, w)
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
 
@@ -90,19 +91,6 @@ def test_deferred_splitk_fused_add_rms_norm_bit_exact(cuda, m, n, k):
     torch.testing.assert_close(h.float(), ref.linear(x.float(), w.float()), atol=2e-2, rtol=2e-2)
     yr, rr = ref.fused_add_rms_norm(h.float(), res0.float(), g.float(), 1e-5)
     torch.testing.assert_close(y1.float(), yr, atol=3e-2, rtol=3e-2)
-
-
-def test_tuned_gemm_table_loads_and_matches(cuda):
-    """The in-tree TunableOp table loads read-only and its solutions stay numerically correct."""
-    import torch.nn.functional as F
-    from distributed_llms_amd.ops import tuning
-    assert os.path.exists(tuning.TUNED_CSV)
-    assert tuning.enable_tuned_gemms()
-    assert torch.cuda.tunable.is_enabled() and not torch.cuda.tunable.tuning_is_enabled()
-    assert len(torch.cuda.tunable.get_results()) > 0
-    x = (torch.randn(256, 4096, device="cuda") * 0.5).to(torch.bfloat16)
-    w = (torch.randn(28672, 4096, device="cuda") * 0.02).to(torch.bfloat16)
-    torch.testing.assert_close(F.linear(x, w).float(), x.float() @ w.float().T, atol=3e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("m", [1, 100, 128, 129, 256, 384, 512])

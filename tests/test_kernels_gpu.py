@@ -201,33 +201,3 @@ def test_decode_rope_consumes_splitk_qkv_bit_exact(cuda, b):
     torch.testing.assert_close(o1, o2, atol=0, rtol=0)
     torch.testing.assert_close(k1, k2, atol=0, rtol=0)
     torch.testing.assert_close(v1, v2, atol=0, rtol=0)
-
-
-@pytest.mark.parametrize("lens", [[1], [7, 33, 100], [640, 5, 2049, 32], [int(x) for x in range(60, 316)]])
-@pytest.mark.parametrize("split_k", [False, True])
-def test_decode_append_in_own_workgroups_bit_exact(cuda, monkeypatch, lens, split_k):
-    """knobs.attn_append_sep: the KV append runs in workgroups of its own (the grid's last x
-    index) -- output and both caches are bit-identical to the in-wave append, with bf16 qkv and
-    with split-K qkv slabs, one split and several (long contexts)."""
-    from distributed_llms_amd import knobs
-    from distributed_llms_amd.ops import gemm
-    hq, hkv, d = 32, 8, 128
-    b = len(lens)
-    k, v, bt = _fill_paged(lens, hkv, d)
-    sl = torch.tensor(lens, dtype=torch.int32, device="cuda")
-    pos = sl - 1
-    slots = torch.stack([bt[i, (n - 1) // 32] * 32 + (n - 1) % 32 for i, n in enumerate(lens)]).to(torch.int32)
-    cs = ref.rope_cos_sin(d, 4096, 500000.0, device="cuda")
-    if split_k:
-        qkv = gemm.linear_wide(_bf(b, 4096), _bf((hq + 2 * hkv) * d, 4096, scale=0.02), splits=5, defer=True)
-        assert isinstance(qkv, gemm.SplitKPartial)
-    else:
-        qkv = _bf(b, (hq + 2 * hkv) * d)
-    outs = []
-    for sep in (False, True):
-        monkeypatch.setattr(knobs.K, "attn_append_sep", sep)
-        k1, v1 = k.clone(), v.clone()
-        o = ops.paged_attention_decode_rope(qkv, pos, cs, k1, v1, slots, bt, sl, hq, hkv, d, 1 / math.sqrt(d))
-        outs.append((o, k1, v1))
-    (o1, k1, v1), (o2, k2, v2) = outs
-    assert torch.equal(o1, o2) and torch.equal(k1, k2) and torch.equal(v1, v2)

@@ -108,15 +108,19 @@ def test_knobs_move_the_cutovers_and_reject_unknown_names():
     assert knobs.K.defer_qkv is False and knobs.changed()["defer_qkv"] is False
 
 
-def test_prefill_gate_up_goes_to_gemm_pp():
-    """Prefill gate|up (SwiGLU) runs on gemm_pp's schedule 2 from knobs.pp_swiglu_min_m; the other
-    prefill projections stay on hipBLASLt (pp_proj_min_m = 0)."""
+def test_prefill_gemms_go_to_hand_written_kernels():
+    """Every prefill projection above the decode ranges runs on the persistent schedule-2 kernel
+    (gemm_pf): gate|up with the SwiGLU from knobs.pp_swiglu_min_m, qkv / o / down from
+    pp_proj_min_m -- hipBLASLt only for shapes none of the kernels takes (N % 256, a bias)."""
     from distributed_llms_amd import knobs
     x, w = _xw(32768, 28672, 4096)
-    assert gemm._use_pp(32768, 28672, 4096, x, w, knobs.K.pp_swiglu_min_m)
-    assert not gemm._use_pp(1024, 28672, 4096, x, w, knobs.K.pp_swiglu_min_m)
-    assert not gemm._use_pp(32768, 6144, 4096, x, w, knobs.K.pp_proj_min_m)
-    assert not gemm._use_pp(32768, 28672 + 128, 4096, x, w, knobs.K.pp_swiglu_min_m)   # N % 256
+    kn = knobs.K
+    assert kn.pp_persistent and kn.pp_swiglu_min_m <= 257 and kn.pp_proj_min_m <= 257
+    assert gemm._use_pp(32768, 28672, 4096, x, w, kn.pp_swiglu_min_m)
+    assert gemm._use_pp(1024, 28672, 4096, x, w, kn.pp_swiglu_min_m)
+    assert gemm._use_pp(32768, 6144, 4096, x, w, kn.pp_proj_min_m)
+    assert gemm._use_pp(32768, 4096, 14336, x, w, kn.pp_proj_min_m)
+    assert not gemm._use_pp(32768, 28672 + 128, 4096, x, w, kn.pp_swiglu_min_m)   # N % 256
     knobs.update(pp_swiglu_min_m=0)
     assert not gemm._use_pp(32768, 28672, 4096, x, w, knobs.K.pp_swiglu_min_m)
 
