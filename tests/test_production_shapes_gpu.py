@@ -167,7 +167,7 @@ def _run(model: str, layers: int, prompt_len: int, decode_steps: int, max_rel: f
 @pytest.mark.slow
 def test_llama3_8b_dims_b256_prefill_and_graph_decode_vs_fp32(cuda):
     """4 layers, 16 graph-replayed decode steps."""
-    _run("llama3-8b", layers=4, prompt_len=128, decode_steps=16, max_rel=0.12, mean_rel=0.015)
+    _run("llama3-8b", layers=4, prompt_len=128, decode_steps=16, max_rel=0.15, mean_rel=0.02)
 
 
 @pytest.mark.slow
@@ -175,9 +175,9 @@ def test_llama3_70b_dims_layer_b256_vs_fp32(cuda):
     """One Llama-3-70B layer (H 8192, I 28672, 64 / 8 heads) through the default dispatch: the
     K = 8192 qkv / o projections ("proj" rule: N >= K, not the down-projection path), the 57344 x
     8192 gate|up, the 8192 x 28672 down, and the 128,256-row LM head at H = 8192."""
-    _run("llama3-70b", layers=1, prompt_len=64, decode_steps=4, max_rel=0.12, mean_rel=0.015)
+    _run("llama3-70b", layers=1, prompt_len=64, decode_steps=4, max_rel=0.1, mean_rel=0.013)
 
 
 @pytest.mark.slow
 def test_mixtral_dims_moe_layer_b256_vs_fp32(cuda):
-    _run("mixtral-8x7b", layers=1, prompt_len=16, decode_steps=3, max_rel=0.12, mean_rel=0.015)
+    _run("mixtral-8x7b", layers=1, prompt_len=16, decode_steps=3, max_rel=0.15, mean_rel=0.02)
