@@ -1,6 +1,7 @@
 """GEMM kernels for rocprofv3 counter passes (scripts/gpu_gemm_counters.sh), a few dispatches
-each.  GCTR=decode: the decode MLP gate|up (M = 256, SwiGLU) on gemm_wide and on gemm_rw (default
-and nontemporal weight policy), the o projection (split-K) on both.  GCTR=prefill: a prefill
+each.  GCTR=decode: the decode MLP gate|up (M = 256, SwiGLU) and the o projection (split-K) on
+gemm_wide.  (The round-4 gemm_rw rows of profiles/round4_gemm_counters.md came from the same
+script with that kernel in the tree.)  GCTR=prefill: a prefill
 projection (T = 8192, N = 6144, K = 4096) on gemm_pf, gemm_pp schedule 2 and hipBLASLt."""
 import os
 import sys
@@ -23,10 +24,7 @@ def main():
         wo = [bf(4096, 4096, sc=0.02) for _ in range(4)]
         for i in range(4):
             gemm.linear_wide(xd, wgu[i % 4], swiglu=True)
-            gemm.linear_rw(xd, wgu[(i + 1) % 4], swiglu=True, variant=16 | 4)
-            gemm.linear_rw(xd, wgu[(i + 2) % 4], swiglu=True, variant=4)
             gemm.linear_wide(xd, wo[i % 4], defer=True)
-            gemm.linear_rw(xd, wo[(i + 1) % 4], defer=True, variant=16 | 4)
     else:
         x, w = bf(8192, 4096), bf(6144, 4096, sc=0.02)
         for _ in range(4):

@@ -29,7 +29,6 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("moe_wide_gemm_fp8", &dllm::moe_wide_gemm_fp8);
   m.def("splitk_add_rms_norm_q8", &dllm::splitk_add_rms_norm_q8);
   m.def("gemm_sq", &dllm::gemm_sq);
-  m.def("gemm_rw", &dllm::gemm_rw);
   m.def("gemm_pp_moe", &dllm::gemm_pp_moe);
   m.def("gemm_pp", &dllm::gemm_pp);
   m.def("gemm_pf", &dllm::gemm_pf);

@@ -41,13 +41,6 @@ class Knobs:
     wide_target_wgs: int = 256        # split-K: about one workgroup per CU
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
-    # register-weight decode GEMM (gemm_rw.hip: weight fragments straight into VGPRs, activations
-    # through an LDS-DMA ring) for rw_min_m <= M <= 256: roles ("all", "none", or a comma list of
-    # gate_up / down / proj / head) -- ahead of gemm_sq / gemm_wide / the gemm_pp LM head; rw_ns:
-    # ring slots (K-tiles in flight)
-    rw: str = "none"
-    rw_min_m: int = 1
-    rw_ns: int = 0                    # 0: the row tile's default (4 / 6 / 8 at 256 / 128 / 64 rows)
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
     # from this M up to 256, unsplit grids only unless sq_split
     sq: str = "all"

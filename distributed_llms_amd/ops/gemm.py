@@ -3,8 +3,6 @@
 Decode-sized M goes to hand-written gfx950 kernels, per projection role (cutovers measured in
 the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..knobs`):
 
-* register-weight kernel (gemm_rw.hip, knobs.rw roles): weight fragments stream straight into
-  VGPRs, activations through an LDS-DMA ring, split-K / SwiGLU like gemm_wide, M <= 256;
 * wide-M kernel (gemm_wide.hip: 64/128/192/256-row x 128 tiles, 3-stage LDS-DMA pipeline,
   split-K over workgroups) for every decode M:
   - gate|up (SwiGLU fused into the epilogue): M <= knobs.wide_gate_up_max_m (256);
@@ -91,8 +89,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if w.shape[1] != k:
         raise ValueError(f"linear: x[..., {k}] vs w {tuple(w.shape)}")
     kn = knobs.K
-    if bias is None and use_rw(m, n, k, x, w):
-        return linear_rw(x, w, defer=defer, variant=kn.rw_ns)
     if bias is None and n > 65536 and 0 < kn.pp_head_min_m <= m <= 256 and _use_pp(m, n, k, x, w, 1):
         return linear_pp(x, w, splits=1, variant=PP_HEAD_VARIANT)           # decode LM head
     if bias is None and _use_wide(m, n, k, x, w):
@@ -184,73 +180,6 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
     _ext.kernels().gemm_wide(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s,
                              1 if swiglu else 0, v, stream)
-    return y
-
-
-def use_rw(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
-    """Decode GEMM on gemm_rw.hip (knobs.rw roles, rw_min_m <= M <= 256)."""
-    kn = knobs.K
-    roles = {t for t in kn.rw.split(",") if t and t != "none"}
-    if not roles or not (kn.rw_min_m <= m <= 256) or n % 128 or k % 64:
-        return False
-    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
-        return False
-    if n * k * 2 >= (1 << 31) or m * k * 2 >= (1 << 31):
-        return False
-    role = "gate_up" if swiglu else ("down" if is_down_proj(n, k) else ("head" if n > 65536 else "proj"))
-    return "all" in roles or role in roles
-
-
-def rw_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 256) -> int:
-    """K slices for gemm_rw: about one workgroup per CU (128-column tiles x slices), >= 4 K-tiles
-    (256) per slice."""
-    tiles = n // 128
-    return max(1, min(round(target_wgs / max(1, tiles)), (k // 64) // 4, 16))
-
-
-def pack_rw(w: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
-    """``w`` [N, K] (nn.Linear layout; SwiGLU: [Wg; Wu]) -> the fragment-major layout gemm_rw's
-    packed form streams (csrc/kernels/gemm_rw.hip, PK): for 32-row group g, 64-deep K-tile t,
-    16-deep k-step j and lane L, 8 elements W[32 g + L % 32][64 t + 16 j + 8 (L // 32) ..+ 8] -- one
-    contiguous KiB per (g, t, j), the MFMA A fragment of a wave.  SwiGLU groups hold gate rows
-    16 g .. 16 g + 15 then the same up rows.  Same shape and dtype; a different element order."""
-    n, k = w.shape
-    if n % 32 or k % 64 or (swiglu and n % 64):
-        raise ValueError(f"pack_rw: N {n} % 32 (SwiGLU: % 64), K {k} % 64")
-    if swiglu:   # [Wg; Wu] -> per 16-row output group: 16 gate rows, then its 16 up rows
-        w = w.view(2, n // 32, 16, k).transpose(0, 1).reshape(n, k)
-    # (g, r, t, j, h, e) -> (g, t, j, h, r, e): lane L = 32 h + r
-    return w.reshape(n // 32, 32, k // 64, 4, 2, 8).permute(0, 2, 3, 4, 1, 5).contiguous().view(n, k)
-
-
-def linear_rw(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = False, defer: bool = False,
-              variant: int = 0, packed: bool = False):
-    """Register-weight decode GEMM (csrc/kernels/gemm_rw.hip), M <= 256: weights stream straight
-    into VGPRs as MFMA fragments, activations through an LDS-DMA ring; fused SwiGLU (``w`` =
-    [Wg; Wu]) and split-K.  ``defer``: may return a :class:`SplitKPartial` (no SwiGLU).
-    ``packed``: ``w`` is :func:`pack_rw`'s fragment-major layout (coalesced weight loads).
-    ``variant``: bits 0-3 ring slots (0 = the row tile's default), bits 8-9 row tile override
-    (1 = 64, 2 = 128, 3 = 256 rows; the default is the smallest that holds M)."""
-    k = x.shape[-1]
-    n = w.shape[0]
-    m = x.numel() // k
-    if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
-        raise ValueError("linear_rw: bf16 contiguous operands")
-    if not 1 <= m <= 256 or n % 128 or k % 64:
-        raise ValueError(f"linear_rw: M {m} <= 256, N {n} % 128, K {k} % 64")
-    s = splits or rw_splits(m, n, k, swiglu)
-    ws = _workspace(x.device)
-    if s > 1 and s * m * n > ws.numel():
-        s = max(1, ws.numel() // (m * n))
-    stream = torch.cuda.current_stream().cuda_stream
-    variant = (variant & ~16) | (16 if packed else 0)
-    if defer and not swiglu and s > 1:
-        se = _ext.kernels().gemm_rw(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, variant,
-                                    stream)
-        return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
-    y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
-    _ext.kernels().gemm_rw(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s,
-                           1 if swiglu else 0, variant, stream)
     return y
 
 
@@ -372,8 +301,6 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Te
     k = x.shape[-1]
     n = w_gate_up.shape[0]
     m = x.numel() // k
-    if use_rw(m, n, k, x, w_gate_up, swiglu=True):
-        return linear_rw(x, w_gate_up, swiglu=True, variant=knobs.K.rw_ns)
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
     if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):

@@ -131,28 +131,3 @@ def test_decode_lm_head_goes_to_gemm_pp():
     kn = knobs.K
     assert 0 < kn.pp_head_min_m <= 256 and gemm._use_pp(256, 128256, 4096, x, w, 1)
     assert gemm.PP_HEAD_VARIANT & 64 and gemm.PP_HEAD_VARIANT & 2
-
-
-def test_async_load_checker_flags_reuse_of_in_flight_destinations(tmp_path):
-    """scripts/check_async_loads.py: a VALU op reading a VGPR whose asm global_load is still in
-    flight is flagged; after a vmcnt wait that covers the load it is not."""
-    import subprocess
-    import sys
-    from pathlib import Path
-    asm = """_ZN4dllm14gemm_rw_kernelILi4ELi2ELb1ELb1EEEvX:
-\tbuffer_load_dwordx4 v[8:11], v1, s[8:11], s7 offen nt
-\tbuffer_load_dwordx4 v4, s[12:15], 0 offen lds
-\tv_add_u32_e32 v12, v9, v1
-\ts_waitcnt vmcnt(1)
-\tv_add_u32_e32 v13, v9, v1
-\tglobal_load_dwordx4 v[20:23], v[2:3], off
-\tv_mfma_f32_32x32x16_bf16 a[0:15], v[20:23], v[24:27], a[0:15]
-\ts_waitcnt vmcnt(0)
-\tv_mov_b32_e32 v24, v21
-.Lfunc_end0:
-"""
-    f = tmp_path / "k.s"
-    f.write_text(asm)
-    tool = Path(__file__).resolve().parent.parent / "scripts" / "check_async_loads.py"
-    out = subprocess.run([sys.executable, str(tool), str(f)], capture_output=True, text=True, check=True).stdout
-    assert "hazards 2 " in out, out        # the add before the wait and the MFMA on the pending v[20:23]
