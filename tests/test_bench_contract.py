@@ -61,6 +61,28 @@ def test_torchrun_bench_cpu(n, par, trace, tmp_path):
         assert all(f"rank {r}:" in out for r in range(n)) and "stage.decode" in out
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("n", [2, 4])
+def test_torchrun_bench_over_rccl_transport_cpu(n):
+    """The driver's N-GPU bench path with the pipeline data plane on the native RCCL transport's
+    multi-rank branch (2-rank edge communicators, rings, ids ring closure), its byte movement
+    replaced by the stand-in communicator (parallel/rccl_standin.py): the bench JSON must report
+    the rccl transport on every rank and the edge communicators it built."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT, DLLM_TRANSPORT="rccl", DLLM_RCCL_STANDIN="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "1", "--warmup", "1", "--model", "tiny-llama", "--batch", "3",
+           "--prompt-len", "6", "--gen-len", "4", "--parallelism", "pp"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert KEYS <= set(rec) and rec["n_gpus"] == n and rec["value"] > 0
+    assert rec["transport"] == "rccl"
+    # n - 1 stage edges + the ids ring closure, every rank on at least one 2-rank communicator
+    assert rec["rccl_comms"] == n and rec["rccl_ranks"] == n and rec["rccl_comm_nranks"] == [2]
+    assert all(v > 0 for v in rec["hop_tx_MBps"])
+
+
 def test_single_process_bench_json_cpu():
     env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0", "--model",
