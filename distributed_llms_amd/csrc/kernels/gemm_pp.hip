@@ -736,7 +736,19 @@ void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintpt
 // w = (b % 8) (P / 8) + b / 8), so each XCD's L2 serves 32 consecutive tiles of the grouped order
 // (8 row tiles x 4 column tiles) at a time.
 // MODE 0: C bf16 [M, N];  2: SwiGLU C [M, N / 2] with B = [Bg; Bu] (row groups as pp_b_row).
-template <int MODE>
+// SCH: schedule variant (0 = the shipped one; others for bench/pp_bench.py sweeps): see pf_sched
+struct PfSched {
+  int ib1, ib3, ge, gm;
+};
+constexpr PfSched pf_sched(int sch) {
+  // {barrier after set-1 reads (MFMA), barrier before set-0 reads, MFMAs between pieces (0 = spread
+  // over the rest of the K-tile), row tiles per group of the tile order}
+  return sch == 1 ? PfSched{36, 88, 0, 8} : sch == 2 ? PfSched{48, 88, 0, 8} : sch == 3 ? PfSched{40, 80, 0, 8}
+       : sch == 4 ? PfSched{40, 96, 0, 8} : sch == 5 ? PfSched{40, 88, 4, 8} : sch == 6 ? PfSched{40, 88, 0, 4}
+       : sch == 7 ? PfSched{40, 88, 0, 16} : PfSched{40, 88, 0, 8};
+}
+
+template <int MODE, int SCH = 0>
 __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                          bf16* __restrict__ C, int M, int N, int K) {
   constexpr int NW = 4, NWN = 2, BM = 256, BN = 256, TM = 128, TN = BN / NWN;
@@ -758,9 +770,10 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   const int w = (int)(blockIdx.x & 7) * (P >> 3) + (int)(blockIdx.x >> 3);
   const int mine = w < tiles ? (tiles - 1 - w) / P + 1 : 0;
   if (mine == 0) return;                               // uniform: before any load or barrier
-  const int nt = K / PBK, per = 8 * ntn;
+  constexpr int GM = pf_sched(SCH).gm;                // row tiles per group of the tile order
+  const int nt = K / PBK, per = GM * ntn;
   auto tile_mn = [&](int i, int& m_t, int& n_t) {      // my i-th tile, grouped order
-    const int tau = w + i * P, g = tau / per, first = g * 8, gsz = min(mtiles - first, 8), q = tau - g * per;
+    const int tau = w + i * P, g = tau / per, first = g * GM, gsz = min(mtiles - first, GM), q = tau - g * per;
     m_t = first + q % gsz;
     n_t = q / gsz;
   };
@@ -828,9 +841,11 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   f32x4 acc[RT][CT];
   bf16x8 fa0[RT], fb0[CT], fa1[RT], fb1[CT];
   constexpr int NMF = RT * CT, NR = RT + CT;
-  constexpr int IB1 = 2 * NR + 8 < NMF - 1 ? 2 * NR + 8 : NMF - 1;
-  constexpr int GE = (2 * NMF - 4 - IB1 - 1) / G > 1 ? (2 * NMF - 4 - IB1 - 1) / G : 1;
-  constexpr int IB3 = 2 * NMF - 8 - 2 * NR > NMF ? 2 * NMF - 8 - 2 * NR : NMF;
+  constexpr PfSched SC = pf_sched(SCH);
+  constexpr int IB1 = SC.ib1;
+  constexpr int GE = SC.ge ? SC.ge : ((2 * NMF - 4 - IB1 - 1) / G > 1 ? (2 * NMF - 4 - IB1 - 1) / G : 1);
+  constexpr int IB3 = SC.ib3;
+  static_assert(IB1 > 2 * NR - 1 && IB1 < NMF && IB3 >= NMF, "schedule 2 barriers");
   constexpr int PB3 = (IB3 - IB1 - 1) / GE + 1 < G ? (IB3 - IB1 - 1) / GE + 1 : G;
   constexpr int VC = (NB - 2) * G + PB3;
   static_assert(IB1 + 1 + GE * (G - 1) < 2 * NMF && IB3 + 1 + 2 * (NR - 1) < 2 * NMF, "schedule 2 fits a K-tile");
@@ -960,7 +975,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
 
 // Persistent prefill GEMM: C = A B^T (mode 0) or SwiGLU (mode 1, C [M, N / 2], B = [Bg; Bu]),
 // 256 x 256 tiles, grid = min(tiles, CUs) rounded up to a multiple of 8.
-void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mode, uintptr_t stream) {
+void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mode, int variant, uintptr_t stream) {
   DLLM_HOST_CHECK(M >= 1, "M >= 1");
   DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
@@ -977,13 +992,25 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   const long tiles = (long)(N / 256) * ((M + 255) / 256);
   DLLM_HOST_CHECK(tiles < (1L << 30), "tiles");
   const long grid = ((tiles < cus ? tiles : cus) + 7) / 8 * 8;
+  DLLM_HOST_CHECK(variant >= 0 && variant <= 7 && (mode == 0 || variant == 0), "schedule variant 0..7 (plain only)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (mode == 1)
-    hipLaunchKernelGGL((gemm_pf_kernel<2>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, (const bf16*)b,
-                       (bf16*)c, M, N, K);
-  else
-    hipLaunchKernelGGL((gemm_pf_kernel<0>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, (const bf16*)b,
-                       (bf16*)c, M, N, K);
+#define DLLM_PF_GO(MODE_, SCH_)                                                                               \
+  hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a,     \
+                     (const bf16*)b, (bf16*)c, M, N, K)
+  if (mode == 1) DLLM_PF_GO(2, 0);
+  else {
+    switch (variant) {
+      case 1: DLLM_PF_GO(0, 1); break;
+      case 2: DLLM_PF_GO(0, 2); break;
+      case 3: DLLM_PF_GO(0, 3); break;
+      case 4: DLLM_PF_GO(0, 4); break;
+      case 5: DLLM_PF_GO(0, 5); break;
+      case 6: DLLM_PF_GO(0, 6); break;
+      case 7: DLLM_PF_GO(0, 7); break;
+      default: DLLM_PF_GO(0, 0); break;
+    }
+  }
+#undef DLLM_PF_GO
   DLLM_HIP_CHECK(hipGetLastError());
 }
 

@@ -219,10 +219,11 @@ def linear_pp(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = 
     return y
 
 
-def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
+def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, variant: int = 0) -> torch.Tensor:
     """Persistent prefill GEMM (gemm_pf in csrc/kernels/gemm_pp.hip): schedule 2's 256 x 256 tiles,
     one workgroup per CU walking its tiles with the LDS-DMA pipeline running across tile
-    boundaries; optional fused SwiGLU (``w`` = [Wg; Wu], y [M, N / 2])."""
+    boundaries; optional fused SwiGLU (``w`` = [Wg; Wu], y [M, N / 2]).  ``variant`` 1-7: schedule
+    variants of the plain form for sweeps (csrc/kernels/gemm_pp.hip pf_sched)."""
     k = x.shape[-1]
     n = w.shape[0]
     m = x.numel() // k
@@ -231,7 +232,7 @@ def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> torch.T
     if n % 256 or k % 64:
         raise ValueError("linear_pf: N % 256 and K % 64")
     y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
-    _ext.kernels().gemm_pf(y.data_ptr(), x.data_ptr(), w.data_ptr(), m, n, k, 1 if swiglu else 0,
+    _ext.kernels().gemm_pf(y.data_ptr(), x.data_ptr(), w.data_ptr(), m, n, k, 1 if swiglu else 0, variant,
                            torch.cuda.current_stream().cuda_stream)
     return y
 

@@ -318,6 +318,14 @@ def test_pf_swiglu(cuda, m, inter, k):
     torch.testing.assert_close(y.float(), ref, atol=6e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("variant", range(1, 8))
+def test_pf_schedule_variants_bit_exact(cuda, variant):
+    """The schedule variants (bench sweeps) only move barriers, staging slots and the tile order:
+    same K order per output, same bits."""
+    x, w = _bf(2100, 1024), _bf(2048, 1024, scale=0.05)
+    assert torch.equal(gemm.linear_pf(x, w, variant=variant), gemm.linear_pf(x, w))
+
+
 def test_pf_matches_pp_schedule2_bit_exact(cuda):
     """Same K-tile body and accumulation order as gemm_pp schedule 2: identical bits, plain and
     SwiGLU (the SwiGLU of gemm_pp rounds gate / up to bf16 first, so only the plain form is exact)."""

@@ -33,7 +33,7 @@ def test_pf_persistent_kernel_keeps_the_pipeline_full(pp_asm):
     vmcnt(0) anywhere before the final drain -- the tile-boundary epilogue included."""
     s = pp_asm.read_text()
     names = re.findall(r"^(_ZN4dllm14gemm_pf_kernel\w+):", s, re.M)
-    assert len(names) == 2
+    assert len(names) >= 2
     for name in names:
         start = s.index(name + ":")
         body = s[start: s.index(".Lfunc_end", start)]
