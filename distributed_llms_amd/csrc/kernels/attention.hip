@@ -224,8 +224,11 @@ __device__ __forceinline__ void rope_rotate(bf16x8 (&f)[D / 32], const float* cs
     for (int j = 0; j < 8; ++j) {
       const float c = j < 4 ? c0[j] : c1[j - 4], s = j < 4 ? s0[j] : s1[j - 4];
       const float a = bf2f(f[ks][j]), b = bf2f(f[ks + D / 64][j]);
-      f[ks][j] = f2bf(a * c - b * s);
-      f[ks + D / 64][j] = f2bf(b * c + a * s);
+      // explicit FMAs: left to hipcc's default contraction, the fused / unfused choice here may
+      // differ between kernel instantiations, and the bf16-qkv and split-K-slab forms of the fused
+      // decode must rotate q / k bit-identically (a trial build rotated them 1 ulp apart at times)
+      f[ks][j] = f2bf(__builtin_fmaf(a, c, -(b * s)));
+      f[ks + D / 64][j] = f2bf(__builtin_fmaf(b, c, a * s));
     }
   }
 }
