@@ -980,7 +980,10 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
   DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
-  DLLM_HOST_CHECK((long)M * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32) && (long)M * N * 2 < (1L << 31),
+  // the output's byte range must stay below 2^31: rows past M are dropped by giving their stores
+  // the offset 0x80000000, which has to lie outside the buffer's range
+  DLLM_HOST_CHECK((long)M * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32) &&
+                      (long)M * (mode == 1 ? N / 2 : N) * 2 < (1L << 31),
                   "operands must be < 4 GiB, the output < 2 GiB");
   static int cus = 0;
   if (cus == 0) {

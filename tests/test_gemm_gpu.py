@@ -333,6 +333,17 @@ def test_pf_matches_pp_schedule2_bit_exact(cuda):
     assert torch.equal(gemm.linear_pf(x, w), gemm.linear_pp(x, w, splits=1, variant=gemm.PP_PREFILL_VARIANT))
 
 
+def test_pf_swiglu_output_range_is_the_half_width(cuda):
+    """SwiGLU's output is [M, N / 2]: a 70B prefill gate|up (M 32768, 2I 57344) is within the
+    kernel's 2 GiB output range although M x 2I x 2 bytes is not (a small-K stand-in shape)."""
+    x, w = _bf(32768, 64), _bf(57344, 64, scale=0.05)
+    y = gemm.linear_swiglu(x, w)
+    assert y.shape == (32768, 28672)
+    gu = x[-300:].float() @ w.float().t()
+    ref = F.silu(gu[:, :28672]) * gu[:, 28672:]
+    torch.testing.assert_close(y[-300:].float(), ref, atol=6e-2, rtol=3e-2)
+
+
 def test_pf_dispatch_and_graph(cuda):
     from distributed_llms_amd import knobs
     x, w = _bf(4096, 4096), _bf(4096, 4096, scale=0.05)
