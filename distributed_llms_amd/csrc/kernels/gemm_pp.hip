@@ -29,6 +29,7 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <atomic>
 #include <type_traits>
 #include <utility>
 
@@ -985,12 +986,16 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   DLLM_HOST_CHECK((long)M * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32) &&
                       (long)M * (mode == 1 ? N / 2 : N) * 2 < (1L << 31),
                   "operands must be < 4 GiB, the output < 2 GiB");
-  static int cus = 0;
+  // CUs of the current device, cached per device (a benign race: every thread stores the same value)
+  static std::atomic<int> cus_of[64];
+  int dev = 0;
+  DLLM_HIP_CHECK(hipGetDevice(&dev));
+  int cus = dev >= 0 && dev < 64 ? cus_of[dev].load(std::memory_order_relaxed) : 0;
   if (cus == 0) {
-    int dev = 0, n = 0;
-    DLLM_HIP_CHECK(hipGetDevice(&dev));
+    int n = 0;
     DLLM_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
     cus = n > 0 ? n : 256;
+    if (dev >= 0 && dev < 64) cus_of[dev].store(cus, std::memory_order_relaxed);
   }
   const long tiles = (long)(N / 256) * ((M + 255) / 256);
   DLLM_HOST_CHECK(tiles < (1L << 30), "tiles");
