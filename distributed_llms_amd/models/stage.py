@@ -405,13 +405,16 @@ class ModelStage:
                     h = ops.add_(self._dense(self._mlp(x, lw)), carry)
         if out_aux is not None:
             return torch.cat([residual, out_aux.view(out_aux.shape[0], -1)], dim=1)
-        h = self._dense(h)
         if not self.is_last:
-            return ops.add_(residual, h)
+            return ops.add_(residual, self._dense(h))
         return self._logits(h, residual, meta)
 
-    def _logits(self, h: torch.Tensor, residual: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
+    def _logits(self, h, residual: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
+        # ``h`` may still be the last down projection's split-K partials: at decode (every row's
+        # logits) they are reduced inside the final add + RMSNorm, as between layers
         cfg = self.cfg
+        if meta.logits_idx is not None or cfg.arch == "gpt2":
+            h = self._dense(h)
         if meta.logits_idx is not None:
             h = h.index_select(0, meta.logits_idx)
             residual = residual.index_select(0, meta.logits_idx)
