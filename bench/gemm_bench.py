@@ -47,9 +47,6 @@ def main():
     ap.add_argument("--variants", type=int, nargs="*", default=[0],
                     help="extra gemm_wide variants timed beside the engine's choice")
     ap.add_argument("--sq", action="store_true", help="also time the 256 x 256-tile gemm_sq kernel")
-    ap.add_argument("--band", type=int, nargs="*", default=[],
-                    help="also time gemm_gu.hip's band kernel with these CT (column fragments) on plain shapes")
-    ap.add_argument("--gu", action="store_true", help="also time gemm_gu.hip (SwiGLU shapes, M <= 256)")
     ap.add_argument("--sq-alt", type=int, default=0, help="--sq: second gemm_sq variant timed (sq0)")
     a = ap.parse_args()
     return wide(a)
@@ -77,13 +74,6 @@ def wide(a):
                    for v in a.variants},
                 **({"sq": lambda w: gemm.linear_sq(x, w, swiglu=sw, variant=4),
                     "sq0": lambda w: gemm.linear_sq(x, w, swiglu=sw, variant=a.sq_alt)} if a.sq and n % 256 == 0 else {}),
-                **{f"b{c}": (lambda w, c=c: gemm.linear_band(x, w, ct=c)) for c in a.band
-                   if not sw and m <= 256 and n % (16 * c) == 0},
-                **{f"r{c}": (lambda w, c=c: gemm.linear_band(x, w, ct=c, areg=True)) for c in a.band
-                   if not sw and m <= 256 and n % (16 * c) == 0},
-                **({"gu": lambda w: gemm.linear_gate_up56(x, w, variant=0),
-                    "gua": lambda w: gemm.linear_gate_up56(x, w, variant=1)}
-                   if a.gu and sw and m <= 256 and (n // 2) % 56 == 0 else {}),
                 "blas": (lambda w: ops.silu_mul(F.linear(x, w))) if sw else (lambda w: F.linear(x, w)),
             }
             reps = max(copies, 8)
@@ -111,10 +101,6 @@ def wide(a):
             print(f"{name:12s} {m:4d} {t['wide']*1e6:8.1f} {byt/t['wide']/1e12:6.2f} {fl_/t['wide']/1e12:6.0f} "
                   f"{t['blas']*1e6:8.1f} {t['blas']/t['wide']:8.2f} "
                   + " ".join(f"v{v} {t[f'v{v}']*1e6:6.1f}" for v in a.variants)
-                  + "".join(f" {p}{c} {t[f'{p}{c}']*1e6:6.1f} ({t['wide']/t[f'{p}{c}']:.2f}x)"
-                            for c in a.band for p in "br" if f"{p}{c}" in t)
-                  + (f" gu {t['gu']*1e6:6.1f} ({t['wide']/t['gu']:.2f}x) gua {t['gua']*1e6:6.1f} "
-                     f"({t['wide']/t['gua']:.2f}x)" if "gu" in t else "")
                   + (f" sq {t['sq']*1e6:6.1f} ({t['wide']/t['sq']:.2f}x) sq0 {t['sq0']*1e6:6.1f}" if "sq" in t else ""),
                   flush=True)
 
