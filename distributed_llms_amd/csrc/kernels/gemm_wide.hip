@@ -191,34 +191,21 @@ constexpr int PFD = 2;
 template <int BM, int NBUF, int VAR, bool FP8 = false>
 __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&srcA)[BM / 64],
                                               const bf16* const (&srcB)[2], int nt, f32x4 (&acc)[BM / 64][4],
-                                              int wv, int lane, const bf16* pfB = nullptr, bf16* pf_lds = nullptr,
-                                              int rot = 0) {
+                                              int wv, int lane, const bf16* pfB = nullptr, bf16* pf_lds = nullptr) {
   constexpr int AEL = BM * WBK, BEL = WBN * WBK, BUF = AEL + BEL;
   constexpr bool PF = (VAR & 128) != 0;
-  // ROT (VAR & 256): this workgroup walks its K range starting at K-tile `rot` (wrapping), so the
-  // workgroups of an XCD that share the activation matrix request different lines of it at any
-  // moment instead of all the same ones
-  constexpr bool ROT = (VAR & 256) != 0;
-  auto kof = [&](int t) {                              // element offset of logical K-tile t
-    if constexpr (ROT) {
-      const int u = t + rot;
-      return (u >= nt ? u - nt : u) * WBK;
-    } else {
-      return t * WBK;
-    }
-  };
   constexpr int AI = BM / 64, BI = 2, G0 = AI + BI, G = PF ? G0 + 1 : G0, RT = BM / 64;
   // the L2 prefetch of the weight tile staged PFD slots after this one (clamped: counts stay static)
   auto prefetch = [&](int tile) {
     if constexpr (PF)
-      __builtin_amdgcn_global_load_lds((glb_vptr_w)(pfB + kof(min(tile, nt - 1))), (lds_vptr_w)pf_lds, 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_vptr_w)(pfB + min(tile, nt - 1) * WBK), (lds_vptr_w)pf_lds, 4, 0, 0);
   };
   const int wm = wv >> 1, wn = wv & 1;
   // cache policy of the staging loads (aux: 2 = nt): VAR 2 streams the weights nt, VAR 3 both operands
   constexpr int BAUX = (VAR & 7) >= 2 ? 2 : 0, AAUX = (VAR & 7) == 3 ? 2 : 0;
   auto stage = [&](int buf, int t) {
     bf16* base = smem + buf * BUF;
-    const int ko = kof(t);
+    const int ko = t * WBK;
 #pragma unroll
     for (int j = 0; j < AI; ++j)
       __builtin_amdgcn_global_load_lds((glb_vptr_w)(srcA[j] + ko), (lds_vptr_w)(base + (wv * AI + j) * 512), 16, 0,
@@ -415,14 +402,14 @@ __device__ __forceinline__ void wide_mainloop(bf16* smem, const bf16* const (&sr
       // this barrier: refill it with tile t + NBUF - 1
       const int nb = cur == 0 ? NBUF - 1 : cur - 1;
       if constexpr (FP8) {
-        ktile8(cur, smem + nb * BUF, kof(t + NBUF - 1), std::true_type{});
+        ktile8(cur, smem + nb * BUF, (t + NBUF - 1) * WBK, std::true_type{});
       } else if constexpr (SPLITRD) {
-        ktile_sr(cur, smem + nb * BUF, kof(t + NBUF - 1), std::true_type{});
+        ktile_sr(cur, smem + nb * BUF, (t + NBUF - 1) * WBK, std::true_type{});
       } else if constexpr ((VAR & 7) == 0) {
         stage(nb, t + NBUF - 1);
         ktile(cur, smem, 0, std::false_type{});
       } else {
-        ktile(cur, smem + nb * BUF, kof(t + NBUF - 1), std::true_type{});
+        ktile(cur, smem + nb * BUF, (t + NBUF - 1) * WBK, std::true_type{});
       }
       cur = cur == NBUF - 1 ? 0 : cur + 1;
     }
@@ -494,12 +481,7 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
   // PF: lanes l and l + 16k of wave w touch weight row 16 w + (l & 15) of the tile: 128 lines per K-tile
   const bf16* pfB = B + (size_t)wide_b_row<SWIGLU>(16 * wv + (lane & 15), n_t, N / 2) * K + (size_t)kt0 * WBK;
   f32x4 acc[RT][4];
-  int rot = 0;
-  if constexpr ((VAR & 256) != 0) {   // spread this XCD's workgroups evenly over the K range
-    const int q = max(1, total >> 3);
-    rot = nt > 0 ? (int)(((long)(b % q) * nt) / q) : 0;
-  }
-  wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, nt, acc, wv, lane, pfB, smem + NBUF * BUF, rot);
+  wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, nt, acc, wv, lane, pfB, smem + NBUF * BUF);
   if ((VAR & 8) && nsplit >= 0) return;
   wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
 }
@@ -707,10 +689,8 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   const bool swiglu = mode == 1;
   DLLM_HOST_CHECK(swiglu ? (N % 128 == 0) : (N % WBN == 0), "N must be a multiple of 128");
   DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
-  // variant bits 8..19: optional row tile override (64 / 128 / 192 / 256), 0 = wide_bm(M);
-  // bit 20: K-start rotation per workgroup (wide_mainloop ROT)
-  const int bm_force = (variant >> 8) & 0xfff;
-  const bool rot = (variant >> 20) & 1;
+  // variant bits 8..: optional row tile override (64 / 128 / 192 / 256), 0 = wide_bm(M)
+  const int bm_force = variant >> 8;
   variant &= 0xff;
   DLLM_HOST_CHECK(bm_force == 0 || bm_force == 64 || bm_force == 128 || bm_force == 192 || bm_force == 256,
                   "row tile override must be 64, 128, 192 or 256");
@@ -744,9 +724,7 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
                      (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S)
 #define DLLM_WIDE_GO(BM_, SPLIT_, SW_)                                                                          \
   do {                                                                                                         \
-    if (rot && abl == 32) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 290); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 289); } \
-    else if (rot) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 258); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 257); } \
-    else if (abl == 8) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 10); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 9); } \
+    if (abl == 8) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 10); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 9); } \
     else if (abl == 16) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 18); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 17); } \
     else if (pf && abl == 32) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 162); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 161); } \
     else if (pf) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 130); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 129); } \

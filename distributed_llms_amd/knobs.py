@@ -41,9 +41,6 @@ class Knobs:
     wide_target_wgs: int = 256        # split-K: about one workgroup per CU
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
-    # each workgroup starts its K walk at its own K-tile (spread over the range per XCD), so the
-    # workgroups sharing the activation matrix do not all request the same L2 lines at once
-    wide_krot: bool = False
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
     # from this M up to 256, unsplit grids only unless sq_split
     sq: str = "all"

@@ -157,26 +157,6 @@ def test_wide_grouped_tile_order_bit_exact(cuda, m, n, k, swiglu):
     torch.testing.assert_close(b.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("m,n,k,splits,swiglu", [(256, 28672, 4096, 1, True), (256, 4096, 14336, 8, False),
-                                                  (256, 6144, 4096, 5, False), (100, 4096, 4096, 8, False),
-                                                  (33, 1024, 512, 1, False), (256, 2048, 4096, 3, True)])
-def test_wide_k_rotation(cuda, m, n, k, splits, swiglu):
-    """knobs.wide_krot: each workgroup starts its K walk at its own K-tile -- the same sums in
-    another order (fp32 reference), deferred slabs included."""
-    from distributed_llms_amd import knobs
-    torch.manual_seed(m + n + k)
-    x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    with knobs.override(wide_krot=True):
-        y = gemm.linear_wide(x, w, splits=splits, swiglu=swiglu)
-        p = None if swiglu or splits == 1 else gemm.linear_wide(x, w, splits=splits, defer=True)
-    ref = x.float() @ w.float().t()
-    if swiglu:
-        ref = F.silu(ref[:, : n // 2]) * ref[:, n // 2:]
-    torch.testing.assert_close(y.float(), ref, atol=6e-2 if swiglu else 3e-2, rtol=3e-2)
-    if p is not None:
-        torch.testing.assert_close(p.materialize(), y, atol=0, rtol=0)
-
-
 def test_splitk_slabs_keep_output_precision(cuda):
     """Split-K slabs are stored as f16 x 2^-6 (csrc/kernels/common.h, DLLM_PART_TYPE 2): the split
     result must stay within one bf16 ulp of the exact product (plus half an ulp of the output's typical
