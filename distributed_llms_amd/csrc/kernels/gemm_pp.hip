@@ -603,6 +603,10 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
     if constexpr (MODE == 1) {
       _Float16* Ph = reinterpret_cast<_Float16*>(P);
       *reinterpret_cast<int4*>(Ph + ((size_t)split * M + m) * N + col0) = v;
+    } else if constexpr (SWIGLU) {                    // nontemporal, as gemm_pf's SwiGLU tiles
+      typedef int i32x4v __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(*reinterpret_cast<const i32x4v*>(&v),
+                                  reinterpret_cast<i32x4v*>(C + (size_t)m * ldc + col0));
     } else {
       *reinterpret_cast<int4*>(C + (size_t)m * ldc + col0) = v;
     }
@@ -965,7 +969,9 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
           y[d] = sw[1];
         }
         const u32x4 o = {x[0], x[1], y[0], y[1]};
-        __builtin_amdgcn_raw_buffer_store_b128(o, rsC, (int)(vo + pr * 64), 0, 0);
+        // SwiGLU: nontemporal stores (+1-3 % on the 8B gate|up; neutral to -2 % on plain tiles,
+        // profiles/round4_ab_results.md)
+        __builtin_amdgcn_raw_buffer_store_b128(o, rsC, (int)(vo + pr * 64), 0, SWIGLU ? 2 : 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
