@@ -603,10 +603,6 @@ __global__ void __launch_bounds__(256, 1) gemm_pp_kernel(const bf16* __restrict_
     if constexpr (MODE == 1) {
       _Float16* Ph = reinterpret_cast<_Float16*>(P);
       *reinterpret_cast<int4*>(Ph + ((size_t)split * M + m) * N + col0) = v;
-    } else if constexpr (SWIGLU) {                    // nontemporal, as gemm_pf's SwiGLU tiles
-      typedef int i32x4v __attribute__((ext_vector_type(4)));
-      __builtin_nontemporal_store(*reinterpret_cast<const i32x4v*>(&v),
-                                  reinterpret_cast<i32x4v*>(C + (size_t)m * ldc + col0));
     } else {
       *reinterpret_cast<int4*>(C + (size_t)m * ldc + col0) = v;
     }
