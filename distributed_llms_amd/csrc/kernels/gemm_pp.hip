@@ -737,7 +737,8 @@ void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintpt
 // w = (b % 8) (P / 8) + b / 8), so each XCD's L2 serves 32 consecutive tiles of the grouped order
 // (8 row tiles x 4 column tiles) at a time.
 // MODE 0: C bf16 [M, N];  2: SwiGLU C [M, N / 2] with B = [Bg; Bu] (row groups as pp_b_row).
-// SCH: schedule variant (0 = the shipped one; others for bench/pp_bench.py sweeps): see pf_sched
+// SCH: schedule variant (0 = the shipped one; others for bench/pp_bench.py sweeps): see pf_sched;
+// 8 = the shipped schedule with nontemporal output stores (large SwiGLU outputs)
 struct PfSched {
   int ib1, ib3, ge, gm;
 };
@@ -965,9 +966,10 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
           y[d] = sw[1];
         }
         const u32x4 o = {x[0], x[1], y[0], y[1]};
-        // SwiGLU: nontemporal stores (+1-3 % on the 8B gate|up; neutral to -2 % on plain tiles,
-        // profiles/round4_ab_results.md)
-        __builtin_amdgcn_raw_buffer_store_b128(o, rsC, (int)(vo + pr * 64), 0, SWIGLU ? 2 : 0);
+        // SCH 8 (SwiGLU outputs larger than the Infinity Cache): nontemporal stores, +1-3 % on the
+        // 8B gate|up at T = 32768; neutral to -2 % on plain tiles, and -0.5 % in-engine where the
+        // next GEMM could re-read the output from the caches (profiles/round4_ab_results.md)
+        __builtin_amdgcn_raw_buffer_store_b128(o, rsC, (int)(vo + pr * 64), 0, SCH == 8 ? 2 : 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1002,13 +1004,17 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   const long tiles = (long)(N / 256) * ((M + 255) / 256);
   DLLM_HOST_CHECK(tiles < (1L << 30), "tiles");
   const long grid = ((tiles < cus ? tiles : cus) + 7) / 8 * 8;
-  DLLM_HOST_CHECK(variant >= 0 && variant <= 7 && (mode == 0 || variant == 0), "schedule variant 0..7 (plain only)");
+  DLLM_HOST_CHECK(variant >= 0 && variant <= 8 && (mode == 0 || variant == 0 || variant == 8),
+                  "variant 0..8 (SwiGLU: 0 or 8)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 #define DLLM_PF_GO(MODE_, SCH_)                                                                               \
   hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a,     \
                      (const bf16*)b, (bf16*)c, M, N, K)
-  if (mode == 1) DLLM_PF_GO(2, 0);
-  else {
+  if (mode == 1) {
+    // variant 8 forces the nontemporal stores; by default they go with outputs > 256 MiB
+    if (variant == 8 || (variant == 0 && (long)M * (N / 2) * 2 > (256L << 20))) DLLM_PF_GO(2, 8);
+    else DLLM_PF_GO(2, 0);
+  } else {
     switch (variant) {
       case 1: DLLM_PF_GO(0, 1); break;
       case 2: DLLM_PF_GO(0, 2); break;
@@ -1017,6 +1023,7 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
       case 5: DLLM_PF_GO(0, 5); break;
       case 6: DLLM_PF_GO(0, 6); break;
       case 7: DLLM_PF_GO(0, 7); break;
+      case 8: DLLM_PF_GO(0, 8); break;
       default: DLLM_PF_GO(0, 0); break;
     }
   }

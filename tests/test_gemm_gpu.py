@@ -318,12 +318,20 @@ def test_pf_swiglu(cuda, m, inter, k):
     torch.testing.assert_close(y.float(), ref, atol=6e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("variant", range(1, 8))
+@pytest.mark.parametrize("variant", range(1, 9))
 def test_pf_schedule_variants_bit_exact(cuda, variant):
-    """The schedule variants (bench sweeps) only move barriers, staging slots and the tile order:
-    same K order per output, same bits."""
+    """The schedule variants (bench sweeps) only move barriers, staging slots, the tile order and
+    the stores' cache policy (8: nontemporal): same K order per output, same bits."""
     x, w = _bf(2100, 1024), _bf(2048, 1024, scale=0.05)
     assert torch.equal(gemm.linear_pf(x, w, variant=variant), gemm.linear_pf(x, w))
+
+
+@pytest.mark.parametrize("m", [256, 2100])
+def test_pf_swiglu_nontemporal_stores_bit_exact(cuda, m):
+    """SwiGLU with the nontemporal output stores (variant 8; the default above 256 MiB of output):
+    the same bits as the default stores, rows past M dropped."""
+    x, w = _bf(m, 1024), _bf(2 * 1536, 1024, scale=0.05)
+    assert torch.equal(gemm.linear_pf(x, w, swiglu=True, variant=8), gemm.linear_pf(x, w, swiglu=True))
 
 
 def test_pf_matches_pp_schedule2_bit_exact(cuda):
