@@ -60,10 +60,16 @@ def rccl():
     """The native RCCL p2p module; raises if it is not built.  ``DLLM_RCCL_STANDIN=1`` (tests /
     rehearsal only) returns parallel/rccl_standin.py instead: the same interface over the
     torch.distributed store, so the transport's multi-rank path runs where RCCL cannot."""
-    global _rccl
     if os.environ.get("DLLM_RCCL_STANDIN", "0") == "1":
         from .parallel import rccl_standin
+        rccl_standin.warn_selected()
         return rccl_standin
+    return rccl_native()
+
+
+def rccl_native():
+    """The native module itself (also the stand-in's HIP-IPC helpers)."""
+    global _rccl
     if _rccl is None:
         try:
             _rccl = _import("_C_rccl")

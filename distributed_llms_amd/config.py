@@ -231,6 +231,11 @@ class EngineConfig:
     streams: int = 1
     max_batch: int = 256               # max sequences decoded per step (per replica)
     max_prefill_tokens: int = 16384    # max prompt tokens per prefill step
+    # prompt tokens a step may add to a slot's running decode rows (mixed prefill + decode step,
+    # SURVEY §5.7): arrivals during decode are prefilled in chunks of at most this many tokens
+    # riding along with the decode batch, so running sequences never stall behind a whole
+    # max_prefill_tokens chunk; 0 = prefill-first (a step is all prefill or all decode)
+    mixed_prefill_tokens: int = 512
     max_seq_len: int = 4096
     kv_block_size: int = 32            # tokens per paged-KV block
     kv_cache_fraction: float = 0.80    # of free HBM after weights

@@ -38,4 +38,8 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("paged_attention_decode", &dllm::paged_attention_decode);
   m.def("paged_attention_decode_rope", &dllm::paged_attention_decode_rope);
   m.def("paged_attention_prefill", &dllm::paged_attention_prefill);
+  m.def("p2p_inbox_bytes", &dllm::p2p_inbox_bytes);
+  m.def("p2p_standin", &dllm::p2p_standin);
+  m.def("p2p_host_words", &dllm::p2p_host_words);
+  m.def("p2p_host_words_free", &dllm::p2p_host_words_free);
 }

@@ -30,7 +30,9 @@
 #include "launchers.h"
 
 #include <atomic>
+#include <mutex>
 #include <type_traits>
+#include <unordered_map>
 #include <utility>
 
 namespace dllm {
@@ -742,6 +744,60 @@ void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintpt
 struct PfSched {
   int ib1, ib3, ge, gm;
 };
+
+// ---- gemm_pf's dynamic tile queue (DYN).  The grouped tile order is cut into chunks of PF_CH
+// consecutive tiles (8 row tiles x 4 column tiles); chunk c belongs to XCD c % 8, whose workgroups
+// pull its tiles in order from the XCD's head counter (one 128-byte line each) and, when it is
+// empty, steal from the other XCDs' heads.  A workgroup that starts late -- its CU held by a
+// co-resident kernel, e.g. an RCCL receive spinning on its LDS -- finds the tiles taken and exits,
+// instead of owning a static share (tile = w + i P) that the whole GEMM then waits for.  The last
+// workgroup to retire resets the heads for the next launch on the stream.
+// queue layout (ints): head of XCD x at [32 x], retire counter at [256].
+constexpr int PF_CH = 32;
+constexpr int PF_QUEUE_INTS = 9 * 32;
+
+__device__ __forceinline__ int pf_count(int x, int tiles) {         // tiles of XCD x's partition
+  const int nch = (tiles + PF_CH - 1) / PF_CH;
+  if (x >= nch) return 0;
+  const int cx = (nch - 1 - x) / 8 + 1, last = x + 8 * (cx - 1);
+  return (cx - 1) * PF_CH + min(PF_CH, tiles - last * PF_CH);
+}
+
+__device__ __forceinline__ int pf_tau(int x, int j) { return (x + 8 * (j / PF_CH)) * PF_CH + j % PF_CH; }
+
+// blocking fetch (lane 0): the XCD's own head first, then the others'; -1 = no tile left
+__device__ int pf_fetch(int* q, int xcd, int tiles, int first_try = -1) {
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) {
+    const int x = (xcd + k) & 7, n = pf_count(x, tiles);
+    if (n == 0) continue;
+    int j;
+    if (k == 0 && first_try >= 0) {
+      j = first_try;                                                // the asynchronous fetch's result
+    } else {
+      if (__hip_atomic_load(q + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n) continue;
+      j = atomicAdd(q + 32 * x, 1);
+    }
+    if (j < n) return pf_tau(x, j);
+  }
+  return -1;
+}
+
+// the K loop's fetch: issued in inline asm, so hipcc inserts no wait for it; the counted vmcnt
+// wait of the NEXT K-tile (every LDS-DMA piece of that K-tile is younger) covers its return
+__device__ __forceinline__ int pf_fetch_async(int* head) {
+  int old;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(old) : "v"(head), "v"(1) : "memory");
+  return old;
+}
+
+__device__ void pf_retire(int* q, int grid) {                      // lane 0, once per workgroup
+  if (atomicAdd(q + 256, 1) == grid - 1) {
+#pragma unroll
+    for (int x = 0; x < 8; ++x) __hip_atomic_store(q + 32 * x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 256, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 constexpr PfSched pf_sched(int sch) {
   // {barrier after set-1 reads (MFMA), barrier before set-0 reads, MFMAs between pieces (0 = spread
   // over the rest of the K-tile), row tiles per group of the tile order}
@@ -750,9 +806,10 @@ constexpr PfSched pf_sched(int sch) {
        : sch == 7 ? PfSched{40, 88, 0, 16} : PfSched{40, 88, 0, 8};
 }
 
-template <int MODE, int SCH = 0>
+template <int MODE, int SCH = 0, bool DYN = false>
 __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                         bf16* __restrict__ C, int M, int N, int K) {
+                                                         bf16* __restrict__ C, int M, int N, int K,
+                                                         int* __restrict__ queue) {
   constexpr int NW = 4, NWN = 2, BM = 256, BN = 256, TM = 128, TN = BN / NWN;
   constexpr int RT = TM / 16, CT = TN / 16;            // 8 x 8 accumulators per wave
   constexpr int SLOT = (BM + BN) * PBK, NB = 2;        // 2 x 64 KiB ring
@@ -762,6 +819,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) bf16 smem[NB * SLOT];
+  __shared__ int tq[4];                                // DYN: tile of local ordinal i at [i & 3]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -770,12 +828,28 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   const int ntn = N / BN, mtiles = (M + BM - 1) / BM, tiles = ntn * mtiles;
   const int P = gridDim.x;                             // a multiple of 8 (host)
   const int w = (int)(blockIdx.x & 7) * (P >> 3) + (int)(blockIdx.x >> 3);
-  const int mine = w < tiles ? (tiles - 1 - w) / P + 1 : 0;
-  if (mine == 0) return;                               // uniform: before any load or barrier
+  const int xcd = (int)(blockIdx.x & 7);               // blocks are dealt round-robin over the XCDs
+  int mine = 0;                                        // static: my tile count
+  if constexpr (DYN) {
+    if (tid == 0) {
+      const int t0 = pf_fetch(queue, xcd, tiles);
+      tq[0] = t0;
+      tq[1] = t0 >= 0 ? pf_fetch(queue, xcd, tiles) : -1;
+    }
+    __syncthreads();
+    if (tq[0] < 0) {                                   // uniform: every tile already taken
+      if (tid == 0) pf_retire(queue, P);
+      return;
+    }
+  } else {
+    mine = w < tiles ? (tiles - 1 - w) / P + 1 : 0;
+    if (mine == 0) return;                             // uniform: before any load or barrier
+  }
   constexpr int GM = pf_sched(SCH).gm;                // row tiles per group of the tile order
   const int nt = K / PBK, per = GM * ntn;
-  auto tile_mn = [&](int i, int& m_t, int& n_t) {      // my i-th tile, grouped order
-    const int tau = w + i * P, g = tau / per, first = g * GM, gsz = min(mtiles - first, GM), q = tau - g * per;
+  auto tile_of = [&](int i) { return DYN ? tq[i & 3] : w + i * P; };   // my i-th tile (grouped order)
+  auto tile_mn = [&](int tau, int& m_t, int& n_t) {
+    const int g = tau / per, first = g * GM, gsz = min(mtiles - first, GM), q = tau - g * per;
     m_t = first + q % gsz;
     n_t = q / gsz;
   };
@@ -796,9 +870,10 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   for (int par = 0; par < 2; ++par) offB[par] = (uint32_t)(lane >> 3) * (uint32_t)(K * 2) + chunk_q[par];
   uint32_t offA[GA];
   int s_i = 0, s_kt = 0, s_n = 0;
-  auto set_stage = [&](int i) {
+  int pend = -1, pend_i = 0;                           // DYN (lane 0): fetch in flight, its ordinal
+  auto set_stage = [&](int tau) {
     int m_t, n_t;
-    tile_mn(i, m_t, n_t);
+    tile_mn(tau, m_t, n_t);
     s_n = n_t;
 #pragma unroll
     for (int j = 0; j < GA; ++j) {
@@ -821,12 +896,34 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   };
   // next staging K-tile; past my last tile: K-tile nt - 1 of it again (a DUMMY piece into a slot
   // nobody reads again, so every K-tile issues exactly G pieces: static vmcnt counts)
+  // DYN: the staging side moving onto ordinal s_i issues the fetch of ordinal s_i + 1 (lane 0,
+  // asynchronous); the next advance(), one K-tile and one counted vmcnt wait later, resolves it
+  // into tq -- read by every wave at the following tile switch, at least one K-tile (two barriers)
+  // later (nt >= 2, host check)
   auto advance = [&]() {
+    if constexpr (DYN) {
+      if (tid == 0 && pend_i > 0) {
+        asm volatile("" : "+v"(pend));              // not before this point (the vmcnt wait above)
+        tq[pend_i & 3] = pf_fetch(queue, xcd, tiles, pend);
+        pend_i = 0;
+      }
+    }
     if (++s_kt == nt) {
-      if (s_i + 1 < mine) {
+      const bool more = DYN ? tq[(s_i + 1) & 3] >= 0 : s_i + 1 < mine;
+      if (more) {
         ++s_i;
         s_kt = 0;
-        set_stage(s_i);
+        set_stage(tile_of(s_i));
+        if constexpr (DYN) {
+          if (tid == 0) {
+            if (pf_count(xcd, tiles) > 0) {
+              pend = pf_fetch_async(queue + 32 * xcd);
+            } else {
+              pend = 1 << 30;                          // no own partition: resolve by stealing
+            }
+            pend_i = s_i + 1;
+          }
+        }
       } else {
         s_kt = nt - 1;
       }
@@ -864,7 +961,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   };
 
   // prologue: the first NB K-tiles of my first tile in flight, K-tile 0 landed, its K-half 0 read
-  set_stage(0);
+  set_stage(tile_of(0));
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
 #pragma unroll
@@ -879,7 +976,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
 
   const int lr = lane & 15, lq = lane >> 4;
   int slot = 0;
-  for (int ti = 0; ti < mine; ++ti) {
+  for (int ti = 0; DYN ? ti <= s_i : ti < mine; ++ti) {   // DYN: s_i > ti once staging moved on
 #pragma unroll
     for (int i = 0; i < RT; ++i)
 #pragma unroll
@@ -931,7 +1028,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
     // stores, rows past M dropped by the range check (offset 0x80000000): no branch to hoist
     // accumulator reads over.
     int m_t, n_t;
-    tile_mn(ti, m_t, n_t);
+    tile_mn(tile_of(ti), m_t, n_t);
     const uint32_t colb = (uint32_t)(n_t * OUTW + wn * (OUTW / NWN) + 16 * (lq & 1) + 8 * (lq >> 1)) * 2;
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
@@ -976,11 +1073,42 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   }
   // the dummy pieces of the last K-tiles must land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (DYN) {
+    if (tid == 0) pf_retire(queue, P);
+  }
 }
 
+namespace {
+// one tile queue per (device, stream): launches on one stream run one after the other, so its
+// heads are back at zero (reset by the last workgroup of the previous launch) when the next starts
+int* pf_queue(hipStream_t s) {
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, int*> queues;
+  int dev = 0;
+  DLLM_HIP_CHECK(hipGetDevice(&dev));
+  const uint64_t key = ((uint64_t)(unsigned)dev << 56) ^ (uint64_t)(uintptr_t)s;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = queues.find(key);
+  if (it != queues.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  DLLM_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+  DLLM_HOST_CHECK(cs == hipStreamCaptureStatusNone, "gemm_pf's tile queue is created outside graph capture "
+                                                    "(run the GEMM once on this stream before capturing)");
+  int* q = nullptr;
+  DLLM_HIP_CHECK(hipMalloc(&q, PF_QUEUE_INTS * sizeof(int)));
+  DLLM_HIP_CHECK(hipMemsetAsync(q, 0, PF_QUEUE_INTS * sizeof(int), s));
+  queues.emplace(key, q);
+  return q;
+}
+}  // namespace
+
 // Persistent prefill GEMM: C = A B^T (mode 0) or SwiGLU (mode 1, C [M, N / 2], B = [Bg; Bu]),
-// 256 x 256 tiles, grid = min(tiles, CUs) rounded up to a multiple of 8.
+// 256 x 256 tiles, grid = min(tiles, CUs) rounded up to a multiple of 8.  variant bit 16: the
+// dynamic tile queue (DYN; needs K >= 128) instead of the static tile = w + i P walk.
 void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mode, int variant, uintptr_t stream) {
+  const bool dyn = (variant & 16) != 0;
+  variant &= ~16;
+  DLLM_HOST_CHECK(!dyn || K >= 2 * PBK, "the dynamic tile queue needs K >= 128");
   DLLM_HOST_CHECK(M >= 1, "M >= 1");
   DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
@@ -1007,12 +1135,26 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   DLLM_HOST_CHECK(variant >= 0 && variant <= 8 && (mode == 0 || variant == 0 || variant == 8),
                   "variant 0..8 (SwiGLU: 0 or 8)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int* q = dyn ? pf_queue(s) : nullptr;
 #define DLLM_PF_GO(MODE_, SCH_)                                                                               \
   hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a,     \
-                     (const bf16*)b, (bf16*)c, M, N, K)
-  if (mode == 1) {
+                     (const bf16*)b, (bf16*)c, M, N, K, q)
+#define DLLM_PF_GO_DYN(MODE_, SCH_)                                                                           \
+  hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_, true>), dim3((unsigned)grid), dim3(256), 0, s,               \
+                     (const bf16*)a, (const bf16*)b, (bf16*)c, M, N, K, q)
+  const bool nt_store = variant == 8 || (variant == 0 && (long)M * (N / 2) * 2 > (256L << 20));
+  if (dyn) {
+    DLLM_HOST_CHECK(variant == 0 || variant == 8, "the dynamic tile queue runs the shipped schedule (0 / 8)");
+    if (mode == 1) {
+      if (nt_store) DLLM_PF_GO_DYN(2, 8);
+      else DLLM_PF_GO_DYN(2, 0);
+    } else {
+      if (variant == 8) DLLM_PF_GO_DYN(0, 8);
+      else DLLM_PF_GO_DYN(0, 0);
+    }
+  } else if (mode == 1) {
     // variant 8 forces the nontemporal stores; by default they go with outputs > 256 MiB
-    if (variant == 8 || (variant == 0 && (long)M * (N / 2) * 2 > (256L << 20))) DLLM_PF_GO(2, 8);
+    if (nt_store) DLLM_PF_GO(2, 8);
     else DLLM_PF_GO(2, 0);
   } else {
     switch (variant) {
@@ -1028,6 +1170,7 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
     }
   }
 #undef DLLM_PF_GO
+#undef DLLM_PF_GO_DYN
   DLLM_HIP_CHECK(hipGetLastError());
 }
 

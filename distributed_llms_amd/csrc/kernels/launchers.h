@@ -67,4 +67,11 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
                              int hq, int hkv, int d, int block_size, int max_blocks, int max_q_len, float scale,
                              int version, uintptr_t stream);
 
+long p2p_inbox_bytes(long chunk, int nslots);
+void p2p_standin(uintptr_t src, uintptr_t s_inbox, long s_bytes, uint64_t s_seq0, uintptr_t dst, uintptr_t r_inbox,
+                 long r_bytes, uint64_t r_seq0, long chunk, int nslots, int channels, uintptr_t abort_word,
+                 double timeout_s, uintptr_t err, int lds_bytes, uintptr_t stream);
+uintptr_t p2p_host_words(int n);
+void p2p_host_words_free(uintptr_t p);
+
 }  // namespace dllm

@@ -33,6 +33,9 @@ class HostBatch:
     slot: int = 0
     step_id: int = 0
     sampling: Optional[np.ndarray] = None   # [B, 3] int32: temperature*1e4, top_k, top_p*1e4 (None = greedy)
+    # mixed prefill + decode step: the first num_decode sequences are single-token decode rows
+    # (decode attention), the rest prefill chunks (prefill attention); 0 = not mixed
+    num_decode: int = 0
     # the packed array this batch was unpacked from (its fields are views into it): pack() then
     # only refreshes the header instead of concatenating everything again
     raw: Optional[np.ndarray] = field(default=None, repr=False, compare=False)
@@ -56,7 +59,7 @@ class HostBatch:
         mb = self.block_tables.shape[1] if self.block_tables.ndim == 2 else 0
         has_s = 1 if self.sampling is not None else 0
         hdr = np.array([1 if self.is_prefill else 0, t, b, mb, self.max_q_len, self.max_ctx, self.slot,
-                        self.step_id, has_s] + [0] * 7, dtype=np.int32)
+                        self.step_id, has_s, self.num_decode] + [0] * 6, dtype=np.int32)
         parts = [hdr, self.ids, self.positions, self.slots, self.seq_lens, self.cu_seqlens,
                  self.block_tables.reshape(-1), self.logits_idx]
         if has_s:
@@ -73,7 +76,7 @@ class HostBatch:
     @staticmethod
     def unpack(arr: np.ndarray) -> "HostBatch":
         hdr = arr[:16]
-        pf, t, b, mb, mq, mc, slot, sid, has_s = (int(x) for x in hdr[:9])
+        pf, t, b, mb, mq, mc, slot, sid, has_s, nd = (int(x) for x in hdr[:10])
         o = 16
         def take(n):
             nonlocal o
@@ -85,7 +88,8 @@ class HostBatch:
         bt = take(b * mb).reshape(b, mb)
         lidx = take(b)
         samp = take(3 * b).reshape(b, 3) if has_s else None
-        return HostBatch(bool(pf), ids, pos, slots, seq_lens, cu, bt, lidx, mq, mc, slot, sid, samp, raw=arr)
+        return HostBatch(bool(pf), ids, pos, slots, seq_lens, cu, bt, lidx, mq, mc, slot, sid, samp, raw=arr,
+                         num_decode=nd)
 
 
 def next_pow2(x: int, lo: int = 1) -> int:
@@ -98,7 +102,12 @@ def next_pow2(x: int, lo: int = 1) -> int:
 def build_host_batch(step: Step, bm, block_size: int, max_blocks: Optional[int] = None,
                      step_id: int = 0) -> HostBatch:
     """Metadata of one step.  Decode steps of the native batcher arrive packed already (their
-    block-table width is the scheduler's ``max_blocks``); only the step id is stamped here."""
+    block-table width is the scheduler's ``max_blocks``); only the step id is stamped here.  A
+    mixed step is the decode rows' packed batch followed by its prefill chunk's (merge_mixed)."""
+    if getattr(step, "mixed", False):
+        dec = HostBatch.unpack(step.packed)
+        pre = build_host_batch(Step(True, step.seqs, step.slot), bm, block_size, None, step_id)
+        return merge_mixed(dec, pre, step.slot, step_id)
     if step.packed is not None:
         step.packed[7] = step_id
         return HostBatch.unpack(step.packed)
@@ -151,6 +160,30 @@ def build_host_batch(step: Step, bm, block_size: int, max_blocks: Optional[int] 
                      max_ctx, step.slot, step_id, sampling)
 
 
+def merge_mixed(dec: HostBatch, pre: HostBatch, slot: int, step_id: int) -> HostBatch:
+    """One HostBatch for a mixed step: decode rows (one token each) first, then the prefill
+    chunks; block tables padded to the wider of the two; runs the eager prefill path with
+    ``num_decode`` telling the attention which rows are decode rows."""
+    nd = dec.num_seqs
+    mb = max(dec.block_tables.shape[1], pre.block_tables.shape[1])
+    bt = np.zeros((nd + pre.num_seqs, mb), dtype=np.int32)
+    bt[:nd, : dec.block_tables.shape[1]] = dec.block_tables
+    bt[nd:, : pre.block_tables.shape[1]] = pre.block_tables
+    cu = np.concatenate([np.arange(nd, dtype=np.int32), pre.cu_seqlens.astype(np.int32) + nd])
+    sampling = None
+    if dec.sampling is not None or pre.sampling is not None:
+        zd = np.zeros((nd, 3), np.int32)
+        zp = np.zeros((pre.num_seqs, 3), np.int32)
+        sampling = np.concatenate([dec.sampling if dec.sampling is not None else zd,
+                                   pre.sampling if pre.sampling is not None else zp])
+    return HostBatch(True, np.concatenate([dec.ids, pre.ids]).astype(np.int32),
+                     np.concatenate([dec.positions, pre.positions]).astype(np.int32),
+                     np.concatenate([dec.slots, pre.slots]).astype(np.int32),
+                     np.concatenate([dec.seq_lens, pre.seq_lens]).astype(np.int32), cu, bt,
+                     np.concatenate([np.arange(nd, dtype=np.int32), pre.logits_idx.astype(np.int32) + nd]),
+                     max(1, pre.max_q_len), max(dec.max_ctx, pre.max_ctx), slot, step_id, sampling, num_decode=nd)
+
+
 def build_decode_batch(seq_ids: np.ndarray, seq_lens: np.ndarray, bm, block_size: int, max_blocks: int,
                        step_id: int = 0, slot: int = 0) -> HostBatch:
     """Decode HostBatch straight from arrays (lookahead path: the input ids are not known on the
@@ -187,4 +220,11 @@ def to_device_meta(hb: HostBatch, device, pad_ctx_to: Optional[int] = None) -> (
         logits_idx=up(hb.logits_idx, torch.int64) if hb.is_prefill else None,
         max_q_len=hb.max_q_len, max_ctx=pad_ctx_to or hb.max_ctx, num_seqs=hb.num_seqs,
         num_tokens=hb.num_tokens)
+    nd = hb.num_decode
+    if nd and hb.is_prefill:
+        # mixed step: the prefill rows' own cu_seqlens (from 0) and the decode rows' context bound
+        meta.num_decode = nd
+        meta.cu_seqlens_p = up(hb.cu_seqlens[nd:] - nd)
+        meta.max_ctx_d = int(hb.seq_lens[:nd].max())
+        meta.max_q_len_p = int((hb.cu_seqlens[nd + 1:] - hb.cu_seqlens[nd:-1]).max())
     return ids, meta

@@ -73,7 +73,8 @@ class LLMEngine:
         self.bm = make_block_manager(self.runner.num_blocks, ecfg.kv_block_size)
         # max_batch is the engine's total decode batch, split evenly over the slots
         per_slot = -(-ecfg.max_batch // self.num_slots)
-        self.scheduler = Scheduler(self.bm, self.num_slots, per_slot, ecfg.max_prefill_tokens, ecfg.max_seq_len)
+        self.scheduler = Scheduler(self.bm, self.num_slots, per_slot, ecfg.max_prefill_tokens, ecfg.max_seq_len,
+                                   ecfg.mixed_prefill_tokens)
         self.step_id = 0
         self.num_prefill_tokens = 0
         self.num_decode_tokens = 0

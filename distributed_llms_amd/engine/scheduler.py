@@ -27,13 +27,18 @@ class Step:
     """One microbatch: a prefill over ``seqs`` or a decode step.  Decode steps from the native
     batcher carry their sequence ids (``rows``), the packed batch metadata (``packed``, the
     HostBatch wire format) and, for lookahead steps, ``keep`` (positions of the rows in the slot's
-    previous step); ``seqs`` is then resolved lazily from the scheduler's registry."""
+    previous step); ``seqs`` is then resolved lazily from the scheduler's registry.
 
-    __slots__ = ("is_prefill", "_seqs", "slot", "rows", "packed", "keep", "_live")
+    A MIXED step (``mixed``; ``is_prefill`` is True: it runs the eager prefill path) carries both:
+    the slot's decode rows (``rows`` / ``packed``, one token each, first in the batch) and a bounded
+    prefill chunk over ``seqs``."""
+
+    __slots__ = ("is_prefill", "_seqs", "slot", "rows", "packed", "keep", "_live", "mixed")
 
     def __init__(self, is_prefill: bool, seqs: Optional[List[Sequence]] = None, slot: int = 0,
                  rows: Optional[np.ndarray] = None, packed: Optional[np.ndarray] = None,
-                 keep: Optional[np.ndarray] = None, live: Optional[Dict[int, Sequence]] = None):
+                 keep: Optional[np.ndarray] = None, live: Optional[Dict[int, Sequence]] = None,
+                 mixed: bool = False):
         self.is_prefill = is_prefill
         self._seqs = seqs
         self.slot = slot
@@ -41,21 +46,36 @@ class Step:
         self.packed = packed
         self.keep = keep
         self._live = live
+        self.mixed = mixed
 
     @property
     def seqs(self) -> List[Sequence]:
+        """The step's sequences (a mixed step: its PREFILL sequences; see decode_seqs)."""
         if self._seqs is None:
             live = self._live
             self._seqs = [live[int(i)] for i in self.rows]
         return self._seqs
 
     @property
+    def decode_seqs(self) -> List[Sequence]:
+        """A mixed step's decode sequences (in row order)."""
+        return [self._live[int(i)] for i in self.rows] if self.mixed else []
+
+    @property
+    def num_decode(self) -> int:
+        return len(self.rows) if self.mixed else 0
+
+    @property
     def size(self) -> int:
-        """Sequences (= rows) in the step."""
+        """Sequences (= logit rows) in the step."""
+        if self.mixed:
+            return len(self.rows) + len(self._seqs)
         return len(self.rows) if self.rows is not None else len(self._seqs)
 
     @property
     def num_tokens(self) -> int:
+        if self.mixed:
+            return len(self.rows) + sum(s.prefill_len for s in self._seqs)
         if self.is_prefill:
             return sum(s.prefill_len for s in self.seqs)
         return self.size
@@ -76,11 +96,16 @@ class Scheduler:
     MIN_CHUNK = 32          # smallest chunk worth starting in a step whose budget is nearly used
 
     def __init__(self, block_manager, num_slots: int = 1, max_batch: int = 256,
-                 max_prefill_tokens: int = 16384, max_seq_len: int = 4096):
+                 max_prefill_tokens: int = 16384, max_seq_len: int = 4096, mixed_prefill_tokens: int = 0):
+        """``mixed_prefill_tokens`` > 0: a slot with running sequences admits waiting prompts as a
+        chunk of at most this many tokens riding along with its decode rows (a mixed step) instead
+        of a prefill-only step that stalls every running sequence for a whole chunk."""
         self.bm = block_manager
         self.num_slots = max(1, num_slots)
         self.max_batch = max_batch
         self.max_prefill_tokens = max_prefill_tokens
+        self.mixed_prefill_tokens = max(0, int(mixed_prefill_tokens))
+        self.num_mixed = 0
         self.max_seq_len = max_seq_len
         self.max_blocks = -(-max_seq_len // block_manager.block_size)    # decode block-table width
         self.native = _ext.runtime().SlotBatcher(block_manager, self.num_slots, max_seq_len)
@@ -139,35 +164,55 @@ class Scheduler:
         return min(self.max_batch, -(-total // self.num_slots))
 
     # ------------------------------------------------------------ schedule
+    def _admit(self, slot: int, n_running: int, max_tokens: int):
+        """Admit waiting prompts (whole, or a chunk of the first one that does not fit) into a step
+        of at most ``max_tokens`` prompt tokens.  Returns (admitted, blocked on KV)."""
+        admitted: List[Sequence] = []
+        tokens = 0
+        target = self._admission_target()
+        blocked = False
+        while self.waiting and n_running + len(admitted) < target:
+            seq = self.waiting[0]
+            n = seq.total_len - seq.num_cached
+            budget = max_tokens - tokens
+            if n > budget:
+                # chunked prefill: a prompt longer than what is left of this step's token
+                # budget contributes a chunk; the rest follows in later steps (SURVEY §5.7)
+                if admitted and budget < min(n, self.MIN_CHUNK):
+                    break
+                if budget <= 0:
+                    break
+                n = budget
+            seq.chunk = n if n < seq.total_len - seq.num_cached else 0
+            if not self.bm.ensure_capacity(seq.seq_id, seq.num_cached + n):
+                seq.chunk = 0
+                blocked = True
+                break
+            self.waiting.popleft()
+            seq.status = SeqStatus.RUNNING
+            seq.slot = slot
+            admitted.append(seq)
+            tokens += n
+        return admitted, blocked
+
     def schedule(self, slot: int = 0, _retry: bool = True) -> Optional[Step]:
         n_running = self.native.num_running(slot)
+        if self.waiting and n_running and self.mixed_prefill_tokens:
+            # mixed step: the slot's decode rows first (they get KV before any new prompt), then a
+            # bounded chunk of waiting prompts in the same forward
+            res = self.native.build_decode(slot, self.max_blocks, 0, False)
+            self._sync_preempted()
+            if res is not None:
+                packed, rows, _ = res
+                admitted, _blocked = self._admit(slot, len(rows), self.mixed_prefill_tokens)
+                if admitted:
+                    self.num_prefilling += len(admitted)
+                    self.num_mixed += 1
+                    return Step(True, admitted, slot, rows=rows, packed=packed, live=self.live, mixed=True)
+                return Step(False, None, slot, rows=rows, packed=packed, live=self.live)
+            n_running = self.native.num_running(slot)
         if self.waiting:
-            admitted: List[Sequence] = []
-            tokens = 0
-            target = self._admission_target()
-            blocked = False
-            while self.waiting and n_running + len(admitted) < target:
-                seq = self.waiting[0]
-                n = seq.total_len - seq.num_cached
-                budget = self.max_prefill_tokens - tokens
-                if n > budget:
-                    # chunked prefill: a prompt longer than what is left of this step's token
-                    # budget contributes a chunk; the rest follows in later steps
-                    if admitted and budget < min(n, self.MIN_CHUNK):
-                        break
-                    if budget <= 0:
-                        break
-                    n = budget
-                seq.chunk = n if n < seq.total_len - seq.num_cached else 0
-                if not self.bm.ensure_capacity(seq.seq_id, seq.num_cached + n):
-                    seq.chunk = 0
-                    blocked = True
-                    break
-                self.waiting.popleft()
-                seq.status = SeqStatus.RUNNING
-                seq.slot = slot
-                admitted.append(seq)
-                tokens += n
+            admitted, blocked = self._admit(slot, n_running, self.max_prefill_tokens)
             if admitted:
                 self.num_prefilling += len(admitted)
                 return Step(True, admitted, slot)
@@ -255,6 +300,13 @@ class Scheduler:
                 return self._sync_finished(now)
             return []
         done = []
+        if step.mixed:
+            # decode rows first in the batch: their tokens go to the native batcher
+            toks = np.asarray(tokens, dtype=np.int32)
+            nd = len(step.rows)
+            if self.native.complete(step.slot, step.rows, np.ascontiguousarray(toks[:nd]), now):
+                done.extend(self._sync_finished(now))
+            tokens = toks[nd:]
         self.num_prefilling -= len(step.seqs)
         if hasattr(tokens, "tolist"):
             tokens = tokens.tolist()      # python ints once, not a numpy scalar per sequence

@@ -57,6 +57,9 @@ class Knobs:
     pp_swiglu_min_m: int = 257
     pp_proj_min_m: int = 257
     pp_persistent: bool = True
+    # gemm_pf pulls its tiles from per-XCD device queues (a workgroup that starts late -- its CU held
+    # by a co-resident RCCL / stand-in kernel -- finds them taken) instead of the static w + i P walk
+    pf_dynamic: bool = True
     # decode LM head (N > 65536) at pp_head_min_m <= M <= 256 on gemm_pp schedule 2 with nontemporal
     # weights: 230 vs 265 us for gemm_sq at M = 256 (Llama-3-8B); 0 = off
     pp_head_min_m: int = 225

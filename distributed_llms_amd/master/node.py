@@ -73,7 +73,9 @@ class MasterNode:
         self.running = False
         self.server_socket: Optional[socket.socket] = None
         self.proto = MessageProtocol()
-        self.state = "idle"                       # idle | ready | degraded
+        self.state = "idle"                       # idle | ready | degraded | failed
+        self._recovering = False                  # a recovery thread is running (guarded by _lock)
+        self.recover_timeout = 600.0              # seconds a recovery waits for replacement workers
         self.metrics = RequestMetrics()
         self._lock = threading.RLock()
         self._ids = itertools.count()
@@ -239,6 +241,7 @@ class MasterNode:
                     if ww:
                         self.proto.send_message(ww["socket"], "UNLOAD_SHARD", metadata={"pipeline": True})
                 if self.auto_recover:
+                    self._recovering = True
                     threading.Thread(target=self._recover_when_possible, daemon=True).start()
 
     def _fail_all(self, exc: Exception):
@@ -464,30 +467,44 @@ class MasterNode:
         log.info("pipeline ready: %s", {w: a.get("layer_range") for w, a in acks.items()})
         return acks
 
-    def _recover_when_possible(self, timeout: float = 600.0):
+    def _recover_when_possible(self, timeout: Optional[float] = None):
         """Re-admit a full set of stage workers (waits for replacements), reload the plan, then
-        re-run the parked requests from their prompts.  Failed attempts back off exponentially."""
-        t_end = time.time() + timeout
+        re-run the parked requests from their prompts.  Failed attempts back off exponentially.
+
+        ``_recovering`` is set (under the lock) by whoever starts this thread and cleared here under
+        the same lock as the final hand-over: on success together with the resubmission of the
+        parked requests, on give-up together with the state change to "failed" and the swap-out of
+        the parked list -- so a concurrent submit() either parks before that swap (and is failed or
+        resubmitted with the rest) or sees "failed" / "ready" and never parks into a list that
+        nobody will drain."""
+        t_end = time.time() + (self.recover_timeout if timeout is None else timeout)
         backoff = 0.5
-        while self.running and time.time() < t_end and self.state == "degraded":
+        try:
+            while self.running and time.time() < t_end and self.state == "degraded":
+                with self._lock:
+                    have = len(self.workers)
+                if have >= self.num_shards:
+                    try:
+                        self.shard_assignments = {}
+                        self.assign_shards()
+                        self.distribute_shards()
+                        log.info("pipeline recovered")
+                        self._resubmit_parked()
+                        return
+                    except Exception as e:
+                        log.error("recovery attempt failed: %s (next in %.1fs)", e, backoff)
+                        time.sleep(backoff)
+                        backoff = min(30.0, backoff * 2)
+                        continue
+                time.sleep(0.5)
+        finally:
             with self._lock:
-                have = len(self.workers)
-            if have >= self.num_shards:
-                try:
-                    self.shard_assignments = {}
-                    self.assign_shards()
-                    self.distribute_shards()
-                    log.info("pipeline recovered")
-                    self._resubmit_parked()
-                    return
-                except Exception as e:
-                    log.error("recovery attempt failed: %s (next in %.1fs)", e, backoff)
-                    time.sleep(backoff)
-                    backoff = min(30.0, backoff * 2)
-                    continue
-            time.sleep(0.5)
-        if self.state != "ready":
-            self._fail_all(WorkerFailure("pipeline did not recover"))
+                self._recovering = False
+                gave_up = self.state != "ready"
+                if gave_up:
+                    self.state = "failed"
+            if gave_up:
+                self._fail_all(WorkerFailure("pipeline did not recover"))
 
     # ---------------------------------------------------------------- inference
     def submit(self, prompt_ids: Sequence[int], params: Optional[Dict[str, Any]] = None, _stream_queue=None,
@@ -500,7 +517,7 @@ class MasterNode:
             # until the stage is re-admitted (plan.md:430-436) -- checked under the
             # lock that _resubmit_parked takes after the state is back to "ready", so a request
             # is either parked before the resubmission or sent directly after it
-            if self.state == "degraded" and self.auto_recover:
+            if self.state == "degraded" and self.auto_recover and self._recovering and self.running:
                 if len(self._retry) >= self.max_parked:
                     raise WorkerFailure(f"pipeline degraded and {len(self._retry)} requests already held")
                 self._retry.append({"ids": ids, "params": params, "attempts": 0, "hint": _task_out,

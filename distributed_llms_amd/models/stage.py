@@ -47,6 +47,13 @@ class BatchMeta:
     num_seqs: int = 0
     num_tokens: int = 0
     attn_workspace: Optional[tuple] = None
+    # mixed prefill + decode step (is_prefill True): sequences [0, num_decode) are one-token decode
+    # rows; cu_seqlens_p / max_q_len_p describe the prefill rows after them, max_ctx_d the decode
+    # rows' longest context
+    num_decode: int = 0
+    cu_seqlens_p: Optional[torch.Tensor] = None
+    max_ctx_d: int = 0
+    max_q_len_p: int = 0
 
 
 class KVCache:
@@ -310,6 +317,16 @@ class ModelStage:
             return o.view(o.shape[0], self.q_size_local)
         q = ops.rope_cache_append(qkv, meta.positions, self.cos_sin, k_cache, v_cache, meta.slot_mapping,
                                   self.hq, self.hkv, cfg.head_dim)
+        if meta.is_prefill and meta.num_decode:
+            # mixed step: decode rows through the split-KV decode kernel, prefill chunks through
+            # the prefill kernel (both read the cache the append above just completed)
+            nd = meta.num_decode
+            o = torch.empty_like(q)
+            ops.paged_attention_decode(q[:nd], k_cache, v_cache, meta.block_tables[:nd], meta.seq_lens[:nd],
+                                       self.scale, max_ctx=meta.max_ctx_d or None, out=o[:nd])
+            ops.paged_attention_prefill(q[nd:], k_cache, v_cache, meta.block_tables[nd:], meta.cu_seqlens_p,
+                                        meta.seq_lens[nd:], self.scale, max_q_len=meta.max_q_len_p, out=o[nd:])
+            return o.view(o.shape[0], self.q_size_local)
         if meta.is_prefill:
             o = ops.paged_attention_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_seqlens_q,
                                             meta.seq_lens, self.scale, max_q_len=meta.max_q_len)

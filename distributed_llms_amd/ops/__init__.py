@@ -2,9 +2,9 @@
 
 Device dispatch only (no backend choice on the GPU): a CUDA tensor always goes to the
 in-tree ``_C_kernels`` module and raises if it is not built -- there is no silent
-eager fallback on the GPU.  The single exception is the plain dense GEMM for large
-M (prefill), which is a library GEMM (hipBLASLt through ``torch.matmul``); small-M
-decode GEMMs run on the hand-written MFMA kernel (``linear``).
+eager fallback on the GPU.  Every GEMM of the forward path is hand-written too (ops/gemm.py:
+gemm_wide / gemm_sq for decode-sized M, the persistent gemm_pf for prefill-sized M); torch's
+F.linear remains only for shapes none of them takes (a bias, N not a multiple of 256).
 
 Every wrapper checks dtype/contiguity/shape on the host before launching, and launches
 on torch's current stream so the whole decode step can be captured in a HIP graph.
@@ -230,10 +230,19 @@ def decode_split_plan(batch: int, num_kv_heads: int, max_ctx: int, block_size: i
     return splits, split_len
 
 
+def _into(out: Optional[torch.Tensor], y: torch.Tensor) -> torch.Tensor:
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
 def paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale: float,
-                           max_ctx: Optional[int] = None, workspace: Optional[tuple] = None):
+                           max_ctx: Optional[int] = None, workspace: Optional[tuple] = None,
+                           out: Optional[torch.Tensor] = None):
+    """``out``: write the result there (a contiguous [B, Hq, D] view, e.g. rows of a mixed step)."""
     if not _gpu(q):
-        return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
+        return _into(out, ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale))
     _ck(q, "attn.q")
     _ck(k_cache, "k_cache")
     _ck(v_cache, "v_cache")
@@ -247,7 +256,10 @@ def paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale: f
     if max_ctx > max_blocks * bs:
         raise ValueError("max_ctx exceeds block table capacity")
     splits, split_len = decode_split_plan(b, hkv, max_ctx, bs, max_blocks)
-    out = torch.empty_like(q)
+    if out is None:
+        out = torch.empty_like(q)
+    elif out.shape != q.shape or not out.is_contiguous() or out.dtype != q.dtype:
+        raise ValueError("attention out must be a contiguous tensor shaped like q")
     po = pml = 0
     if splits > 1:
         if workspace is None:
@@ -330,10 +342,11 @@ def paged_attention_decode_rope(qkv, positions, cos_sin, k_cache, v_cache, slot_
 
 
 def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, scale: float,
-                            max_q_len: Optional[int] = None, version: int = 0):
-    """``version``: prefill kernel 1..5 (0: knobs.prefill_attn)."""
+                            max_q_len: Optional[int] = None, version: int = 0, out: Optional[torch.Tensor] = None):
+    """``version``: prefill kernel 1..5 (0: knobs.prefill_attn); ``out`` as paged_attention_decode."""
     if not _gpu(q):
-        return ref.paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, scale)
+        return _into(out, ref.paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens,
+                                                      scale))
     _ck(q, "attn.q")
     _ck(k_cache, "k_cache")
     _ck(v_cache, "v_cache")
@@ -344,7 +357,10 @@ def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq
     b = seq_lens.shape[0]
     if max_q_len is None:
         max_q_len = int((cu_seqlens_q[1:] - cu_seqlens_q[:-1]).max().item()) if b else 0
-    out = torch.empty_like(q)
+    if out is None:
+        out = torch.empty_like(q)
+    elif out.shape != q.shape or not out.is_contiguous() or out.dtype != q.dtype:
+        raise ValueError("attention out must be a contiguous tensor shaped like q")
     _ext.kernels().paged_attention_prefill(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                            block_tables.data_ptr(), cu_seqlens_q.data_ptr(), seq_lens.data_ptr(),
                                            b, hq, k_cache.shape[1], d, k_cache.shape[2], block_tables.shape[1],

@@ -223,7 +223,8 @@ def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, variant: i
     """Persistent prefill GEMM (gemm_pf in csrc/kernels/gemm_pp.hip): schedule 2's 256 x 256 tiles,
     one workgroup per CU walking its tiles with the LDS-DMA pipeline running across tile
     boundaries; optional fused SwiGLU (``w`` = [Wg; Wu], y [M, N / 2]).  ``variant`` 1-7: schedule
-    variants of the plain form for sweeps (csrc/kernels/gemm_pp.hip pf_sched)."""
+    variants of the plain form for sweeps (csrc/kernels/gemm_pp.hip pf_sched); the tiles come from
+    per-XCD device queues unless knobs.pf_dynamic is off (bit 16 of the launcher's variant)."""
     k = x.shape[-1]
     n = w.shape[0]
     m = x.numel() // k
@@ -232,6 +233,8 @@ def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, variant: i
     if n % 256 or k % 64:
         raise ValueError("linear_pf: N % 256 and K % 64")
     y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
+    if knobs.K.pf_dynamic and k >= 128 and variant in (0, 8):
+        variant |= 16                  # per-XCD dynamic tile queues (gemm_pp.hip, DYN)
     _ext.kernels().gemm_pf(y.data_ptr(), x.data_ptr(), w.data_ptr(), m, n, k, 1 if swiglu else 0, variant,
                            torch.cuda.current_stream().cuda_stream)
     return y

@@ -124,8 +124,10 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
                                cnt_p, off_p, e_loc, two_i, h, 1, rows, knobs.K.moe_variant, st)
             k.moe_grouped_gemm(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, 0,
                                rows, knobs.K.moe_variant, st)
-    elif x.dtype == torch.bfloat16 and two_i % 256 == 0 and h % 256 == 0 and inter % 64 == 0 and h % 64 == 0:
-        # prefill: one grouped launch per projection over every local expert's row tiles
+    elif x.dtype == torch.bfloat16 and two_i % 256 == 0 and h % 256 == 0 and inter % 64 == 0 and h % 64 == 0 \
+            and t * h * 2 < (1 << 32) and t * top_k * inter * 2 < (1 << 32):
+        # prefill: one grouped launch per projection over every local expert's row tiles (the kernel
+        # addresses each A operand with 32-bit buffer offsets: larger batches take the per-expert path)
         slots = t * top_k
         act = torch.empty(slots, inter, dtype=x.dtype, device=dev)
         k.gemm_pp_moe(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p, e_loc,

@@ -84,6 +84,9 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
     # per-rank device busy fraction over the timed rounds, and what the data plane ran on
     mine = {"busy": round(runner.busy_seconds() / elapsed, 4) if runner is not None else None}
     mine["transport"] = getattr(tp_, "kind", "none") if tp_ is not None else "none"
+    from . import rccl_standin
+    if mine["transport"] == "rccl" and rccl_standin.enabled():
+        mine["transport"] = "rccl-standin"          # the result was NOT measured over RCCL
     d = {k: hop1.get(k, 0) - hop0.get(k, 0) for k in hop1}
     mine["hop_tx"] = (d.get("hidden_tx", 0) + d.get("ids_tx", 0)) / elapsed   # device-plane bytes / s out
     mine["hop_rx"] = (d.get("hidden_rx", 0) + d.get("ids_rx", 0)) / elapsed

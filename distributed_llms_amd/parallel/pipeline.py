@@ -111,7 +111,7 @@ class PipelineDriver:
         self.bm = block_manager
         self.num_slots = num_slots or pipeline_slots(ecfg, transport.num_stages, runner.stage.device)
         self.scheduler = Scheduler(block_manager, self.num_slots, ecfg.max_batch, ecfg.max_prefill_tokens,
-                                   ecfg.max_seq_len)
+                                   ecfg.max_seq_len, ecfg.mixed_prefill_tokens)
         self.mcfg = runner.stage.cfg
         self.device = runner.stage.device
         self.inflight: Deque[_Issued] = collections.deque()           # issue order

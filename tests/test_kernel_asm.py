@@ -41,6 +41,15 @@ def test_pf_persistent_kernel_keeps_the_pipeline_full(pp_asm):
         scratch = int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", meta).group(1))
         assert scratch == 0, (name, scratch)
         assert "scratch_" not in body
-        waits = re.findall(r"s_waitcnt vmcnt\((\d+)\)", body)
-        assert waits.count("0") <= 1, (name, waits)
+        lines = body.split("\n")
+        # vmcnt(0) is allowed once (the final drain) -- and, in the dynamic-tile-queue form (template
+        # flag DYN, "Lb1E" in the mangled name), on the queue's own blocking paths (start, steal,
+        # retire: right behind its atomic or relaxed sc1 head load, lane 0 only), never in the
+        # K loop's pipeline itself
+        drains = [i for i, l in enumerate(lines) if "s_waitcnt vmcnt(0)" in l
+                  and not ("Lb1E" in name and any("global_atomic_add" in p or " sc1" in p
+                                                  for p in lines[max(0, i - 4): i]))]
+        assert len(drains) <= 1, (name, [lines[i - 2: i + 1] for i in drains])
+        if "Lb1E" in name:                 # the K loop's fetch is the asynchronous inline-asm one
+            assert "global_atomic_add" in body and "off sc0" in body
         assert body.count("v_mfma_f32_16x16x32_bf16") >= 128

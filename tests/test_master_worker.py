@@ -4,6 +4,7 @@ pipeline, request routing, heartbeat eviction and recovery (SURVEY §4.4 items 3
 import os
 import subprocess
 import sys
+import threading
 import time
 
 import pytest
@@ -201,3 +202,42 @@ def test_http_api_generate_completions_status_metrics(cluster):
         assert ei.value.code == 400
     finally:
         srv.shutdown()
+
+
+def test_recovery_timeout_fails_parked_and_later_requests():
+    """Recovery that never gets its replacement workers gives up: requests parked while it ran fail
+    with WorkerFailure, the state becomes "failed", and later submits raise instead of parking into
+    a list nobody drains (advisor round 4: park only while a recovery thread runs)."""
+    from distributed_llms_amd.master.node import MasterNode, WorkerFailure
+    m = MasterNode("127.0.0.1", 0, auto_recover=True).start()
+    try:
+        m.num_shards = 2
+        m.stage_workers = ["w0", "w1"]
+        with m._lock:                      # what _evict does when a stage worker dies
+            m.state = "degraded"
+            m._recovering = True
+        th = threading.Thread(target=m._recover_when_possible, kwargs={"timeout": 1.0}, daemon=True)
+        th.start()
+        parked = m.submit([1, 2, 3], {"max_new_tokens": 2})
+        assert not parked.done() and len(m._retry) == 1
+        th.join(10)
+        assert not th.is_alive()
+        assert m.state == "failed" and not m._recovering and m._retry == []
+        with pytest.raises(WorkerFailure):
+            parked.result(timeout=5)
+        with pytest.raises(WorkerFailure):
+            m.submit([4, 5], {"max_new_tokens": 2})
+    finally:
+        m.stop(shutdown_workers=False)
+
+
+def test_degraded_without_recovery_thread_does_not_park():
+    from distributed_llms_amd.master.node import MasterNode, WorkerFailure
+    m = MasterNode("127.0.0.1", 0, auto_recover=True).start()
+    try:
+        m.state = "degraded"               # no recovery thread running (e.g. it already returned)
+        with pytest.raises(WorkerFailure):
+            m.submit([1, 2], {"max_new_tokens": 1})
+        assert m._retry == []
+    finally:
+        m.stop(shutdown_workers=False)
