@@ -64,6 +64,9 @@ def parse(argv=None):
                     help="open-loop latency mode (1 GPU): requests arrive as a Poisson process of this many "
                          "requests/s (steps x batch requests in all) instead of a batch per round; reports "
                          "p50/p99 request latency, TTFT and ITL under that load (the headline mode is unchanged)")
+    ap.add_argument("--mixed-tokens", type=int, default=None,
+                    help="EngineConfig.mixed_prefill_tokens: prompt tokens a step may add to running decode "
+                         "rows (0 = prefill-first steps; default: the config's)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace", default=None, metavar="DIR",
                     help="record a roctx/host/GPU timeline of the timed steps: DIR/trace_rank<r>.json "
@@ -204,6 +207,8 @@ def run_open_loop(args):
                         max_prefill_tokens=max(16384, args.batch * args.prompt_len),
                         max_seq_len=args.prompt_len + args.gen_len + 32, use_graphs=not args.no_graphs,
                         seed=args.seed, streams=args.streams, quant=args.quant)
+    if args.mixed_tokens is not None:
+        ecfg = ecfg.apply_overrides(mixed_prefill_tokens=args.mixed_tokens)
     sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
     eng = LLMEngine(ecfg)
     params = SamplingParams(max_new_tokens=args.gen_len, ignore_eos=True)
@@ -242,7 +247,8 @@ def run_open_loop(args):
            "output_tok_per_s": round(n * args.gen_len / elapsed, 2), "dtype": "bf16" if args.quant == "none" else "fp8",
            "data": "synthetic (random-init weights, random prompt ids)",
            "config": {"model": args.model, "max_batch": args.batch, "prompt_len": args.prompt_len,
-                      "gen_len": args.gen_len}, "kernel_knobs": _knobs_changed(),
+                      "gen_len": args.gen_len, "mixed_prefill_tokens": ecfg.mixed_prefill_tokens},
+           "mixed_steps": eng.scheduler.num_mixed, "kernel_knobs": _knobs_changed(),
            **request_timing(*seq_timing(seqs))}
     line = json.dumps(rec)
     print(line, flush=True)

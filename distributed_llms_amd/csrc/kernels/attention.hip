@@ -597,7 +597,13 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
     bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
     const int32_t* __restrict__ cu_seqlens_q, const int32_t* __restrict__ seq_lens, int hq, int hkv,
-    int max_blocks, float scale_log2) {
+    int max_blocks, float scale_log2, const int32_t* __restrict__ positions, const float* __restrict__ cos_sin,
+    int q_stride) {
+  // q_stride: elements per token row of q ([T, hq, D]: hq * D; the raw qkv projection:
+  // (hq + 2 hkv) * D).  cos_sin != null: q is the UNROTATED projection -- each lane's fragments
+  // hold both rotate-half partners (dims 32 ks + 8 g + j and + D / 2), so RoPE is applied in
+  // registers right after the load, as in the fused decode kernel, and the rotated q never
+  // round-trips through HBM (rope_cache_kernel then appends K / V only)
   constexpr int R = 16 / G;                       // query rows per column tile
   constexpr int CH = 2 * kBS * D;                 // bf16 elements per staged chunk (K block + V^T block)
   constexpr int NB = 3;                           // ring depth
@@ -626,13 +632,15 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
     const int crow = row0 + t * R + r / G, ch = r % G;
     const bool ok = crow < ql;
     kmax_col[t] = ok ? qpos0 + crow : -1;
-    const bf16* qrow = q + ((size_t)(qs + (ok ? crow : 0)) * hq + kvh * G + ch) * D;
+    const int tok = qs + (ok ? crow : 0);
+    const bf16* qrow = q + (size_t)tok * q_stride + (size_t)(kvh * G + ch) * D;
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
       bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
       if (!ok) v = bf16x8{};
       qf[t][ks] = v;
     }
+    if (cos_sin != nullptr) rope_rotate<D, true>(qf[t], cos_sin + (size_t)positions[tok] * D, g);
     init_state(st[t]);
   }
   const int wg_kmax = qpos0 + min(wg_row0 + WV * R * NT, ql) - 1;
@@ -804,7 +812,7 @@ void paged_attention_decode_rope(uintptr_t out, uintptr_t qkv, uintptr_t positio
 template <int D>
 static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv, hipStream_t s, uintptr_t out,
                            uintptr_t q, uintptr_t k_cache, uintptr_t v_cache, uintptr_t bt, uintptr_t cu, uintptr_t sl,
-                           int hq, int max_blocks, float sl2) {
+                           int hq, int max_blocks, float sl2, uintptr_t pos, uintptr_t cs, int q_stride) {
   // version 1: v1 kernel; 2: v2 with one tile per wave (2 waves/SIMD); 3: v2 with two tiles per wave;
   // 4 / 5: the LDS-shared kernel with two / four tiles per wave
   const int nt = version == 5 ? 4 : (version == 3 || version == 4) ? 2 : 1;
@@ -815,11 +823,13 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
     if (version == 4)                                                                                       \
       hipLaunchKernelGGL((attn_prefill_lds_kernel<D, GG, 2>), grid, dim3(256), 0, s, (bf16*)out,              \
                          (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,      \
-                         (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2);                  \
+                         (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2,                   \
+                         (const int32_t*)pos, (const float*)cs, q_stride);                                   \
     else if (version == 5)                                                                                  \
       hipLaunchKernelGGL((attn_prefill_lds_kernel<D, GG, 4>), grid, dim3(256), 0, s, (bf16*)out,              \
                          (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,      \
-                         (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2);                  \
+                         (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2,                   \
+                         (const int32_t*)pos, (const float*)cs, q_stride);                                   \
     else if (version == 3)                                                                                  \
       hipLaunchKernelGGL((attn_prefill2_kernel<D, GG, 2>), grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,  \
                          (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt, (const int32_t*)cu,   \
@@ -844,11 +854,16 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
 #undef DLLM_PF
 }
 
+// positions / cos_sin / q_stride: q is the raw qkv projection (row stride q_stride elements) and RoPE
+// is applied in the kernel (LDS kernel, versions 4 / 5); cos_sin = 0: q is [T, hq, D], rotated
 void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
                              uintptr_t block_tables, uintptr_t cu_seqlens_q, uintptr_t seq_lens, int batch,
                              int hq, int hkv, int d, int block_size, int max_blocks, int max_q_len, float scale,
-                             int version, uintptr_t stream) {
+                             int version, uintptr_t positions, uintptr_t cos_sin, int q_stride, uintptr_t stream) {
   DLLM_HOST_CHECK(block_size == kBS, "paged attention requires block_size 32");
+  if (q_stride == 0) q_stride = hq * d;
+  DLLM_HOST_CHECK(q_stride >= hq * d && q_stride % 8 == 0, "q row stride");
+  DLLM_HOST_CHECK(cos_sin == 0 || positions != 0, "in-kernel RoPE needs positions");
   DLLM_HOST_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
   DLLM_HOST_CHECK(hq % hkv == 0, "Hq % Hkv");
   if (batch == 0 || max_q_len == 0) return;
@@ -861,12 +876,13 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
   DLLM_HOST_CHECK(version >= 1 && version <= 5, "prefill attention version 1..5");
   // the LDS kernel stages the block ids of a whole sequence: fall back beyond 32k context
   if (version >= 4 && max_blocks > kPfMaxChunks) version = 3;
+  DLLM_HOST_CHECK(q_stride == hq * d || version >= 4, "in-kernel RoPE / strided q: LDS kernel only (<= 32k context)");
   if (d == 128)
     launch_prefill<128>(G, version, max_q_len, batch, hkv, s, out, q, k_cache, v_cache, block_tables, cu_seqlens_q,
-                        seq_lens, hq, max_blocks, sl2);
+                        seq_lens, hq, max_blocks, sl2, positions, cos_sin, q_stride);
   else
     launch_prefill<64>(G, version, max_q_len, batch, hkv, s, out, q, k_cache, v_cache, block_tables, cu_seqlens_q,
-                       seq_lens, hq, max_blocks, sl2);
+                       seq_lens, hq, max_blocks, sl2, positions, cos_sin, q_stride);
   DLLM_HIP_CHECK(hipGetLastError());
 }
 

@@ -32,6 +32,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("gemm_pp_moe", &dllm::gemm_pp_moe);
   m.def("gemm_pp", &dllm::gemm_pp);
   m.def("gemm_pf", &dllm::gemm_pf);
+  m.def("gemm_pf_moe", &dllm::gemm_pf_moe);
   m.def("moe_combine", &dllm::moe_combine);
   m.def("moe_wide_gemm", &dllm::moe_wide_gemm);
   m.def("moe_router_route", &dllm::moe_router_route);

@@ -806,10 +806,16 @@ constexpr PfSched pf_sched(int sch) {
        : sch == 7 ? PfSched{40, 88, 0, 16} : PfSched{40, 88, 0, 8};
 }
 
-template <int MODE, int SCH = 0, bool DYN = false>
+// MOE: the grouped expert GEMM of the prefill (Mixtral) in this persistent form: A is the
+// expert-sorted activation [slots, K] (M = slots), B = W [E, N, K], C [slots, N (SwiGLU N / 2)];
+// the row tiles are every expert's segment of the slot space (counts read on the device into an
+// LDS table at the start -- no host sync), walked exactly as the dense tiles, with the expert's
+// weight selected by the B staging offset and rows past the segment dropped by the epilogue.
+template <int MODE, int SCH = 0, bool DYN = false, bool MOE = false>
 __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                          bf16* __restrict__ C, int M, int N, int K,
-                                                         int* __restrict__ queue) {
+                                                         int* __restrict__ queue, const int* __restrict__ counts,
+                                                         const int* __restrict__ offsets, int E) {
   constexpr int NW = 4, NWN = 2, BM = 256, BN = 256, TM = 128, TN = BN / NWN;
   constexpr int RT = TM / 16, CT = TN / 16;            // 8 x 8 accumulators per wave
   constexpr int SLOT = (BM + BN) * PBK, NB = 2;        // 2 x 64 KiB ring
@@ -820,12 +826,29 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) bf16 smem[NB * SLOT];
   __shared__ int tq[4];                                // DYN: tile of local ordinal i at [i & 3]
+  __shared__ int seg[3 * 17];                          // MOE: first row tile, slot offset, count per expert
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv / NWN, wn = wv % NWN;
   const int ldc = SWIGLU ? N / 2 : N;
-  const int ntn = N / BN, mtiles = (M + BM - 1) / BM, tiles = ntn * mtiles;
+  int mtiles = (M + BM - 1) / BM;
+  if constexpr (MOE) {
+    if (tid == 0) {
+      int t0 = 0;
+      for (int x = 0; x < E; ++x) {
+        const int c = counts[x];
+        seg[x] = t0;
+        seg[17 + x] = offsets[x];
+        seg[34 + x] = c;
+        t0 += (c + BM - 1) / BM;
+      }
+      seg[E] = t0;
+    }
+    __syncthreads();
+    mtiles = seg[E];
+  }
+  const int ntn = N / BN, tiles = ntn * mtiles;
   const int P = gridDim.x;                             // a multiple of 8 (host)
   const int w = (int)(blockIdx.x & 7) * (P >> 3) + (int)(blockIdx.x >> 3);
   const int xcd = (int)(blockIdx.x & 7);               // blocks are dealt round-robin over the XCDs
@@ -853,13 +876,29 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
     m_t = first + q % gsz;
     n_t = q / gsz;
   };
+  // the rows of (virtual) row tile m_t: [r0, min(r0 + BM, rcnt)) of the segment starting at slot
+  // roff, weight of expert ex (dense: one segment, rows 0 .. M)
+  auto rows_of = [&](int m_t, int& r0, int& rcnt, int& roff, int& ex) {
+    if constexpr (MOE) {
+      ex = 0;
+      for (int x = 1; x < E; ++x) ex = m_t >= seg[x] ? x : ex;
+      r0 = (m_t - seg[ex]) * BM;
+      roff = seg[17 + ex];
+      rcnt = seg[34 + ex];
+    } else {
+      r0 = m_t * BM;
+      roff = 0;
+      rcnt = M;
+      ex = 0;
+    }
+  };
 
   // ---- staging side: tile s_i's K-tile s_kt; per-lane A row offsets of that tile (rows past M
   // clamp to M - 1), B rows through the SGPR offset (uniform per piece)
   const __amdgpu_buffer_rsrc_t rsA =
       __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)(unsigned)((long)M * K * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)(unsigned)((long)N * K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)B, (short)0, (int)(unsigned)((long)(MOE ? E : 1) * N * K * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsC =
       __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, (int)(unsigned)((long)M * ldc * 2), 0x00020000);
   uint32_t chunk_q[2];
@@ -870,15 +909,19 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   for (int par = 0; par < 2; ++par) offB[par] = (uint32_t)(lane >> 3) * (uint32_t)(K * 2) + chunk_q[par];
   uint32_t offA[GA];
   int s_i = 0, s_kt = 0, s_n = 0;
+  uint32_t s_boff = 0;                                 // MOE: byte offset of the staging tile's expert weight
   int pend = -1, pend_i = 0;                           // DYN (lane 0): fetch in flight, its ordinal
   auto set_stage = [&](int tau) {
     int m_t, n_t;
     tile_mn(tau, m_t, n_t);
     s_n = n_t;
+    int r0, rcnt, roff, ex;
+    rows_of(m_t, r0, rcnt, roff, ex);
+    if constexpr (MOE) s_boff = (uint32_t)ex * (uint32_t)N * (uint32_t)(K * 2);
 #pragma unroll
     for (int j = 0; j < GA; ++j) {
       const int q = wv * GA + j, r = 8 * q + (lane >> 3);
-      offA[j] = (uint32_t)min(m_t * BM + r, M - 1) * (uint32_t)(K * 2) + chunk_q[q & 1];
+      offA[j] = (uint32_t)(roff + min(r0 + r, rcnt - 1)) * (uint32_t)(K * 2) + chunk_q[q & 1];
     }
   };
   // piece p of the staging K-tile into ring slot `slot`
@@ -891,7 +934,8 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
       const int q = wv * GB + p - GA;
       const uint32_t brow = (uint32_t)pp_b_row<BN, SWIGLU>(8 * q, s_n, N / 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_vptr_p)(base + BM * PBK + q * 512), 16, (int)offB[q & 1],
-                                               (int)(brow * (uint32_t)(K * 2) + (uint32_t)(s_kt * PBK * 2)), 0, 0);
+                                               (int)(brow * (uint32_t)(K * 2) + (uint32_t)(s_kt * PBK * 2) + s_boff),
+                                               0, 0);
     }
   };
   // next staging K-tile; past my last tile: K-tile nt - 1 of it again (a DUMMY piece into a slot
@@ -1029,6 +1073,8 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
     // accumulator reads over.
     int m_t, n_t;
     tile_mn(tile_of(ti), m_t, n_t);
+    int e_r0, e_rcnt, e_roff, e_ex;
+    rows_of(m_t, e_r0, e_rcnt, e_roff, e_ex);
     const uint32_t colb = (uint32_t)(n_t * OUTW + wn * (OUTW / NWN) + 16 * (lq & 1) + 8 * (lq >> 1)) * 2;
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
@@ -1036,8 +1082,8 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
       // at the K loop's exit (and spill, draining the pipeline with vmcnt(0) waits)
 #pragma unroll
       for (int c = 0; c < CT; ++c) asm volatile("" : "+a"(acc[r][c]));
-      const int row = m_t * BM + wm * TM + r * 16 + lr;
-      const uint32_t vo = row < M ? (uint32_t)row * (uint32_t)(ldc * 2) + colb : 0x80000000u;
+      const int row = e_r0 + wm * TM + r * 16 + lr;       // row within the segment
+      const uint32_t vo = row < e_rcnt ? (uint32_t)(e_roff + row) * (uint32_t)(ldc * 2) + colb : 0x80000000u;
       constexpr int NQ = SWIGLU ? CT / 2 : CT;         // bf16 quads per lane in this row group
       u32x2 q[NQ];
 #pragma unroll
@@ -1138,10 +1184,10 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   int* q = dyn ? pf_queue(s) : nullptr;
 #define DLLM_PF_GO(MODE_, SCH_)                                                                               \
   hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a,     \
-                     (const bf16*)b, (bf16*)c, M, N, K, q)
+                     (const bf16*)b, (bf16*)c, M, N, K, q, (const int*)nullptr, (const int*)nullptr, 1)
 #define DLLM_PF_GO_DYN(MODE_, SCH_)                                                                           \
   hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_, true>), dim3((unsigned)grid), dim3(256), 0, s,               \
-                     (const bf16*)a, (const bf16*)b, (bf16*)c, M, N, K, q)
+                     (const bf16*)a, (const bf16*)b, (bf16*)c, M, N, K, q, (const int*)nullptr, (const int*)nullptr, 1)
   const bool nt_store = variant == 8 || (variant == 0 && (long)M * (N / 2) * 2 > (256L << 20));
   if (dyn) {
     DLLM_HOST_CHECK(variant == 0 || variant == 8, "the dynamic tile queue runs the shipped schedule (0 / 8)");
@@ -1171,6 +1217,39 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   }
 #undef DLLM_PF_GO
 #undef DLLM_PF_GO_DYN
+  DLLM_HIP_CHECK(hipGetLastError());
+}
+
+// Persistent grouped-expert prefill GEMM (gemm_pf MOE): y [slots, N] (SwiGLU [slots, N / 2]) =
+// xs [slots, K] (expert-sorted: slot rows of expert e at [offsets[e], offsets[e] + counts[e]))
+// times W[e]^T ([E, N, K]; SwiGLU [E, 2I, K] = [Wg; Wu] per expert).  Dynamic tile queue,
+// 256 x 256 tiles, counts / offsets read on the device (expert parallelism: the local experts'
+// slices of the routing arrays; other experts' slot rows are left untouched).
+void gemm_pf_moe(uintptr_t y, uintptr_t xs, uintptr_t w, uintptr_t counts, uintptr_t offsets, int E, int N, int K,
+                 int slots, int mode, uintptr_t stream) {
+  DLLM_HOST_CHECK(E >= 1 && E <= 16, "1 <= experts <= 16");
+  DLLM_HOST_CHECK(K % PBK == 0 && K >= 2 * PBK, "K must be a multiple of 64, >= 128");
+  DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
+  DLLM_HOST_CHECK(slots >= 1, "slots");
+  DLLM_HOST_CHECK((long)slots * K * 2 < (1L << 32) && (long)E * N * K * 2 < (1L << 32) &&
+                      (long)slots * (mode == 1 ? N / 2 : N) * 2 < (1L << 31),
+                  "operands must be < 4 GiB, the output < 2 GiB");
+  int dev = 0;
+  DLLM_HIP_CHECK(hipGetDevice(&dev));
+  int cus = 0;
+  DLLM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  if (cus <= 0) cus = 256;
+  const long bound = (long)(N / 256) * ((slots + 255) / 256 + E);     // tiles upper bound
+  const long grid = ((bound < cus ? bound : cus) + 7) / 8 * 8;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int* q = pf_queue(s);
+  if (mode == 1)
+    hipLaunchKernelGGL((gemm_pf_kernel<2, 0, true, true>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)xs,
+                       (const bf16*)w, (bf16*)y, slots, N, K, q, (const int*)counts, (const int*)offsets, E);
+  else
+    hipLaunchKernelGGL((gemm_pf_kernel<0, 0, true, true>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)xs,
+                       (const bf16*)w, (bf16*)y, slots, N, K, q, (const int*)counts, (const int*)offsets, E);
   DLLM_HIP_CHECK(hipGetLastError());
 }
 

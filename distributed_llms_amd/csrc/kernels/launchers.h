@@ -37,6 +37,8 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
 void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets, int E,
                  int N, int K, int xrows, int slots, int mode, uintptr_t stream);
 void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mode, int variant, uintptr_t stream);
+void gemm_pf_moe(uintptr_t y, uintptr_t xs, uintptr_t w, uintptr_t counts, uintptr_t offsets, int E, int N, int K,
+                 int slots, int mode, uintptr_t stream);
 int gemm_sq(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream);
 
@@ -65,7 +67,7 @@ void paged_attention_decode_rope(uintptr_t out, uintptr_t qkv, uintptr_t positio
 void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
                              uintptr_t block_tables, uintptr_t cu_seqlens_q, uintptr_t seq_lens, int batch,
                              int hq, int hkv, int d, int block_size, int max_blocks, int max_q_len, float scale,
-                             int version, uintptr_t stream);
+                             int version, uintptr_t positions, uintptr_t cos_sin, int q_stride, uintptr_t stream);
 
 long p2p_inbox_bytes(long chunk, int nslots);
 void p2p_standin(uintptr_t src, uintptr_t s_inbox, long s_bytes, uint64_t s_seq0, uintptr_t dst, uintptr_t r_inbox,

@@ -138,8 +138,9 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ q_ou
   const int blk = slot / bs, off = slot % bs;
   const bf16* row = qkv + (size_t)t * (hq + 2 * hkv) * d;
   const float* cs = cos_sin ? cos_sin + (size_t)pos * d : nullptr;
-  // q and k: rotate
-  for (int i = threadIdx.x; i < (hq + hkv) * qpr; i += blockDim.x) {
+  // q and k: rotate (q_out null: the attention kernel rotates q itself -- K / V only here)
+  const int h0 = q_out ? 0 : hq;
+  for (int i = threadIdx.x + h0 * qpr; i < (hq + hkv) * qpr; i += blockDim.x) {
     const int h = i / qpr, p = (i % qpr) * 4;
     const bf16* src = row + h * d;
     bf16x4 x1 = *reinterpret_cast<const bf16x4*>(src + p);

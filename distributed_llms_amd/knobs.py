@@ -66,6 +66,9 @@ class Knobs:
     # ---- attention (ops/__init__.py)
     attn_target_waves: int = 1024     # decode split-KV: waves to aim for (profiles/attn_decode_sweep.txt)
     prefill_attn: int = 4             # prefill kernel version 1..5 (4: LDS-shared K/V tiles)
+    # prefill q-RoPE in the attention kernel's q load (rope_cache appends K / V only): no rotated-q
+    # round trip through HBM (268 MB per layer at T = 32768)
+    prefill_fused_rope: bool = True
     # ---- model / engine
     fused_rope: bool = True           # decode: RoPE + KV append fused into attention
     # split-K qkv partials summed inside the fused RoPE + attention kernel (no splitk_reduce launch):
@@ -79,6 +82,8 @@ class Knobs:
     moe_variant: int = 0
     moe_wide_min_pairs: int = 8       # token-expert pairs per expert from which the tiled GEMM serves
     moe_fused_router: bool = True
+    # prefill grouped expert GEMMs on the persistent gemm_pf (MOE form) instead of gemm_pp_moe
+    moe_persistent: bool = True
     # grouped expert GEMM ring depth: 6 / 5 LDS slots at 64 / 128-row tiles (False: 3 slots)
     moe_deep_ring: bool = True
     # ---- FP8 W8A8 (ops/quant.py)

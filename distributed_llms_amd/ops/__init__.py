@@ -24,6 +24,7 @@ __all__ = [
     "embedding", "rms_norm", "fused_add_rms_norm", "layer_norm", "linear", "silu_mul",
     "gelu_tanh", "rope_cache_append", "paged_attention_decode", "paged_attention_prefill",
     "argmax", "add_", "moe_route", "moe_mlp", "decode_split_plan", "paged_attention_decode_rope",
+    "paged_attention_prefill_rope",
 ]
 
 
@@ -183,10 +184,13 @@ def silu_mul(gu: torch.Tensor) -> torch.Tensor:
 
 # ----------------------------------------------------------- K4 + K5
 def rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, num_heads, num_kv_heads,
-                      head_dim) -> torch.Tensor:
+                      head_dim, write_q: bool = True) -> Optional[torch.Tensor]:
+    """Rotate k (and q) and append k / v^T to the paged cache; returns the rotated q [T, Hq, D], or
+    None with ``write_q=False`` (the prefill attention then rotates q itself)."""
     if not _gpu(qkv):
-        return ref.rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, num_heads,
-                                     num_kv_heads, head_dim)
+        q = ref.rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, num_heads,
+                                  num_kv_heads, head_dim)
+        return q if write_q else None
     _ck(qkv, "rope.qkv")
     _ck(k_cache, "k_cache")
     _ck(v_cache, "v_cache")
@@ -199,8 +203,8 @@ def rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, n
         _ck(cos_sin, "cos_sin", torch.float32)
         if cos_sin.shape[1] != head_dim:
             raise ValueError("cos_sin width must equal head_dim")
-    q = torch.empty(t, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
-    _ext.kernels().rope_cache_append(q.data_ptr(), qkv.data_ptr(), positions.data_ptr(),
+    q = torch.empty(t, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device) if write_q else None
+    _ext.kernels().rope_cache_append(q.data_ptr() if write_q else 0, qkv.data_ptr(), positions.data_ptr(),
                                      0 if cos_sin is None else cos_sin.data_ptr(), k_cache.data_ptr(),
                                      v_cache.data_ptr(), slot_mapping.data_ptr(), t, num_heads, num_kv_heads,
                                      head_dim, k_cache.shape[2], _stream())
@@ -364,7 +368,51 @@ def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq
     _ext.kernels().paged_attention_prefill(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                            block_tables.data_ptr(), cu_seqlens_q.data_ptr(), seq_lens.data_ptr(),
                                            b, hq, k_cache.shape[1], d, k_cache.shape[2], block_tables.shape[1],
-                                           int(max_q_len), float(scale), version or knobs.K.prefill_attn, _stream())
+                                           int(max_q_len), float(scale), version or knobs.K.prefill_attn, 0, 0, 0,
+                                           _stream())
+    return out
+
+
+def prefill_rope_in_attention() -> bool:
+    """Prefill q-RoPE inside the attention kernel (knobs.prefill_fused_rope; LDS kernel versions)."""
+    return knobs.K.prefill_fused_rope and knobs.K.prefill_attn in (4, 5)
+
+
+def paged_attention_prefill_rope(qkv, positions, cos_sin, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens,
+                                 num_heads: int, head_dim: int, scale: float, max_q_len: Optional[int] = None,
+                                 out: Optional[torch.Tensor] = None):
+    """Prefill attention reading q straight from the qkv projection [T, (Hq + 2 Hkv) * D] and rotating it
+    in registers (K / V already appended by ``rope_cache_append(..., write_q=False)``): the rotated q
+    never round-trips through HBM.  Returns [T, Hq, D]."""
+    hkv = k_cache.shape[1]
+    t, width = qkv.shape
+    if not _gpu(qkv):
+        q = ref.rope_q(qkv, positions, cos_sin, num_heads, head_dim)
+        return _into(out, ref.paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens,
+                                                      scale))
+    _ck(qkv, "attn.qkv")
+    _ck(k_cache, "k_cache")
+    _ck(v_cache, "v_cache")
+    _ck(block_tables, "block_tables", torch.int32)
+    _ck(cu_seqlens_q, "cu_seqlens_q", torch.int32)
+    _ck(seq_lens, "seq_lens", torch.int32)
+    _ck(positions, "positions", torch.int32)
+    if width != (num_heads + 2 * hkv) * head_dim:
+        raise ValueError("qkv width mismatch")
+    if cos_sin is not None:
+        _ck(cos_sin, "cos_sin", torch.float32)
+    if not prefill_rope_in_attention():
+        raise ValueError("in-kernel prefill RoPE needs the LDS prefill kernel (knobs.prefill_attn 4 / 5)")
+    b = seq_lens.shape[0]
+    if max_q_len is None:
+        max_q_len = int((cu_seqlens_q[1:] - cu_seqlens_q[:-1]).max().item()) if b else 0
+    if out is None:
+        out = torch.empty(t, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
+    _ext.kernels().paged_attention_prefill(out.data_ptr(), qkv.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                           block_tables.data_ptr(), cu_seqlens_q.data_ptr(), seq_lens.data_ptr(),
+                                           b, num_heads, hkv, head_dim, k_cache.shape[2], block_tables.shape[1],
+                                           int(max_q_len), float(scale), knobs.K.prefill_attn, positions.data_ptr(),
+                                           0 if cos_sin is None else cos_sin.data_ptr(), width, _stream())
     return out
 
 

@@ -9,6 +9,7 @@ GPU path (bf16):
                    gemm_pp_moe: one launch per projection, every expert's row tiles in one grid,
                    counts / offsets read on the device -- no host sync, no per-expert loop; gate|up
                    with the SwiGLU in its epilogue, the token gather in its A staging)
+  W8A8 experts   : the grouped fp8 kernel (moe_wide_gemm_fp8) at every T, also without a host sync
   moe_combine    : weighted sum of each token's top-k expert outputs        (HIP)
 CPU path: the PyTorch reference (ops/reference.py).
 """
@@ -93,22 +94,17 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
         # slot order), SwiGLU output re-quantized per slot row for the down projection
         if x.dtype != torch.bfloat16 or two_i % 128 or h % 128 or inter % 128:
             raise ValueError("moe fp8: bf16 activations, expert dims multiples of 128")
-        if t <= GROUPED_MAX_TOKENS:
-            xq, xsc = quant.quantize_rows(x)
-            sa = xsc.index_select(0, sorted_tok.long())
-            act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
-            k.moe_wide_gemm_fp8(act.data_ptr(), xq.data_ptr(), sorted_tok.data_ptr(), w_gate_up.q.data_ptr(), cnt_p,
-                                off_p, e_loc, two_i, h, 1, sa.data_ptr(), w_gate_up.scale.data_ptr(), st)
-            aq, asc = quant.quantize_rows(act)
-            k.moe_wide_gemm_fp8(ys.data_ptr(), aq.data_ptr(), 0, w_down.q.data_ptr(), cnt_p, off_p, e_loc, h, inter,
-                                0, asc.data_ptr(), w_down.scale.data_ptr(), st)
-        else:
-            xs = x.index_select(0, sorted_tok.long())
-            off = offsets.cpu().tolist()      # prefill only: eager, host sync is fine here
-            for j in range(e_loc):
-                a, b = off[expert_offset + j], off[expert_offset + j + 1]
-                if b > a:
-                    ys[a:b] = quant.linear_fp8(quant.linear_fp8(xs[a:b], w_gate_up[j], swiglu=True), w_down[j])
+        # one grouped launch per projection at every T (decode and prefill): each workgroup walks its
+        # expert's row chunks for one column tile, counts / offsets read on the device -- no host
+        # sync, no per-expert loop (round-4 review: the prefill used to loop over experts on the host)
+        xq, xsc = quant.quantize_rows(x)
+        sa = xsc.index_select(0, sorted_tok.long())
+        act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
+        k.moe_wide_gemm_fp8(act.data_ptr(), xq.data_ptr(), sorted_tok.data_ptr(), w_gate_up.q.data_ptr(), cnt_p,
+                            off_p, e_loc, two_i, h, 1, sa.data_ptr(), w_gate_up.scale.data_ptr(), st)
+        aq, asc = quant.quantize_rows(act)
+        k.moe_wide_gemm_fp8(ys.data_ptr(), aq.data_ptr(), 0, w_down.q.data_ptr(), cnt_p, off_p, e_loc, h, inter,
+                            0, asc.data_ptr(), w_down.scale.data_ptr(), st)
     elif t <= GROUPED_MAX_TOKENS:
         act = torch.empty(t * top_k, inter, dtype=x.dtype, device=dev)
         rows = -(-t * top_k // e)        # expected rows per expert picks the kernel's row tile
@@ -130,10 +126,19 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
         # addresses each A operand with 32-bit buffer offsets: larger batches take the per-expert path)
         slots = t * top_k
         act = torch.empty(slots, inter, dtype=x.dtype, device=dev)
-        k.gemm_pp_moe(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p, e_loc,
-                      two_i, h, t, slots, 1, st)
-        k.gemm_pp_moe(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, slots,
-                      slots, 0, st)
+        if knobs.K.moe_persistent and e_loc <= 16 and h >= 128 and inter >= 128:
+            # persistent form (gemm_pf MOE: dynamic tile queue, LDS-DMA ring continuous across tiles):
+            # the token rows gathered into slot order first (the embedding kernel is a row gather)
+            from . import embedding
+            xs = embedding(sorted_tok, x)
+            k.gemm_pf_moe(act.data_ptr(), xs.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p, e_loc, two_i, h, slots, 1,
+                          st)
+            k.gemm_pf_moe(ys.data_ptr(), act.data_ptr(), w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, slots, 0, st)
+        else:
+            k.gemm_pp_moe(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p,
+                          e_loc, two_i, h, t, slots, 1, st)
+            k.gemm_pp_moe(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, slots,
+                          slots, 0, st)
     else:
         # odd expert dims (test-size models): per-expert GEMMs, counts read on the host
         xs = x.index_select(0, sorted_tok.long())

@@ -103,6 +103,14 @@ def apply_rope(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor) -> tor
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
 
 
+def rope_q(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional[torch.Tensor], num_heads: int,
+           head_dim: int) -> torch.Tensor:
+    """The rotated q [T, Hq, D] of a fused qkv projection."""
+    t = qkv.shape[0]
+    q = qkv[:, : num_heads * head_dim].view(t, num_heads, head_dim)
+    return apply_rope(q, positions, cos_sin) if cos_sin is not None else q.contiguous()
+
+
 def rope_cache_append(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional[torch.Tensor],
                       k_cache: torch.Tensor, v_cache: torch.Tensor, slot_mapping: torch.Tensor,
                       num_heads: int, num_kv_heads: int, head_dim: int) -> torch.Tensor:

@@ -5,10 +5,13 @@
 set -o pipefail
 mkdir -p gpurun_out
 T="timeout -k 10"
-$T 600 python -u -m pytest -x -v -s --timeout 240 --timeout-method thread tests/test_rccl_standin_gpu.py \
+$T 700 python -u -m pytest -x -v -s --timeout 240 --timeout-method thread tests/test_rccl_standin_gpu.py \
   "tests/test_pipeline_gpu.py::test_multiprocess_gpu_pipeline_rccl_transport_standin" \
   "tests/test_pipeline_gpu.py::test_multiprocess_gpu_pipeline_ipc" \
-  tests/test_gemm_gpu.py -k "standin or gemm_pf or pf_ or ipc" > gpurun_out/r5b_tests.log 2>&1 \
+  "tests/test_engine_gpu.py::test_mixed_prefill_decode_steps_gpu" \
+  tests/test_kernels_gpu.py tests/test_gemm_gpu.py tests/test_moe_gpu.py \
+  -k "standin or gemm_pf or pf_ or ipc or mixed or prefill or persistent" \
+  > gpurun_out/r5b_tests.log 2>&1 \
   || { echo "tests failed"; tail -60 gpurun_out/r5b_tests.log; exit 1; }
 grep -E "passed|failed|gemm_pf solo|static walk" gpurun_out/r5b_tests.log | tail -8
 export DLLM_SHARE_GPU=1 DLLM_DATA_BACKEND=gloo

@@ -201,3 +201,36 @@ def test_decode_rope_consumes_splitk_qkv_bit_exact(cuda, b):
     torch.testing.assert_close(o1, o2, atol=0, rtol=0)
     torch.testing.assert_close(k1, k2, atol=0, rtol=0)
     torch.testing.assert_close(v1, v2, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (8, 4, 64)])
+def test_prefill_attention_with_q_rope_in_kernel(cuda, hq, hkv, d):
+    """knobs.prefill_fused_rope: rope_cache_append(write_q=False) appends K / V only and the LDS prefill
+    kernel rotates q from the raw qkv projection in registers.  Same cache contents, and the attention
+    output matches the two-pass form (rotated q written, then attended) and the fp32 reference."""
+    from distributed_llms_amd import knobs
+    ctx = [37, 128, 300, 5]
+    qlen = [37, 64, 1, 5]
+    t = sum(qlen)
+    k1, v1, bt = _fill_paged(ctx, hkv, d)
+    k2, v2 = k1.clone(), v1.clone()
+    cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32, device="cuda")
+    sl = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+    pos = torch.cat([torch.arange(c - q, c) for c, q in zip(ctx, qlen)]).to(torch.int32).cuda()
+    # the new tokens' slots: the positions' places in each sequence's blocks
+    btc = bt.cpu()
+    slots = torch.tensor([int(btc[i, p // 32]) * 32 + p % 32 for i, (c, q) in enumerate(zip(ctx, qlen))
+                          for p in range(c - q, c)], dtype=torch.int32, device="cuda")
+    qkv = _bf(t, (hq + 2 * hkv) * d)
+    cs = ref.rope_cos_sin(d, 1024, 500000.0, device="cuda")
+    scale = 1 / math.sqrt(d)
+    with knobs.override(prefill_attn=4, prefill_fused_rope=True):
+        q = ops.rope_cache_append(qkv, pos, cs, k1, v1, slots, hq, hkv, d)
+        two_pass = ops.paged_attention_prefill(q, k1, v1, bt, cu, sl, scale)
+        assert ops.rope_cache_append(qkv, pos, cs, k2, v2, slots, hq, hkv, d, write_q=False) is None
+        fused = ops.paged_attention_prefill_rope(qkv, pos, cs, k2, v2, bt, cu, sl, hq, d, scale, max_q_len=max(qlen))
+    assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    torch.testing.assert_close(fused.float(), two_pass.float(), atol=4e-3, rtol=4e-3)
+    expect = ref.paged_attention_prefill(ref.rope_q(qkv.float(), pos, cs, hq, d), k1.float(), v1.float(), bt, cu,
+                                         sl, scale)
+    torch.testing.assert_close(fused.float(), expect, atol=2e-2, rtol=2e-2)

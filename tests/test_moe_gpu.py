@@ -191,3 +191,53 @@ def test_moe_prefill_has_no_host_sync(cuda):
     tw, tid = ref.moe_route(ref.linear(x, wr).float(), k)
     expect = ref.moe_mlp(x.float(), wgu.float(), wd.float(), tw, tid)
     torch.testing.assert_close(out.float(), expect, atol=2e-2 * expect.abs().max().item(), rtol=3e-2)
+
+
+@pytest.mark.parametrize("t,e,k,h,i,skew", [(4096, 8, 2, 1024, 2048, True), (777, 8, 2, 512, 384, False),
+                                            (4096, 8, 2, 4096, 14336, True)])
+def test_moe_prefill_persistent_matches_grouped(cuda, t, e, k, h, i, skew):
+    """knobs.moe_persistent: the grouped expert GEMMs on the persistent gemm_pf (MOE form: dynamic tile
+    queue over every expert's row tiles, counts / offsets read on the device) compute each tile with
+    the same K order as gemm_pp_moe -- identical outputs; skewed routing, empty experts, ragged
+    segments; and expert parallelism (a slice of the experts) matches the full layer's partial sum."""
+    from distributed_llms_amd import knobs
+    torch.manual_seed(t + h + 1)
+    x = _bf(t, h)
+    wr = _bf(e, h, scale=0.002 if skew else 0.1)
+    if skew:
+        x = x.abs() * 0.5
+        wr[2] += 0.03
+        wr[5] += 0.02
+    wgu, wd = _bf(e, 2 * i, h, scale=0.03), _bf(e, h, i, scale=0.03)
+    with knobs.override(moe_persistent=False):
+        grouped = moe.forward(x, wr, wgu, wd, k)
+    with knobs.override(moe_persistent=True):
+        pers = moe.forward(x, wr, wgu, wd, k)
+        half = e // 2
+        ep = moe.forward(x, wr, wgu[half:].contiguous(), wd[half:].contiguous(), k, half) + \
+            moe.forward(x, wr, wgu[:half].contiguous(), wd[:half].contiguous(), k, 0)
+    torch.testing.assert_close(pers.float(), grouped.float(), atol=1e-2 * grouped.float().abs().max().item(), rtol=0)
+    torch.testing.assert_close(ep.float(), pers.float(), atol=2e-2 * pers.float().abs().max().item(), rtol=2e-2)
+
+
+def test_moe_fp8_prefill_grouped_no_host_sync(cuda):
+    """W8A8 experts at prefill-sized T: one grouped fp8 launch per projection (no expert loop, no
+    counts read on the host -- graph-capturable), against the fp8 reference numerics."""
+    from distributed_llms_amd.ops import quant
+    t, e, k, h, i = 1024, 8, 2, 512, 512
+    torch.manual_seed(3)
+    x, wr = _bf(t, h), _bf(e, h, scale=0.1)
+    wgu, wd = quant.quantize_experts(_bf(e, 2 * i, h, scale=0.05)), quant.quantize_experts(_bf(e, h, i, scale=0.05))
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        moe.forward(x, wr, wgu, wd, k)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        out = moe.forward(x, wr, wgu, wd, k)
+    g.replay()
+    torch.cuda.synchronize()
+    tw, tid = ref.moe_route(ref.linear(x, wr).float(), k)
+    expect = quant.moe_mlp_ref(x, wgu, wd, tw, tid)
+    torch.testing.assert_close(out.float(), expect.float(), atol=3e-2 * expect.abs().max().item(), rtol=5e-2)

@@ -115,11 +115,15 @@ def _check(got: torch.Tensor, ref_out, what: str, max_rel: float, mean_rel: floa
 
 
 def _record(row):
-    """Achieved errors of every check, one JSON line each (gpurun_out/production_shape_errors.jsonl;
-    copied to profiles/ -- the bounds above are set at about 2x these)."""
-    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
-    os.makedirs(d, exist_ok=True)
-    with open(os.path.join(d, "production_shape_errors.jsonl"), "a") as f:
+    """Achieved errors of every check, one JSON line each, appended to the file named by
+    DLLM_RECORD_ERRORS (unset: nothing is written; profiles/production_shape_errors.md holds the
+    recorded table -- the 8B / Mixtral bounds sit ~1.2-1.3x above its max and mean, the 70B ones
+    ~1.4x)."""
+    path = os.environ.get("DLLM_RECORD_ERRORS")
+    if not path:
+        return
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "a") as f:
         f.write(json.dumps(row) + "\n")
 
 

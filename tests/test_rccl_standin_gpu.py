@@ -183,12 +183,14 @@ def _spinner(k, stream, lds_kib, timeout_s, channels=8):
 
 
 def _time(fn, n=10):
+    """Median ms of fn on the current stream -- waiting on its events only: a device-wide
+    synchronize would also wait for the spinner on the other stream."""
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
     for a, b in ev:
         a.record()
         fn()
         b.record()
-    torch.cuda.synchronize()
+    ev[-1][1].synchronize()
     return sorted(a.elapsed_time(b) for a, b in ev)[n // 2]
 
 
@@ -215,7 +217,7 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
         with knobs.override(pf_dynamic=True):
             beside = _time(lambda: gemm.linear_pf(x, w))
             y = gemm.linear_pf(x, w)
-        torch.cuda.synchronize()
+        torch.cuda.current_stream().synchronize()
         assert not spin_stream.query(), "spinner ended early: the timing was not beside it"
     finally:
         wv[0] = 1
@@ -231,7 +233,7 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     with knobs.override(pf_dynamic=False):
         t0 = time.perf_counter()
         ys = gemm.linear_pf(x, w)
-        torch.cuda.synchronize()
+        torch.cuda.current_stream().synchronize()
         static_s = time.perf_counter() - t0
     spin_stream2.synchronize()
     print(f"static walk beside the spinner: {static_s * 1e3:.1f} ms (spinner verdict {wv2[1]})")
