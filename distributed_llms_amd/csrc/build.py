@@ -55,6 +55,14 @@ def _run(cmd):
     return r.stdout
 
 
+def _link(cmd_prefix, target, rest):
+    """Link into a temporary file, then rename over the target: a process importing the module
+    meanwhile (or a snapshot of the tree) never sees a half-written .so."""
+    tmp = target + ".tmp"
+    _run(cmd_prefix + ["-o", tmp] + rest)
+    os.replace(tmp, target)
+
+
 def build_kernels(force=False, jobs=8, verbose=False) -> str:
     src_dir = os.path.join(HERE, "kernels")
     out_dir = os.path.join(BUILD, "kernels")
@@ -85,7 +93,7 @@ def build_kernels(force=False, jobs=8, verbose=False) -> str:
                 print(out)
     target = _ext_path("_C_kernels")
     if force or _stale(target, objs):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", target] + objs)
+        _link([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"], target, objs)
     return target
 
 
@@ -107,7 +115,7 @@ def build_runtime(force=False, jobs=8, verbose=False) -> str:
         list(ex.map(_run, jobs_list))
     target = _ext_path("_C_runtime")
     if force or _stale(target, objs):
-        _run([CXX, "-shared", "-fPIC", "-o", target] + objs)
+        _link([CXX, "-shared", "-fPIC"], target, objs)
     return target
 
 
@@ -142,7 +150,7 @@ def build_comm(force=False, jobs=8, verbose=False) -> str:
                   "-D__HIP_PLATFORM_AMD__", f"-I{rocm}/include"] + [f"-I{p}" for p in _py_includes()])
     target = _ext_path("_C_rccl")
     if force or _stale(target, objs):
-        _run([CXX, "-shared", "-fPIC", "-o", target, *objs, f"-L{rocm}/lib", "-lrccl", "-lamdhip64"])
+        _link([CXX, "-shared", "-fPIC"], target, [*objs, f"-L{rocm}/lib", "-lrccl", "-lamdhip64"])
     return target
 
 

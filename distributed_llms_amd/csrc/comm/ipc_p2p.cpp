@@ -13,11 +13,13 @@
 // the caching allocator's block carries its offset from hipMemGetAddressRange.
 #include <hip/hip_runtime_api.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace py = pybind11;
 
@@ -71,6 +73,27 @@ void wait_value32(uintptr_t stream, uintptr_t ptr, uint32_t value) {
             "hipStreamWaitValue32");
 }
 
+// A stream with a CU mask.  HIP never pools such a stream with others on a shared hardware queue
+// (the mask is a queue property), so a communication kernel that spins on it -- an RCCL receive
+// posted before its peer sends -- cannot hold up the compute stream's kernels behind it in one
+// in-order queue (a process gets GPU_MAX_HW_QUEUES = 4 hardware queues; streams beyond that share).
+// mask: one bit per CU, 32 CUs per word; an empty list = every CU.
+uintptr_t cu_masked_stream(int device, const std::vector<uint32_t>& mask) {
+  ipc_check(hipSetDevice(device), "hipSetDevice");
+  std::vector<uint32_t> m(mask);
+  if (m.empty()) {
+    int cus = 0;
+    ipc_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device), "hipDeviceGetAttribute");
+    m.assign((cus + 31) / 32, 0u);
+    for (int c = 0; c < cus; ++c) m[c / 32] |= 1u << (c % 32);
+  }
+  hipStream_t st = nullptr;
+  ipc_check(hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()), "hipExtStreamCreateWithCUMask");
+  return reinterpret_cast<uintptr_t>(st);
+}
+
+void stream_destroy(uintptr_t st) { ipc_check(hipStreamDestroy(reinterpret_cast<hipStream_t>(st)), "hipStreamDestroy"); }
+
 bool can_wait_value(int device) {
   int v = 0;
   ipc_check(hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, device), "hipDeviceGetAttribute");
@@ -88,4 +111,7 @@ void register_ipc(py::module_& m) {
   m.def("write_value32", &write_value32, py::arg("stream"), py::arg("ptr"), py::arg("value"));
   m.def("wait_value32", &wait_value32, py::arg("stream"), py::arg("ptr"), py::arg("value"));
   m.def("can_wait_value", &can_wait_value, py::arg("device"));
+  m.def("cu_masked_stream", &cu_masked_stream, py::arg("device"), py::arg("mask") = std::vector<uint32_t>{},
+        "a HIP stream on a hardware queue of its own (CU mask; empty = all CUs)");
+  m.def("stream_destroy", &stream_destroy, py::arg("stream"));
 }

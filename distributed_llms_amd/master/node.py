@@ -75,6 +75,7 @@ class MasterNode:
         self.proto = MessageProtocol()
         self.state = "idle"                       # idle | ready | degraded | failed
         self._recovering = False                  # a recovery thread is running (guarded by _lock)
+        self.recoveries = 0                       # completed re-plans after a stage loss
         self.recover_timeout = 600.0              # seconds a recovery waits for replacement workers
         self.metrics = RequestMetrics()
         self._lock = threading.RLock()
@@ -488,7 +489,8 @@ class MasterNode:
                         self.shard_assignments = {}
                         self.assign_shards()
                         self.distribute_shards()
-                        log.info("pipeline recovered")
+                        self.recoveries += 1
+                        log.info("pipeline recovered onto %s", self.stage_workers)
                         self._resubmit_parked()
                         return
                     except Exception as e:
@@ -613,6 +615,8 @@ class MasterNode:
                 reg[wid]["remote"] = f.result(timeout=timeout)
             except Exception as e:
                 reg[wid]["remote"] = {"error": repr(e)}
+        spares = sorted(w for w in reg if w not in self.stage_workers)
         return {"state": self.state, "model": self.model_spec, "num_shards": self.num_shards,
-                "stage_workers": self.stage_workers, "workers": reg, "metrics": self.metrics.summary(),
-                "pending_requests": len(self._tasks)}
+                "stage_workers": self.stage_workers, "spare_workers": spares, "workers": reg,
+                "metrics": self.metrics.summary(), "pending_requests": len(self._tasks),
+                "recoveries": self.recoveries}

@@ -55,6 +55,28 @@ class _HostEvent:
         pass
 
 
+def comm_stream(device, keep: list):
+    """A stream for communication work on a hardware queue of its own.
+
+    HIP deals a process's streams over GPU_MAX_HW_QUEUES (4) hardware queues, and a queue runs in
+    order: a receive kernel spinning in it (a posted ncclRecv whose peer has not sent yet) or a
+    stream-wait on an event holds up every later kernel of every stream sharing that queue -- a
+    compute stream too (round-2 rehearsal: the ids copy stream's wait stalled stage 0's compute;
+    `tests/test_rccl_standin_gpu.py` probes it).  A CU-masked stream is never pooled, so comm
+    streams made here cannot block the compute stream.  ``keep`` collects the raw handles for
+    ``stream_destroy``.  Falls back to a pool stream when the runtime refuses (knobs.comm_own_queues
+    off, or no native module)."""
+    from .. import knobs
+    if knobs.K.comm_own_queues:
+        try:
+            h = _ext.rccl_native().cu_masked_stream(torch.device(device).index or 0)
+            keep.append(h)
+            return torch.cuda.ExternalStream(h, device=torch.device(device))
+        except Exception:            # noqa: BLE001 - a pool stream still works, only less isolated
+            pass
+    return torch.cuda.Stream(device=device)
+
+
 class RcclTransport(DistTransport):
     kind = "rccl"
 
@@ -75,6 +97,7 @@ class RcclTransport(DistTransport):
         if window < 1:
             raise ValueError("in-flight window must be >= 1")
         self.device = dev
+        self._own_streams = []                    # CU-masked comm stream handles (comm_stream)
         self.timeout_s = float(timeout_s)
         self.slots = window + 1
         self.slot_elems = int(max_rows) * int(hidden)
@@ -143,7 +166,7 @@ class RcclTransport(DistTransport):
 
     # streams / events of this stage's device (no-op shims on a CPU stage)
     def _stream(self):
-        return _HostStream() if self.host else torch.cuda.Stream(device=self.device)
+        return _HostStream() if self.host else comm_stream(self.device, self._own_streams)
 
     def _event(self):
         return _HostEvent() if self.host else torch.cuda.Event()
@@ -274,7 +297,7 @@ class RcclTransport(DistTransport):
             p = PendingIds(buf, timeout_s=self.timeout_s)      # the stand-in recv already landed it
         else:
             if self._copy_stream is None:
-                self._copy_stream = torch.cuda.Stream(device=self.device)
+                self._copy_stream = self._stream()
             p = PendingIds(buf, ready=landed, copy_stream=self._copy_stream, timeout_s=self.timeout_s)
         self._ids_users[slot] = p
         return p
@@ -306,6 +329,13 @@ class RcclTransport(DistTransport):
 
     def close(self):
         self.drain()
+        if self._copy_stream is not None:
+            self._copy_stream.synchronize()
         for c in self._comms():
             c.destroy()
         self.comm_in = self.comm_out = self.ring_in = self.ring_out = None
+        if self._own_streams:
+            m = _ext.rccl_native()
+            for h in self._own_streams:
+                m.stream_destroy(h)
+            self._own_streams = []

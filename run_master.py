@@ -42,6 +42,9 @@ def parse(argv=None):
     ap.add_argument("--heartbeat-timeout", type=float, default=None)
     ap.add_argument("--auto", action="store_true", help="wait for workers, assign + distribute, no REPL prompt")
     ap.add_argument("--auto-recover", action="store_true", help="re-distribute after a worker failure")
+    ap.add_argument("--spares", type=int, default=0,
+                    help="hot-spare workers to wait for beyond --workers: registered and heartbeating but "
+                         "unassigned, so --auto-recover re-plans onto one at once when a stage dies")
     ap.add_argument("--bench", type=int, default=0, help="with --auto: submit N synthetic requests, print metrics")
     ap.add_argument("--bench-warmup", type=int, default=1, help="untimed warmup rounds before --bench")
     ap.add_argument("--prompt-len", type=int, default=32)
@@ -70,7 +73,7 @@ def main(argv=None):
           f"  python run_worker.py --master 127.0.0.1:{master.port} [--device cuda:N]", flush=True)
     try:
         if a.auto:
-            master.wait_for_workers(a.workers, timeout=a.wait_timeout)
+            master.wait_for_workers(a.workers + a.spares, timeout=a.wait_timeout)
             print("assignments:", master.assign_shards(), flush=True)
             acks = master.distribute_shards()
             print("loaded:", json.dumps({w: x.get("layer_range") for w, x in acks.items()}), flush=True)

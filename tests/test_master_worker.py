@@ -241,3 +241,23 @@ def test_degraded_without_recovery_thread_does_not_park():
         assert m._retry == []
     finally:
         m.stop(shutdown_workers=False)
+
+
+def test_hot_spare_takes_over_without_a_new_registration(cluster):
+    """Shard redundancy (plan.md:434): a spare worker registered beside the stages stays
+    unassigned; when a stage worker dies, recovery re-plans onto the spare at once -- no replacement
+    has to join -- and the parked requests complete with the fault-free tokens."""
+    make, procs = cluster
+    m = make("synthetic:tiny-llama", 2, auto_recover=True, extra={1: ("--fail-after", "3")})
+    procs.append(_spawn_worker(m.port))                 # the hot spare
+    m.wait_for_workers(3, timeout=120)
+    m.assign_shards()
+    m.distribute_shards(timeout=300)
+    st = m.status()
+    assert len(st["spare_workers"]) == 1 and st["spare_workers"][0] not in m.stage_workers
+    spare = st["spare_workers"][0]
+    futs = [m.submit(p, {"max_new_tokens": 30, "ignore_eos": True}) for p in PROMPTS]
+    res = [m._finish(f, 240) for f in futs]            # no worker is started after the failure
+    assert m.state == "ready" and m.recoveries == 1 and spare in m.stage_workers
+    ref = LLMEngine(_cfg("synthetic:tiny-llama")).generate(PROMPTS, SamplingParams(max_new_tokens=30, ignore_eos=True))
+    assert [r["tokens"] for r in res] == ref

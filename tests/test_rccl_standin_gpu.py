@@ -267,3 +267,46 @@ def test_gemm_pf_dynamic_queue_bit_exact_and_reusable(cuda):
             exp = torch.nn.functional.silu(exp[:, : n // 2]) * exp[:, n // 2:]
         err = (ref.float() - exp).abs().max().item()
         assert err < 0.02 * exp.abs().max().item() + 0.05, (m, n, kk, sw, err)
+
+
+def test_comm_stream_hardware_queue_isolation(cuda):
+    """HIP gives a process GPU_MAX_HW_QUEUES (4) hardware queues and deals streams over them; work in
+    one queue runs in order, so a receive kernel spinning in a queue holds up every later kernel of
+    every stream sharing it (round-4 review: stage 0 runs ~5 streams).  Probe which torch streams a
+    spinning receive blocks, then show that a CU-masked comm stream (a hardware queue of its own;
+    parallel/rccl_transport.comm_stream) blocks none of them."""
+    from distributed_llms_amd import _ext
+    k, m = _ext.kernels(), _ext.rccl_native()
+    bufs = [torch.zeros(1 << 16, device="cuda") for _ in range(8)]
+    torch.cuda.synchronize()
+
+    def probe(spin_stream, others):
+        wv, keep = _spinner(k, spin_stream, 0, 10.0, channels=2)
+        time.sleep(0.05)
+        evs = []
+        for i, s in enumerate(others):
+            with torch.cuda.stream(s):
+                bufs[i].add_(1)
+                e = torch.cuda.Event()
+                e.record(s)
+            evs.append(e)
+        t0 = time.time()
+        while time.time() - t0 < 1.0 and not all(e.query() for e in evs):
+            time.sleep(0.01)
+        blocked = [i for i, e in enumerate(evs) if not e.query()]
+        still = not spin_stream.query()
+        wv[0] = 1
+        spin_stream.synchronize()
+        for e in evs:
+            e.synchronize()
+        return blocked, still
+
+    pool = [torch.cuda.Stream() for _ in range(7)]
+    blocked_pool, s1 = probe(pool[0], [torch.cuda.current_stream()] + pool[1:])
+    masked = torch.cuda.ExternalStream(m.cu_masked_stream(0))
+    blocked_masked, s2 = probe(masked, [torch.cuda.current_stream()] + pool)
+    print(f"spinning in a pool stream blocks {blocked_pool} of [default, pool 1..6]; "
+          f"in a CU-masked stream: {blocked_masked} of [default, pool 0..6]")
+    assert s1 and s2                                  # the probes ran beside a live spinner
+    assert blocked_masked == []
+    m.stream_destroy(masked.cuda_stream)
