@@ -743,6 +743,7 @@ void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintpt
 // 8 = the shipped schedule with nontemporal output stores (large SwiGLU outputs)
 struct PfSched {
   int ib1, ib3, ge, gm;
+  int ibb = 0, geb = 0, gea = 0;   // split release: barrier after the B reads, B / A piece spacing
 };
 
 // ---- gemm_pf's dynamic tile queue (DYN).  The grouped tile order is cut into chunks of PF_CH
@@ -801,9 +802,15 @@ __device__ void pf_retire(int* q, int grid) {                      // lane 0, on
 constexpr PfSched pf_sched(int sch) {
   // {barrier after set-1 reads (MFMA), barrier before set-0 reads, MFMAs between pieces (0 = spread
   // over the rest of the K-tile), row tiles per group of the tile order}
+  // 9 / 10 / 11: the A and B LDS regions released separately (hipBLASLt's loop): a barrier once every
+  // wave has read its B fragments (after MFMA ibb) frees the B half of the slot, whose pieces then
+  // go out every geb MFMAs; the A pieces follow every gea MFMAs after the barrier at ib1 -- the
+  // 16 pieces spread over ~90 MFMAs instead of ~75, each with more MFMA cycles to hide its issue
   return sch == 1 ? PfSched{36, 88, 0, 8} : sch == 2 ? PfSched{48, 88, 0, 8} : sch == 3 ? PfSched{40, 80, 0, 8}
        : sch == 4 ? PfSched{40, 96, 0, 8} : sch == 5 ? PfSched{40, 88, 4, 8} : sch == 6 ? PfSched{40, 88, 0, 4}
-       : sch == 7 ? PfSched{40, 88, 0, 16} : PfSched{40, 88, 0, 8};
+       : sch == 7 ? PfSched{40, 88, 0, 16} : sch == 9 ? PfSched{40, 88, 0, 8, 20, 6, 6}
+       : sch == 10 ? PfSched{40, 88, 0, 8, 20, 5, 6} : sch == 11 ? PfSched{40, 96, 0, 8, 22, 6, 7}
+       : PfSched{40, 88, 0, 8};
 }
 
 // MOE: the grouped expert GEMM of the prefill (Mixtral) in this persistent form: A is the
@@ -989,7 +996,18 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   constexpr int GE = SC.ge ? SC.ge : ((2 * NMF - 4 - IB1 - 1) / G > 1 ? (2 * NMF - 4 - IB1 - 1) / G : 1);
   constexpr int IB3 = SC.ib3;
   static_assert(IB1 > 2 * NR - 1 && IB1 < NMF && IB3 >= NMF, "schedule 2 barriers");
-  constexpr int PB3 = (IB3 - IB1 - 1) / GE + 1 < G ? (IB3 - IB1 - 1) / GE + 1 : G;
+  // split release (SC.ibb > 0): B pieces p = GA .. G-1 at IBB + 1 + GEB k, A pieces p = 0 .. GA-1 at
+  // A0 + GEA k; NA = A-fragment reads issued after the last B read up to MFMA IBB (lgkmcnt(NA) then
+  // means every B read of this wave is done)
+  constexpr bool SPLIT = SC.ibb > 0;
+  constexpr int IBB = SC.ibb, GEB = SC.geb > 0 ? SC.geb : 1, GEA = SC.gea > 0 ? SC.gea : 1;
+  constexpr int BEND = IBB + 1 + GEB * (GB - 1);
+  constexpr int A0 = SPLIT ? (BEND + GEA > IB1 + 1 ? BEND + GEA : IB1 + 1) : IB1 + 1;
+  constexpr int NA = SPLIT ? ((IBB - 1) / 2 - CT + 1 > 0 ? (IBB - 1) / 2 - CT + 1 : 0) : 0;
+  constexpr int PB3S = (BEND <= IB3 ? GB : (IB3 - IBB - 1) / GEB + 1) +
+                       (A0 > IB3 ? 0 : ((IB3 - A0) / GEA + 1 < GA ? (IB3 - A0) / GEA + 1 : GA));
+  static_assert(!SPLIT || (IBB > 2 * CT && IBB < IB1 && A0 + GEA * (GA - 1) < 2 * NMF), "split release schedule");
+  constexpr int PB3 = SPLIT ? PB3S : ((IB3 - IB1 - 1) / GE + 1 < G ? (IB3 - IB1 - 1) / GE + 1 : G);
   constexpr int VC = (NB - 2) * G + PB3;
   static_assert(IB1 + 1 + GE * (G - 1) < 2 * NMF && IB3 + 1 + 2 * (NR - 1) < 2 * NMF, "schedule 2 fits a K-tile");
   static_assert(VC <= 63, "vmcnt");
@@ -1046,12 +1064,23 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
         else
           acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[c], fa1[r], acc[r][c], 0, 0, 0);
         if constexpr (i % 2 == 1 && i / 2 < NR) rd1(base1, std::integral_constant<int, i / 2>{});
+        if constexpr (SPLIT && i == IBB) {                 // every wave's B reads of this slot done
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(NA) : "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
         if constexpr (i == IB1) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (i > IB1 && (i - IB1 - 1) % GE == 0 && (i - IB1 - 1) / GE < G) piece(slot, (i - IB1 - 1) / GE);
+        if constexpr (SPLIT) {
+          if constexpr (i > IBB && (i - IBB - 1) % GEB == 0 && (i - IBB - 1) / GEB < GB)
+            piece(slot, GA + (i - IBB - 1) / GEB);
+          if constexpr (i >= A0 && (i - A0) % GEA == 0 && (i - A0) / GEA < GA) piece(slot, (i - A0) / GEA);
+        } else {
+          if constexpr (i > IB1 && (i - IB1 - 1) % GE == 0 && (i - IB1 - 1) / GE < G) piece(slot, (i - IB1 - 1) / GE);
+        }
         if constexpr (i == IB3) {
           pp_vm<VC>();
           __builtin_amdgcn_sched_barrier(0);
@@ -1178,8 +1207,8 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   const long tiles = (long)(N / 256) * ((M + 255) / 256);
   DLLM_HOST_CHECK(tiles < (1L << 30), "tiles");
   const long grid = ((tiles < cus ? tiles : cus) + 7) / 8 * 8;
-  DLLM_HOST_CHECK(variant >= 0 && variant <= 8 && (mode == 0 || variant == 0 || variant == 8),
-                  "variant 0..8 (SwiGLU: 0 or 8)");
+  DLLM_HOST_CHECK(variant >= 0 && variant <= 11 && (mode == 0 || variant == 0 || variant == 8 || variant >= 9),
+                  "variant 0..11 (SwiGLU: 0, 8 or the split-release schedules 9..11)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int* q = dyn ? pf_queue(s) : nullptr;
 #define DLLM_PF_GO(MODE_, SCH_)                                                                               \
@@ -1189,13 +1218,21 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_, true>), dim3((unsigned)grid), dim3(256), 0, s,               \
                      (const bf16*)a, (const bf16*)b, (bf16*)c, M, N, K, q, (const int*)nullptr, (const int*)nullptr, 1)
   const bool nt_store = variant == 8 || (variant == 0 && (long)M * (N / 2) * 2 > (256L << 20));
+  DLLM_HOST_CHECK(dyn || variant <= 8, "the split-release schedules (9..11) run with the dynamic tile queue");
   if (dyn) {
-    DLLM_HOST_CHECK(variant == 0 || variant == 8, "the dynamic tile queue runs the shipped schedule (0 / 8)");
+    DLLM_HOST_CHECK(variant == 0 || variant == 8 || variant >= 9,
+                    "the dynamic tile queue runs the shipped schedule (0 / 8) or a split-release one (9..11)");
     if (mode == 1) {
-      if (nt_store) DLLM_PF_GO_DYN(2, 8);
+      if (variant == 9) DLLM_PF_GO_DYN(2, 9);
+      else if (variant == 10) DLLM_PF_GO_DYN(2, 10);
+      else if (variant == 11) DLLM_PF_GO_DYN(2, 11);
+      else if (nt_store) DLLM_PF_GO_DYN(2, 8);
       else DLLM_PF_GO_DYN(2, 0);
     } else {
       if (variant == 8) DLLM_PF_GO_DYN(0, 8);
+      else if (variant == 9) DLLM_PF_GO_DYN(0, 9);
+      else if (variant == 10) DLLM_PF_GO_DYN(0, 10);
+      else if (variant == 11) DLLM_PF_GO_DYN(0, 11);
       else DLLM_PF_GO_DYN(0, 0);
     }
   } else if (mode == 1) {

@@ -39,6 +39,12 @@ class Knobs:
     wide_down_max_m: int = 512        # MLP down (K >= 8192, K > N) up to this M
     wide_proj_max_m: int = 256        # qkv / o / LM head up to this M (K >= 8192: the down limit)
     wide_target_wgs: int = 256        # split-K: about one workgroup per CU
+    # medium M (mixed prefill + decode steps, short prefills): above the decode cutovers and up to
+    # this M, a projection whose gemm_pf grid would fill less than pf_min_fill of the CUs (256 x 256
+    # tiles: N / 256 x M / 256) runs on gemm_wide (256 x 128 tiles, several row tiles, split-K to fill
+    # the CUs) instead; 0 = off (bench/medium_m_bench.py)
+    wide_mid_max_m: int = 0
+    pf_min_fill: float = 0.75
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
@@ -60,6 +66,9 @@ class Knobs:
     # gemm_pf pulls its tiles from per-XCD device queues (a workgroup that starts late -- its CU held
     # by a co-resident RCCL / stand-in kernel -- finds them taken) instead of the static w + i P walk
     pf_dynamic: bool = True
+    # gemm_pf main-loop schedule for prefill projections: 0 = the shipped schedule 2 (pieces every 5
+    # MFMAs after one mid-K-tile barrier); 9..11 = A / B LDS regions released separately
+    pf_schedule: int = 0
     # decode LM head (N > 65536) at pp_head_min_m <= M <= 256 on gemm_pp schedule 2 with nontemporal
     # weights: 230 vs 265 us for gemm_sq at M = 256 (Llama-3-8B); 0 = off
     pp_head_min_m: int = 225

@@ -39,6 +39,26 @@ def is_down_proj(n: int, k: int) -> bool:
     return k >= 8192 and k > n
 
 
+def _cus(device) -> int:
+    idx = device.index or 0
+    n = _CUS.get(idx)
+    if n is None:
+        n = _CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return n
+
+
+_CUS = {}
+
+
+def _use_wide_mid(m: int, n: int, k: int, x: torch.Tensor, swiglu: bool) -> bool:
+    """knobs.wide_mid_max_m: medium M whose 256 x 256 persistent grid would leave CUs idle."""
+    kn = knobs.K
+    if not (0 < kn.wide_mid_max_m and m <= kn.wide_mid_max_m) or n % 128 or k % 64:
+        return False
+    tiles = (-(-m // 256)) * (n // 256)              # gemm_pf's grid (SwiGLU: N = 2I, also 256-wide)
+    return tiles < kn.pf_min_fill * _cus(x.device)
+
+
 def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
     kn = knobs.K
     roles = {t for t in kn.wide.split(",") if t and t != "none"}
@@ -46,6 +66,8 @@ def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: 
         return False
     if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
         return False
+    if _use_wide_mid(m, n, k, x, swiglu):
+        return True
     down = is_down_proj(n, k) and not swiglu
     if "all" in roles:
         return m <= 512 or (down and m <= kn.wide_down_max_m)
@@ -233,7 +255,9 @@ def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, variant: i
     if n % 256 or k % 64:
         raise ValueError("linear_pf: N % 256 and K % 64")
     y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
-    if knobs.K.pf_dynamic and k >= 128 and variant in (0, 8):
+    if variant == 0 and knobs.K.pf_schedule:
+        variant = knobs.K.pf_schedule  # split-release schedules 9..11 (gemm_pp.hip pf_sched)
+    if knobs.K.pf_dynamic and k >= 128 and (variant in (0, 8) or variant >= 9):
         variant |= 16                  # per-XCD dynamic tile queues (gemm_pp.hip, DYN)
     _ext.kernels().gemm_pf(y.data_ptr(), x.data_ptr(), w.data_ptr(), m, n, k, 1 if swiglu else 0, variant,
                            torch.cuda.current_stream().cuda_stream)

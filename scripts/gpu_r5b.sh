@@ -10,7 +10,7 @@ $T 700 python -u -m pytest -x -v -s --timeout 240 --timeout-method thread tests/
   "tests/test_pipeline_gpu.py::test_multiprocess_gpu_pipeline_ipc" \
   "tests/test_engine_gpu.py::test_mixed_prefill_decode_steps_gpu" \
   tests/test_kernels_gpu.py tests/test_gemm_gpu.py tests/test_moe_gpu.py \
-  -k "standin or gemm_pf or pf_ or ipc or mixed or prefill or persistent" \
+  -k "standin or gemm_pf or pf_ or ipc or mixed or prefill or persistent or queue" \
   > gpurun_out/r5b_tests.log 2>&1 \
   || { echo "tests failed"; tail -60 gpurun_out/r5b_tests.log; exit 1; }
 grep -E "passed|failed|gemm_pf solo|static walk" gpurun_out/r5b_tests.log | tail -8

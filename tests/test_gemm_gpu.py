@@ -392,3 +392,18 @@ def test_pp_graph_replay_and_determinism(cuda):
         g.replay()
     torch.cuda.synchronize()
     assert torch.equal(y, y0)
+
+
+@pytest.mark.parametrize("sched", [9, 10, 11])
+def test_pf_split_release_schedules_bit_exact(cuda, sched):
+    """gemm_pf schedules 9-11 (A / B LDS regions released separately, pieces spread over more
+    MFMAs) change only when the staging loads are issued: same bits as the shipped schedule, plain
+    and SwiGLU, ragged M (knobs.pf_schedule)."""
+    from distributed_llms_amd import knobs
+    x, w = _bf(3000, 4096), _bf(6144, 4096, scale=0.05)
+    xs, ws = _bf(1000, 1024), _bf(2 * 1536, 1024, scale=0.05)
+    with knobs.override(pf_schedule=0):
+        ref, ref_s = gemm.linear_pf(x, w), gemm.linear_pf(xs, ws, swiglu=True, variant=0)
+    with knobs.override(pf_schedule=sched):
+        assert torch.equal(gemm.linear_pf(x, w), ref)
+        assert torch.equal(gemm.linear_pf(xs, ws, swiglu=True), ref_s)
