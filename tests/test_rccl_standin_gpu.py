@@ -203,7 +203,10 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     from distributed_llms_amd.ops import gemm
     k = _ext.kernels()
     torch.manual_seed(0)
-    m, n, kk = 8192, 4096, 4096
+    # a prefill qkv projection at T = 32768: 3072 tiles, 12 per workgroup -- with 8 CUs taken the
+    # remaining 248 workgroups need 13 rounds (tile quantization: 1.08x); at 512 tiles (2 per
+    # workgroup) the same 8 CUs cost a third round on some workgroups (measured 1.25x)
+    m, n, kk = 32768, 6144, 4096
     x = torch.randn(m, kk, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(n, kk, device="cuda", dtype=torch.bfloat16) * 0.02
     with knobs.override(pf_dynamic=True):
