@@ -232,10 +232,14 @@ class EngineConfig:
     max_batch: int = 256               # max sequences decoded per step (per replica)
     max_prefill_tokens: int = 16384    # max prompt tokens per prefill step
     # prompt tokens a step may add to a slot's running decode rows (mixed prefill + decode step,
-    # SURVEY §5.7): arrivals during decode are prefilled in chunks of at most this many tokens
-    # riding along with the decode batch, so running sequences never stall behind a whole
-    # max_prefill_tokens chunk; 0 = prefill-first (a step is all prefill or all decode)
-    mixed_prefill_tokens: int = 512
+    # SURVEY §5.7; capped by max_prefill_tokens): arrivals during decode are prefilled in chunks
+    # riding along with the decode batch instead of prefill-only steps that stall every running
+    # sequence; 0 = prefill-first (a step is all prefill or all decode).  The budget trades the
+    # running rows' inter-token latency against admission speed: a 512-token budget made the
+    # pipeline's burst admission (256 prompts per slot behind 64 decode rows) take 48 small eager
+    # steps instead of 3 full ones (pp2 rehearsal 17.4k vs 27k tok/s), so the default admits at
+    # the full prefill rate and latency-bound deployments lower it (profiles/round5_open_loop.md)
+    mixed_prefill_tokens: int = 8192
     max_seq_len: int = 4096
     kv_block_size: int = 32            # tokens per paged-KV block
     kv_cache_fraction: float = 0.80    # of free HBM after weights

@@ -98,13 +98,16 @@ class Scheduler:
     def __init__(self, block_manager, num_slots: int = 1, max_batch: int = 256,
                  max_prefill_tokens: int = 16384, max_seq_len: int = 4096, mixed_prefill_tokens: int = 0):
         """``mixed_prefill_tokens`` > 0: a slot with running sequences admits waiting prompts as a
-        chunk of at most this many tokens riding along with its decode rows (a mixed step) instead
-        of a prefill-only step that stalls every running sequence for a whole chunk."""
+        chunk of at most this many tokens (capped by ``max_prefill_tokens``) riding along with its
+        decode rows (a mixed step) instead of a prefill-only step that stalls every running
+        sequence for a whole chunk.  Large budgets keep a burst's admission as fast as
+        prefill-first (the decode rows ride along for free); small ones bound the inter-token
+        latency of the running rows."""
         self.bm = block_manager
         self.num_slots = max(1, num_slots)
         self.max_batch = max_batch
         self.max_prefill_tokens = max_prefill_tokens
-        self.mixed_prefill_tokens = max(0, int(mixed_prefill_tokens))
+        self.mixed_prefill_tokens = min(max(0, int(mixed_prefill_tokens)), max_prefill_tokens)
         self.num_mixed = 0
         self.max_seq_len = max_seq_len
         self.max_blocks = -(-max_seq_len // block_manager.block_size)    # decode block-table width

@@ -87,8 +87,9 @@ class Knobs:
     defer_o: bool = True              # split-K o-proj reduce fused into the next add + RMSNorm
     lookahead: bool = True            # single-GPU engine: issue step n+1 before step n's tokens land
     pp_lookahead: bool = True         # pipeline driver: the same across stages
-    # RCCL transport comm streams (send / recv / ring / ids copy) on CU-masked streams, i.e. hardware
-    # queues of their own: a spinning receive or a stream-wait never blocks the compute stream's queue
+    # RCCL transport comm streams (send / recv / ring / ids copy) on high-priority streams, i.e.
+    # hardware queues of their own: a spinning receive or a stream-wait never blocks the compute
+    # stream's queue (CU-masked streams share the default stream's queue: profiles/round5_comm_queues.md)
     comm_own_queues: bool = True
     # ---- MoE (ops/moe.py)
     moe_variant: int = 0

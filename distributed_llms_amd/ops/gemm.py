@@ -166,10 +166,39 @@ def wide_row_tile(m: int, n: int, k: int, swiglu: bool = False) -> int:
     return wide_bm(m)
 
 
+# CUs a co-resident communication kernel may hold (set by the RCCL transport of a pipeline stage:
+# a p2p receive spins on its CUs for as long as its peer has not sent).  gemm_wide's split-K grids
+# are sized to leave them free: its workgroups (144 KiB of LDS) cannot share a CU with a kernel
+# holding LDS, so a 256-workgroup grid beside 4 such CUs runs a second round for 4 workgroups --
+# the down projection took 1.58x its solo time beside a 4-CU receive, the 224 / 240-workgroup
+# grids 1.00x (scripts/hwq_probe.py gemms, profiles/round5_comm_queues.md)
+_comm_cus = 0
+_comm_users = 0
+
+
+def reserve_cus_for_comm(n: int) -> None:
+    """A transport with spinning comm kernels starts: size gemm_wide grids around ``n`` CUs."""
+    global _comm_cus, _comm_users
+    _comm_users += 1
+    _comm_cus = max(_comm_cus, int(n))
+
+
+def release_cus_for_comm() -> None:
+    global _comm_cus, _comm_users
+    _comm_users = max(0, _comm_users - 1)
+    if not _comm_users:
+        _comm_cus = 0
+
+
 def wide_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 0) -> int:
-    """K slices for gemm_wide: about one workgroup per CU, >= 8 K-tiles (512) per slice."""
+    """K slices for gemm_wide: about one workgroup per CU, >= 8 K-tiles (512) per slice (with CUs
+    reserved for communication: at most one workgroup per remaining CU)."""
     tiles = (n // 128) * (-(-m // wide_row_tile(m, n, k, swiglu)))
-    s = max(1, round((target_wgs or knobs.K.wide_target_wgs) / tiles))
+    target = target_wgs or knobs.K.wide_target_wgs
+    if _comm_cus:
+        s = max(1, (target - _comm_cus) // tiles)
+    else:
+        s = max(1, round(target / tiles))
     return max(1, min(s, (k // 64) // 8, 16))
 
 
@@ -257,7 +286,12 @@ def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, variant: i
     y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
     if variant == 0 and knobs.K.pf_schedule:
         variant = knobs.K.pf_schedule  # split-release schedules 9..11 (gemm_pp.hip pf_sched)
-    if knobs.K.pf_dynamic and k >= 128 and (variant in (0, 8) or variant >= 9):
+    if torch.cuda.is_current_stream_capturing():
+        # inside a graph: the static tile walk.  A tile queue is per stream and self-resetting, but
+        # a replay may run on another stream beside eager launches that use the same queue
+        if variant >= 9:
+            variant = 0
+    elif knobs.K.pf_dynamic and k >= 128 and (variant in (0, 8) or variant >= 9):
         variant |= 16                  # per-XCD dynamic tile queues (gemm_pp.hip, DYN)
     _ext.kernels().gemm_pf(y.data_ptr(), x.data_ptr(), w.data_ptr(), m, n, k, 1 if swiglu else 0, variant,
                            torch.cuda.current_stream().cuda_stream)

@@ -60,21 +60,23 @@ def comm_stream(device, keep: list):
 
     HIP deals a process's streams over GPU_MAX_HW_QUEUES (4) hardware queues, and a queue runs in
     order: a receive kernel spinning in it (a posted ncclRecv whose peer has not sent yet) or a
-    stream-wait on an event holds up every later kernel of every stream sharing that queue -- a
-    compute stream too (round-2 rehearsal: the ids copy stream's wait stalled stage 0's compute;
-    `tests/test_rccl_standin_gpu.py` probes it).  A CU-masked stream is never pooled, so comm
-    streams made here cannot block the compute stream.  ``keep`` collects the raw handles for
-    ``stream_destroy``.  Falls back to a pool stream when the runtime refuses (knobs.comm_own_queues
-    off, or no native module)."""
+    stream-wait on an event holds up every later kernel of every stream sharing that queue -- the
+    compute stream too (round-2 rehearsal: the ids copy stream's wait stalled stage 0's compute).
+    Measured on MI355X (scripts/hwq_probe.py, profiles/round5_comm_queues.md): a spinner in a pool
+    stream blocks the pool streams dealt to its queue; CU-masked streams
+    (hipExtStreamCreateWithCUMask) all share ONE queue with the default stream; high-priority
+    streams get queues of their own -- a spinner in one blocks no normal stream and no other
+    high-priority stream.  So comm streams are high-priority streams (knobs.comm_own_queues; off:
+    pool streams).  ``keep``: unused (kept for callers that collect raw handles)."""
     from .. import knobs
     if knobs.K.comm_own_queues:
-        try:
-            h = _ext.rccl_native().cu_masked_stream(torch.device(device).index or 0)
-            keep.append(h)
-            return torch.cuda.ExternalStream(h, device=torch.device(device))
-        except Exception:            # noqa: BLE001 - a pool stream still works, only less isolated
-            pass
+        return torch.cuda.Stream(device=device, priority=torch.cuda.Stream.priority_range()[1])
     return torch.cuda.Stream(device=device)
+
+
+# CUs a stage's spinning comm kernels may hold at once (receive + send + ids ring, a few channel
+# workgroups each): gemm_wide's split-K grids leave them free (ops/gemm.reserve_cus_for_comm)
+COMM_CUS = 16
 
 
 class RcclTransport(DistTransport):
@@ -97,7 +99,11 @@ class RcclTransport(DistTransport):
         if window < 1:
             raise ValueError("in-flight window must be >= 1")
         self.device = dev
-        self._own_streams = []                    # CU-masked comm stream handles (comm_stream)
+        self._own_streams = []
+        self._reserved = not self.host and not loopback
+        if self._reserved:
+            from ..ops import gemm
+            gemm.reserve_cus_for_comm(COMM_CUS)
         self.timeout_s = float(timeout_s)
         self.slots = window + 1
         self.slot_elems = int(max_rows) * int(hidden)
@@ -334,8 +340,10 @@ class RcclTransport(DistTransport):
         for c in self._comms():
             c.destroy()
         self.comm_in = self.comm_out = self.ring_in = self.ring_out = None
-        if self._own_streams:
-            m = _ext.rccl_native()
-            for h in self._own_streams:
-                m.stream_destroy(h)
-            self._own_streams = []
+        if self._reserved:
+            from ..ops import gemm
+            gemm.release_cus_for_comm()
+            self._reserved = False
+        # the comm streams are torch pool streams (never destroyed): torch's allocators may still
+        # hold blocks whose pending events were recorded on them -- destroying the CU-masked
+        # streams of an earlier version here crashed every stage process at exit

@@ -9,3 +9,6 @@ for kn in "moe_persistent=0" ""; do
   DLLM_KNOBS="$kn" $T 400 python bench.py --model mixtral-8x7b --steps 2 --warmup 1 > gpurun_out/r5d_mixtral.log 2>&1 || { echo "mixtral bench failed"; tail -30 gpurun_out/r5d_mixtral.log; exit 1; }
   echo "mixtral [$kn]: $(tail -1 gpurun_out/r5d_mixtral.log | cut -c1-120) ttft $(tail -1 gpurun_out/r5d_mixtral.log | python -c 'import json,sys; r=json.loads(sys.stdin.read()); print(r["ttft_p50_ms"], r["itl_p50_ms"])')"
 done
+# non-dllm kernels inside one timed Mixtral round (review item 6: ~174 ms of at::native per two rounds in r4)
+$T 400 python bench/debug/torch_op_origins.py --model mixtral-8x7b > gpurun_out/r5d_mixtral_origins.txt 2>&1 || { echo "mixtral origins failed"; tail -30 gpurun_out/r5d_mixtral_origins.txt; exit 1; }
+tail -25 gpurun_out/r5d_mixtral_origins.txt

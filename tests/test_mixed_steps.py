@@ -108,3 +108,10 @@ def test_mixed_steps_pipeline_loopback():
     ref = LLMEngine(ecfg).generate(prompts, p)
     outs, drv, _ = run_loopback_pipeline(ecfg, 2, prompts, p, device="cpu")
     assert outs == ref
+
+
+def test_mixed_budget_capped_by_prefill_budget():
+    bm = make_block_manager(64, 4)
+    sch = Scheduler(bm, 1, 8, max_prefill_tokens=100, max_seq_len=64, mixed_prefill_tokens=8192)
+    assert sch.mixed_prefill_tokens == 100
+    assert Scheduler(bm, 1, 8, 100, 64, mixed_prefill_tokens=0).mixed_prefill_tokens == 0

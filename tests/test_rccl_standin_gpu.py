@@ -72,7 +72,8 @@ def _rank_main(rank, port, q, mode):
             # kernel spins on its CUs (rank 0 sends only after rank 1 reported its GEMMs finished)
             n = 2 << 20
             if rank == 1:
-                rs, cs = torch.cuda.Stream(), torch.cuda.Stream()
+                from distributed_llms_amd.parallel.rccl_transport import comm_stream
+                rs, cs = comm_stream("cuda", []), torch.cuda.Stream()     # the transport's stream kinds
                 dst = torch.zeros(n, dtype=torch.uint8, device="cuda")
                 x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
                 torch.cuda.synchronize()
@@ -198,7 +199,7 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     """gemm_pf with a receive kernel spinning beside it -- 8 workgroups that hold 40 KiB of LDS each,
     so a 128 KiB gemm_pf workgroup cannot share their CUs: with the dynamic tile queue the GEMM takes
     <= 1.1x its solo time (the workgroups that cannot start find their tiles taken); the static
-    w + i P walk waits for the spinner to leave (here: its 1.5 s deadline)."""
+    w + i P walk runs the blocked workgroups' shares as a second round (measured 2.2 vs 1.4 ms)."""
     from distributed_llms_amd import _ext, knobs
     from distributed_llms_amd.ops import gemm
     k = _ext.kernels()
@@ -212,7 +213,8 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     with knobs.override(pf_dynamic=True):
         ref = gemm.linear_pf(x, w)
         solo = _time(lambda: gemm.linear_pf(x, w))
-    spin_stream = torch.cuda.Stream()
+    from distributed_llms_amd.parallel.rccl_transport import comm_stream
+    spin_stream = comm_stream("cuda", [])             # own hardware queue: only the CUs are shared
     wv, keep = _spinner(k, spin_stream, 40, 30.0)
     try:
         time.sleep(0.05)
@@ -229,8 +231,9 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     assert torch.equal(y, ref)                          # same tiles, same order of K: bit-identical
     print(f"gemm_pf solo {solo:.3f} ms, beside the spinner {beside:.3f} ms")
     assert beside <= 1.1 * solo, (solo, beside)
-    # the static walk: the blocked workgroups' tiles wait for the spinner's deadline
-    spin_stream2 = torch.cuda.Stream()
+    # the static walk: the blocked workgroups' whole shares start only when other workgroups have
+    # retired (a second round of 12 tiles: ~2x), while the dynamic queue hands their tiles out
+    spin_stream2 = comm_stream("cuda", [])
     wv2, keep2 = _spinner(k, spin_stream2, 40, 1.5)
     time.sleep(0.05)
     with knobs.override(pf_dynamic=False):
@@ -241,7 +244,7 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     spin_stream2.synchronize()
     print(f"static walk beside the spinner: {static_s * 1e3:.1f} ms (spinner verdict {wv2[1]})")
     assert torch.equal(ys, ref)
-    assert static_s > 10 * beside * 1e-3
+    assert static_s > 1.3 * beside * 1e-3
 
 
 def test_gemm_pf_dynamic_queue_bit_exact_and_reusable(cuda):
@@ -275,15 +278,17 @@ def test_gemm_pf_dynamic_queue_bit_exact_and_reusable(cuda):
 def test_comm_stream_hardware_queue_isolation(cuda):
     """HIP gives a process GPU_MAX_HW_QUEUES (4) hardware queues and deals streams over them; work in
     one queue runs in order, so a receive kernel spinning in a queue holds up every later kernel of
-    every stream sharing it (round-4 review: stage 0 runs ~5 streams).  Probe which torch streams a
-    spinning receive blocks, then show that a CU-masked comm stream (a hardware queue of its own;
-    parallel/rccl_transport.comm_stream) blocks none of them."""
+    every stream sharing it (round-4 review: stage 0 runs ~5 streams).  A spinner in a pool stream
+    blocks some pool streams; in a comm stream (parallel/rccl_transport.comm_stream: a high-priority
+    stream, a hardware queue of its own) it blocks neither the default stream, nor any of 7 pool
+    streams, nor the other comm streams (send / recv / ring of one stage)."""
     from distributed_llms_amd import _ext
-    k, m = _ext.kernels(), _ext.rccl_native()
-    bufs = [torch.zeros(1 << 16, device="cuda") for _ in range(8)]
-    torch.cuda.synchronize()
+    from distributed_llms_amd.parallel.rccl_transport import comm_stream
+    k = _ext.kernels()
 
     def probe(spin_stream, others):
+        bufs = [torch.zeros(1 << 16, device="cuda") for _ in others]
+        torch.cuda.synchronize()
         wv, keep = _spinner(k, spin_stream, 0, 10.0, channels=2)
         time.sleep(0.05)
         evs = []
@@ -305,11 +310,52 @@ def test_comm_stream_hardware_queue_isolation(cuda):
         return blocked, still
 
     pool = [torch.cuda.Stream() for _ in range(7)]
-    blocked_pool, s1 = probe(pool[0], [torch.cuda.current_stream()] + pool[1:])
-    masked = torch.cuda.ExternalStream(m.cu_masked_stream(0))
-    blocked_masked, s2 = probe(masked, [torch.cuda.current_stream()] + pool)
-    print(f"spinning in a pool stream blocks {blocked_pool} of [default, pool 1..6]; "
-          f"in a CU-masked stream: {blocked_masked} of [default, pool 0..6]")
+    blocked_pool, s1 = probe(torch.cuda.Stream(), [torch.cuda.current_stream()] + pool)
+    comm = [comm_stream("cuda", []) for _ in range(4)]
+    blocked_comm, s2 = probe(comm[0], [torch.cuda.current_stream()] + pool + comm[1:])
+    print(f"spinning in a pool stream blocks {blocked_pool} of [default, pool 0..6]; "
+          f"in a comm stream: {blocked_comm} of [default, pool 0..6, comm 1..3]")
     assert s1 and s2                                  # the probes ran beside a live spinner
-    assert blocked_masked == []
-    m.stream_destroy(masked.cuda_stream)
+    assert blocked_comm == []
+
+
+def test_wide_gemm_grids_leave_comm_cus_free(cuda):
+    """gemm_wide's split-K grids beside a receive spinning on 4 CUs with 40 KiB of LDS each (a
+    144 KiB gemm_wide workgroup cannot share those CUs): the 256-workgroup down projection runs a
+    second round for the blocked workgroups (measured 1.58x); with the RCCL transport's CU
+    reservation (ops/gemm.reserve_cus_for_comm) the grid is 224 workgroups and keeps its solo time."""
+    from distributed_llms_amd import _ext
+    from distributed_llms_amd.ops import gemm
+    from distributed_llms_amd.parallel.rccl_transport import COMM_CUS, comm_stream
+    k = _ext.kernels()
+    torch.manual_seed(0)
+    x = torch.randn(256, 14336, device="cuda", dtype=torch.bfloat16)
+    ws = [torch.randn(4096, 14336, device="cuda", dtype=torch.bfloat16) * 0.02 for _ in range(4)]
+    it = [0]
+
+    def down():
+        it[0] += 1
+        return gemm.linear_wide(x, ws[it[0] % 4])
+
+    gemm.reserve_cus_for_comm(COMM_CUS)
+    try:
+        assert gemm.wide_splits(256, 4096, 14336) == 7
+        ref = down()
+        solo = _time(down, 20)
+        st = comm_stream("cuda", [])
+        wv, keep = _spinner(k, st, 40, 30.0, channels=4)
+        time.sleep(0.05)
+        try:
+            beside = _time(down, 20)
+            y = down()
+            live = not st.query()
+        finally:
+            wv[0] = 1
+            st.synchronize()
+    finally:
+        gemm.release_cus_for_comm()
+    assert gemm.wide_splits(256, 4096, 14336) == 8
+    assert live
+    print(f"down projection, 224-workgroup grid: solo {solo * 1e3:.1f} us, beside a 4-CU spinner {beside * 1e3:.1f} us")
+    assert beside <= 1.15 * solo, (solo, beside)
+    assert torch.isfinite(y).all() and ref.shape == (256, 4096)

@@ -131,3 +131,22 @@ def test_decode_lm_head_goes_to_gemm_pp():
     kn = knobs.K
     assert 0 < kn.pp_head_min_m <= 256 and gemm._use_pp(256, 128256, 4096, x, w, 1)
     assert gemm.PP_HEAD_VARIANT & 64 and gemm.PP_HEAD_VARIANT & 2
+
+
+def test_wide_splits_leave_comm_cus_free():
+    """An RCCL pipeline stage reserves CUs for its spinning comm kernels: every split-K grid then
+    fits one workgroup per remaining CU (no second round for the workgroups the comm kernel blocks)."""
+    from distributed_llms_amd.ops import gemm
+    shapes = [(256, 4096, 14336), (256, 4096, 4096), (256, 6144, 4096), (128, 4096, 4096), (64, 8192, 28672)]
+    base = [gemm.wide_splits(*s) for s in shapes]
+    gemm.reserve_cus_for_comm(16)
+    try:
+        for (m, n, k), b in zip(shapes, base):
+            s = gemm.wide_splits(m, n, k)
+            tiles = (n // 128) * (-(-m // gemm.wide_row_tile(m, n, k)))
+            assert tiles * s <= 240 or s == 1, (m, n, k, s)
+            assert s <= b
+        assert gemm.wide_splits(256, 4096, 14336) == 7
+    finally:
+        gemm.release_cus_for_comm()
+    assert [gemm.wide_splits(*s) for s in shapes] == base
