@@ -92,6 +92,18 @@ uintptr_t cu_masked_stream(int device, const std::vector<uint32_t>& mask) {
   return reinterpret_cast<uintptr_t>(st);
 }
 
+// A non-blocking stream at the device's greatest priority.  HIP gives high-priority streams their
+// own pool of hardware queues (up to GPU_MAX_HW_QUEUES, then shared): the first few such streams of
+// a process each get a queue no normal-priority stream uses (profiles/round5_comm_queues.md).
+uintptr_t priority_stream(int device) {
+  ipc_check(hipSetDevice(device), "hipSetDevice");
+  int least = 0, greatest = 0;
+  ipc_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+  hipStream_t st = nullptr;
+  ipc_check(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest), "hipStreamCreateWithPriority");
+  return reinterpret_cast<uintptr_t>(st);
+}
+
 void stream_destroy(uintptr_t st) { ipc_check(hipStreamDestroy(reinterpret_cast<hipStream_t>(st)), "hipStreamDestroy"); }
 
 bool can_wait_value(int device) {
@@ -113,5 +125,7 @@ void register_ipc(py::module_& m) {
   m.def("can_wait_value", &can_wait_value, py::arg("device"));
   m.def("cu_masked_stream", &cu_masked_stream, py::arg("device"), py::arg("mask") = std::vector<uint32_t>{},
         "a HIP stream on a hardware queue of its own (CU mask; empty = all CUs)");
+  m.def("priority_stream", &priority_stream, py::arg("device"),
+        "a non-blocking stream at the greatest priority (a hardware queue of its own, up to the queue limit)");
   m.def("stream_destroy", &stream_destroy, py::arg("stream"));
 }

@@ -207,7 +207,10 @@ class Scheduler:
             self._sync_preempted()
             if res is not None:
                 packed, rows, _ = res
-                admitted, _blocked = self._admit(slot, len(rows), self.mixed_prefill_tokens)
+                # one token budget per step (decode rows + prompt tokens <= max_prefill_tokens): the
+                # step's activations fit every buffer sized for a prefill step (pipeline hop slots)
+                budget = min(self.mixed_prefill_tokens, self.max_prefill_tokens - len(rows))
+                admitted, _blocked = self._admit(slot, len(rows), budget) if budget > 0 else ([], False)
                 if admitted:
                     self.num_prefilling += len(admitted)
                     self.num_mixed += 1

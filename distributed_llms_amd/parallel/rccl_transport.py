@@ -55,23 +55,34 @@ class _HostEvent:
         pass
 
 
-def comm_stream(device, keep: list):
-    """A stream for communication work on a hardware queue of its own.
+_COMM_STREAMS = {}
+
+
+def comm_stream(device, role: str = "comm"):
+    """The stream of one communication role ("send", "recv", "ring", "copy") on a hardware queue of
+    its own.
 
     HIP deals a process's streams over GPU_MAX_HW_QUEUES (4) hardware queues, and a queue runs in
     order: a receive kernel spinning in it (a posted ncclRecv whose peer has not sent yet) or a
     stream-wait on an event holds up every later kernel of every stream sharing that queue -- the
-    compute stream too (round-2 rehearsal: the ids copy stream's wait stalled stage 0's compute).
-    Measured on MI355X (scripts/hwq_probe.py, profiles/round5_comm_queues.md): a spinner in a pool
-    stream blocks the pool streams dealt to its queue; CU-masked streams
-    (hipExtStreamCreateWithCUMask) all share ONE queue with the default stream; high-priority
-    streams get queues of their own -- a spinner in one blocks no normal stream and no other
-    high-priority stream.  So comm streams are high-priority streams (knobs.comm_own_queues; off:
-    pool streams).  ``keep``: unused (kept for callers that collect raw handles)."""
+    compute stream too (round-2 rehearsal: the ids copy stream's wait stalled stage 0's compute),
+    or another comm role's kernel (a send stuck behind a receive is a pipeline deadlock).
+    Measured on MI355X (scripts/hwq_probe.py, profiles/round5_comm_queues.md): CU-masked streams
+    share ONE queue with the default stream; high-priority streams come from a queue pool of their
+    own, one new queue per stream until the limit.  So each role gets ONE native high-priority
+    stream per device and process (created on first use, never destroyed: torch's allocators may
+    hold events recorded on it until exit), at most four in all -- every role on a queue no other
+    stream of the process uses.  knobs.comm_own_queues off: torch pool streams."""
     from .. import knobs
-    if knobs.K.comm_own_queues:
-        return torch.cuda.Stream(device=device, priority=torch.cuda.Stream.priority_range()[1])
-    return torch.cuda.Stream(device=device)
+    dev = torch.device(device)
+    if not knobs.K.comm_own_queues:
+        return torch.cuda.Stream(device=dev)
+    key = (dev.index or 0, role)
+    st = _COMM_STREAMS.get(key)
+    if st is None:
+        h = _ext.rccl_native().priority_stream(dev.index or 0)
+        st = _COMM_STREAMS[key] = torch.cuda.ExternalStream(h, device=dev)
+    return st
 
 
 # CUs a stage's spinning comm kernels may hold at once (receive + send + ids ring, a few channel
@@ -99,7 +110,6 @@ class RcclTransport(DistTransport):
         if window < 1:
             raise ValueError("in-flight window must be >= 1")
         self.device = dev
-        self._own_streams = []
         self._reserved = not self.host and not loopback
         if self._reserved:
             from ..ops import gemm
@@ -146,8 +156,8 @@ class RcclTransport(DistTransport):
                 self.ring_out = self.m.RcclComm(2, 0, mine["ring"], di, self.timeout_s)
             elif first and not last:
                 self.ring_in = self.m.RcclComm(2, 1, table[self.last]["ring"], di, self.timeout_s)
-        self.send_stream = self._stream() if self.comm_out is not None else None
-        self.recv_stream = self._stream() if self.comm_in is not None else None
+        self.send_stream = self._stream("send") if self.comm_out is not None else None
+        self.recv_stream = self._stream("recv") if self.comm_in is not None else None
         if loopback:
             self.recv_stream = self.send_stream
         self.tx = torch.empty(self.slots, self.slot_elems, dtype=dtype, device=dev) if self.comm_out else None
@@ -161,7 +171,7 @@ class RcclTransport(DistTransport):
         # sampled-ids ring closure: int32 slots of max_ids, deeper than the in-flight window
         self.max_ids = int(max_ids or max_rows)
         self.id_slots = 2 * window + 2
-        self.ring_stream = self._stream() if (self.ring_out or self.ring_in) else None
+        self.ring_stream = self._stream("ring") if (self.ring_out or self.ring_in) else None
         self.ids_tx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_out else None
         self.ids_rx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_in else None
         self._ids_sent = [None] * self.id_slots
@@ -171,8 +181,8 @@ class RcclTransport(DistTransport):
         self._copy_stream = None
 
     # streams / events of this stage's device (no-op shims on a CPU stage)
-    def _stream(self):
-        return _HostStream() if self.host else comm_stream(self.device, self._own_streams)
+    def _stream(self, role):
+        return _HostStream() if self.host else comm_stream(self.device, role)
 
     def _event(self):
         return _HostEvent() if self.host else torch.cuda.Event()
@@ -303,7 +313,7 @@ class RcclTransport(DistTransport):
             p = PendingIds(buf, timeout_s=self.timeout_s)      # the stand-in recv already landed it
         else:
             if self._copy_stream is None:
-                self._copy_stream = self._stream()
+                self._copy_stream = self._stream("copy")
             p = PendingIds(buf, ready=landed, copy_stream=self._copy_stream, timeout_s=self.timeout_s)
         self._ids_users[slot] = p
         return p
@@ -344,6 +354,6 @@ class RcclTransport(DistTransport):
             from ..ops import gemm
             gemm.release_cus_for_comm()
             self._reserved = False
-        # the comm streams are torch pool streams (never destroyed): torch's allocators may still
-        # hold blocks whose pending events were recorded on them -- destroying the CU-masked
-        # streams of an earlier version here crashed every stage process at exit
+        # the comm streams live for the process (comm_stream): torch's allocators may still hold
+        # blocks whose pending events were recorded on them -- destroying the CU-masked streams of
+        # an earlier version here crashed every stage process at exit

@@ -6,7 +6,7 @@ T="timeout -k 10"
 $T 300 python bench.py --steps 5 --warmup 2 > gpurun_out/r5c_closed.log 2>&1 || { echo "closed-loop bench failed"; tail -30 gpurun_out/r5c_closed.log; exit 1; }
 tail -1 gpurun_out/r5c_closed.log | cut -c1-400
 : > gpurun_out/r5c_open.jsonl
-for spec in "110 512" "176 512" "209 512" "176 0" "209 0"; do
+for spec in "110 8192" "176 8192" "209 8192" "176 512" "209 512" "176 0" "209 0"; do
   set -- $spec
   $T 300 python bench.py --rate $1 --mixed-tokens $2 --steps 5 --warmup 1 > gpurun_out/r5c_open_$1_$2.log 2>&1 || { echo "open loop $spec failed"; tail -30 gpurun_out/r5c_open_$1_$2.log; exit 1; }
   tail -1 gpurun_out/r5c_open_$1_$2.log >> gpurun_out/r5c_open.jsonl

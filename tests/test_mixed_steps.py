@@ -115,3 +115,23 @@ def test_mixed_budget_capped_by_prefill_budget():
     sch = Scheduler(bm, 1, 8, max_prefill_tokens=100, max_seq_len=64, mixed_prefill_tokens=8192)
     assert sch.mixed_prefill_tokens == 100
     assert Scheduler(bm, 1, 8, 100, 64, mixed_prefill_tokens=0).mixed_prefill_tokens == 0
+
+
+def test_mixed_step_total_tokens_within_prefill_budget():
+    """Decode rows + prompt tokens of a mixed step never exceed max_prefill_tokens (the pipeline's
+    hop slots and prefill buffers are sized for it)."""
+    bm = make_block_manager(256, 4)
+    sch = Scheduler(bm, 1, 16, max_prefill_tokens=40, max_seq_len=64, mixed_prefill_tokens=8192)
+    for _ in range(3):
+        sch.add(Sequence([1] * 10, SamplingParams(max_new_tokens=20, ignore_eos=True)))
+    st = sch.schedule(0)
+    assert st.is_prefill and not st.mixed and st.num_tokens == 30
+    sch.complete(st, [5, 5, 5])
+    for _ in range(6):
+        sch.add(Sequence([2] * 12, SamplingParams(max_new_tokens=4, ignore_eos=True)))
+    while sch.waiting:
+        st = sch.schedule(0)
+        if st.mixed:
+            assert st.num_tokens <= 40, st.num_tokens
+        sch.complete(st, [7] * st.size)
+    assert sch.num_mixed > 0

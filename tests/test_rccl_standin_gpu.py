@@ -73,7 +73,7 @@ def _rank_main(rank, port, q, mode):
             n = 2 << 20
             if rank == 1:
                 from distributed_llms_amd.parallel.rccl_transport import comm_stream
-                rs, cs = comm_stream("cuda", []), torch.cuda.Stream()     # the transport's stream kinds
+                rs, cs = comm_stream("cuda", "recv"), torch.cuda.Stream()     # the transport's stream kinds
                 dst = torch.zeros(n, dtype=torch.uint8, device="cuda")
                 x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
                 torch.cuda.synchronize()
@@ -214,7 +214,7 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
         ref = gemm.linear_pf(x, w)
         solo = _time(lambda: gemm.linear_pf(x, w))
     from distributed_llms_amd.parallel.rccl_transport import comm_stream
-    spin_stream = comm_stream("cuda", [])             # own hardware queue: only the CUs are shared
+    spin_stream = comm_stream("cuda", "recv")         # own hardware queue: only the CUs are shared
     wv, keep = _spinner(k, spin_stream, 40, 30.0)
     try:
         time.sleep(0.05)
@@ -233,7 +233,7 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     assert beside <= 1.1 * solo, (solo, beside)
     # the static walk: the blocked workgroups' whole shares start only when other workgroups have
     # retired (a second round of 12 tiles: ~2x), while the dynamic queue hands their tiles out
-    spin_stream2 = comm_stream("cuda", [])
+    spin_stream2 = comm_stream("cuda", "recv")
     wv2, keep2 = _spinner(k, spin_stream2, 40, 1.5)
     time.sleep(0.05)
     with knobs.override(pf_dynamic=False):
@@ -311,12 +311,18 @@ def test_comm_stream_hardware_queue_isolation(cuda):
 
     pool = [torch.cuda.Stream() for _ in range(7)]
     blocked_pool, s1 = probe(torch.cuda.Stream(), [torch.cuda.current_stream()] + pool)
-    comm = [comm_stream("cuda", []) for _ in range(4)]
-    blocked_comm, s2 = probe(comm[0], [torch.cuda.current_stream()] + pool + comm[1:])
-    print(f"spinning in a pool stream blocks {blocked_pool} of [default, pool 0..6]; "
-          f"in a comm stream: {blocked_comm} of [default, pool 0..6, comm 1..3]")
-    assert s1 and s2                                  # the probes ran beside a live spinner
-    assert blocked_comm == []
+    roles = ["recv", "send", "ring", "copy"]
+    comm = {r: comm_stream("cuda", r) for r in roles}
+    assert comm_stream("cuda", "recv") is comm["recv"]          # one stream per role and device
+    res = {}
+    for spin_role in ("recv", "ring"):
+        rest = [r for r in roles if r != spin_role]
+        res[spin_role] = probe(comm[spin_role], [torch.cuda.current_stream()] + pool + [comm[r] for r in rest])
+        print(f"spinning in the {spin_role} comm stream blocks {res[spin_role][0]} of "
+              f"[default, pool 0..6, {', '.join(rest)}]")
+    print(f"spinning in a pool stream blocks {blocked_pool} of [default, pool 0..6]")
+    assert s1 and all(live for _, live in res.values())     # the probes ran beside a live spinner
+    assert all(blocked == [] for blocked, _ in res.values())
 
 
 def test_wide_gemm_grids_leave_comm_cus_free(cuda):
@@ -342,7 +348,7 @@ def test_wide_gemm_grids_leave_comm_cus_free(cuda):
         assert gemm.wide_splits(256, 4096, 14336) == 7
         ref = down()
         solo = _time(down, 20)
-        st = comm_stream("cuda", [])
+        st = comm_stream("cuda", "recv")
         wv, keep = _spinner(k, st, 40, 30.0, channels=4)
         time.sleep(0.05)
         try:
