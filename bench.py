@@ -64,6 +64,10 @@ def parse(argv=None):
                     help="open-loop latency mode (1 GPU): requests arrive as a Poisson process of this many "
                          "requests/s (steps x batch requests in all) instead of a batch per round; reports "
                          "p50/p99 request latency, TTFT and ITL under that load (the headline mode is unchanged)")
+    ap.add_argument("--comm-timeout", type=float, default=600.0,
+                    help="pipeline ranks: a peer silent this long makes the rank raise (EngineConfig.comm_timeout_s)")
+    ap.add_argument("--hang-dump", type=float, default=0.0,
+                    help="diagnostics: dump every thread's Python stack every N seconds (0 = off)")
     ap.add_argument("--mixed-tokens", type=int, default=None,
                     help="EngineConfig.mixed_prefill_tokens: prompt tokens a step may add to running decode "
                          "rows (0 = prefill-first steps; default: the config's)")
@@ -259,6 +263,11 @@ def run_open_loop(args):
 
 def main(argv=None):
     args = parse(argv)
+    if args.hang_dump > 0:
+        # every rank prints all its threads' Python stacks every hang_dump seconds (stderr): where a
+        # stuck pipeline's host is waiting
+        import faulthandler
+        faulthandler.dump_traceback_later(args.hang_dump, repeat=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.rate > 0:
         if world > 1 or args.gpus > 1:

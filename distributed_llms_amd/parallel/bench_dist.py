@@ -33,7 +33,8 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
                         max_prefill_tokens=pf_tokens,
                         max_seq_len=args.prompt_len + args.gen_len + 32,
                         use_graphs=not args.no_graphs and ctx.tp == 1,
-                        num_workers=ctx.pp, seed=args.seed, quant=getattr(args, "quant", "none"))
+                        num_workers=ctx.pp, seed=args.seed, quant=getattr(args, "quant", "none"),
+                        comm_timeout_s=getattr(args, "comm_timeout", 600.0))
     t0 = time.perf_counter()
     role = RankRole(ctx, ecfg)
     _sync(ctx)
