@@ -87,10 +87,11 @@ class Knobs:
     defer_o: bool = True              # split-K o-proj reduce fused into the next add + RMSNorm
     lookahead: bool = True            # single-GPU engine: issue step n+1 before step n's tokens land
     pp_lookahead: bool = True         # pipeline driver: the same across stages
-    # RCCL transport comm streams (send / recv / ring / ids copy) on high-priority streams, i.e.
-    # hardware queues of their own: a spinning receive or a stream-wait never blocks the compute
-    # stream's queue (CU-masked streams share the default stream's queue: profiles/round5_comm_queues.md)
-    comm_own_queues: bool = True
+    # RCCL transport comm streams (send / recv / ring / ids copy): "pool" (torch pool streams) or
+    # "priority" (one native high-priority stream per role: a queue of its own, but a spinning
+    # high-priority kernel starves the compute queues -- pp2 73 % of IPC, pp4 stalled;
+    # parallel/rccl_transport.comm_stream, profiles/round5_comm_queues.md)
+    comm_queue: str = "pool"
     # ---- MoE (ops/moe.py)
     moe_variant: int = 0
     moe_wide_min_pairs: int = 8       # token-expert pairs per expert from which the tiled GEMM serves

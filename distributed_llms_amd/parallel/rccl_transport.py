@@ -59,23 +59,24 @@ _COMM_STREAMS = {}
 
 
 def comm_stream(device, role: str = "comm"):
-    """The stream of one communication role ("send", "recv", "ring", "copy") on a hardware queue of
-    its own.
+    """The stream of one communication role ("send", "recv", "ring", "copy").
 
     HIP deals a process's streams over GPU_MAX_HW_QUEUES (4) hardware queues, and a queue runs in
     order: a receive kernel spinning in it (a posted ncclRecv whose peer has not sent yet) or a
-    stream-wait on an event holds up every later kernel of every stream sharing that queue -- the
-    compute stream too (round-2 rehearsal: the ids copy stream's wait stalled stage 0's compute),
-    or another comm role's kernel (a send stuck behind a receive is a pipeline deadlock).
-    Measured on MI355X (scripts/hwq_probe.py, profiles/round5_comm_queues.md): CU-masked streams
-    share ONE queue with the default stream; high-priority streams come from a queue pool of their
-    own, one new queue per stream until the limit.  So each role gets ONE native high-priority
-    stream per device and process (created on first use, never destroyed: torch's allocators may
-    hold events recorded on it until exit), at most four in all -- every role on a queue no other
-    stream of the process uses.  knobs.comm_own_queues off: torch pool streams."""
+    stream-wait on an event holds up every later kernel of every stream sharing that queue.
+    Measured on MI355X (scripts/hwq_probe.py, profiles/round5_comm_queues.md):
+      * torch pool streams (default, ``knobs.comm_queue = "pool"``): a spinner blocks the pool
+        streams dealt to its queue; pp4 over the device stand-in keeps 97 % of the IPC rehearsal;
+      * high-priority streams (``"priority"``: one native stream per role, created once, never
+        destroyed) each get a queue of their own -- but a spinning high-priority kernel starves
+        normal-priority work: pp2 kept 73 % of IPC, and pp4 stalled until the spinners' deadlines;
+      * CU-masked streams all share ONE queue with the default stream (not offered).
+    So the roles use pool streams; the pipeline's ordering never needs a send to pass a posted
+    receive in one queue (activations flow downstream only, and stage 0 posts a slot's ids receive
+    after that slot's forward)."""
     from .. import knobs
     dev = torch.device(device)
-    if not knobs.K.comm_own_queues:
+    if knobs.K.comm_queue != "priority":
         return torch.cuda.Stream(device=dev)
     key = (dev.index or 0, role)
     st = _COMM_STREAMS.get(key)

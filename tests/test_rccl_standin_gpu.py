@@ -72,8 +72,7 @@ def _rank_main(rank, port, q, mode):
             # kernel spins on its CUs (rank 0 sends only after rank 1 reported its GEMMs finished)
             n = 2 << 20
             if rank == 1:
-                from distributed_llms_amd.parallel.rccl_transport import comm_stream
-                rs, cs = comm_stream("cuda", "recv"), torch.cuda.Stream()     # the transport's stream kinds
+                rs, cs = torch.cuda.Stream(), torch.cuda.Stream()
                 dst = torch.zeros(n, dtype=torch.uint8, device="cuda")
                 x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
                 torch.cuda.synchronize()
@@ -183,6 +182,15 @@ def _spinner(k, stream, lds_kib, timeout_s, channels=8):
     return wv, (inbox, dst)
 
 
+def _iso_stream(role):
+    """A stream on a hardware queue no other stream of this process uses (the transport's
+    comm_queue="priority" streams): a spinner there shares only CUs with the timed work."""
+    from distributed_llms_amd import knobs
+    from distributed_llms_amd.parallel.rccl_transport import comm_stream
+    with knobs.override(comm_queue="priority"):
+        return comm_stream("cuda", role)
+
+
 def _time(fn, n=10):
     """Median ms of fn on the current stream -- waiting on its events only: a device-wide
     synchronize would also wait for the spinner on the other stream."""
@@ -213,8 +221,7 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     with knobs.override(pf_dynamic=True):
         ref = gemm.linear_pf(x, w)
         solo = _time(lambda: gemm.linear_pf(x, w))
-    from distributed_llms_amd.parallel.rccl_transport import comm_stream
-    spin_stream = comm_stream("cuda", "recv")         # own hardware queue: only the CUs are shared
+    spin_stream = _iso_stream("recv")                 # own hardware queue: only the CUs are shared
     wv, keep = _spinner(k, spin_stream, 40, 30.0)
     try:
         time.sleep(0.05)
@@ -233,7 +240,7 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     assert beside <= 1.1 * solo, (solo, beside)
     # the static walk: the blocked workgroups' whole shares start only when other workgroups have
     # retired (a second round of 12 tiles: ~2x), while the dynamic queue hands their tiles out
-    spin_stream2 = comm_stream("cuda", "recv")
+    spin_stream2 = _iso_stream("recv")
     wv2, keep2 = _spinner(k, spin_stream2, 40, 1.5)
     time.sleep(0.05)
     with knobs.override(pf_dynamic=False):
@@ -278,12 +285,13 @@ def test_gemm_pf_dynamic_queue_bit_exact_and_reusable(cuda):
 def test_comm_stream_hardware_queue_isolation(cuda):
     """HIP gives a process GPU_MAX_HW_QUEUES (4) hardware queues and deals streams over them; work in
     one queue runs in order, so a receive kernel spinning in a queue holds up every later kernel of
-    every stream sharing it (round-4 review: stage 0 runs ~5 streams).  A spinner in a pool stream
-    blocks some pool streams; in a comm stream (parallel/rccl_transport.comm_stream: a high-priority
-    stream, a hardware queue of its own) it blocks neither the default stream, nor any of 7 pool
-    streams, nor the other comm streams (send / recv / ring of one stage)."""
+    every stream sharing it.  A spinner in a pool stream blocks some pool streams; the transport's
+    comm_queue="priority" streams (one native high-priority stream per role) each sit on a queue of
+    their own: a spinner in one blocks neither the default stream, nor any of 7 pool streams, nor
+    the other roles' streams.  (The transport defaults to pool streams all the same: in the
+    multi-process rehearsal spinning high-priority kernels starved the compute queues --
+    profiles/round5_comm_queues.md.)"""
     from distributed_llms_amd import _ext
-    from distributed_llms_amd.parallel.rccl_transport import comm_stream
     k = _ext.kernels()
 
     def probe(spin_stream, others):
@@ -312,8 +320,8 @@ def test_comm_stream_hardware_queue_isolation(cuda):
     pool = [torch.cuda.Stream() for _ in range(7)]
     blocked_pool, s1 = probe(torch.cuda.Stream(), [torch.cuda.current_stream()] + pool)
     roles = ["recv", "send", "ring", "copy"]
-    comm = {r: comm_stream("cuda", r) for r in roles}
-    assert comm_stream("cuda", "recv") is comm["recv"]          # one stream per role and device
+    comm = {r: _iso_stream(r) for r in roles}
+    assert _iso_stream("recv") is comm["recv"]                  # one stream per role and device
     res = {}
     for spin_role in ("recv", "ring"):
         rest = [r for r in roles if r != spin_role]
@@ -332,7 +340,7 @@ def test_wide_gemm_grids_leave_comm_cus_free(cuda):
     reservation (ops/gemm.reserve_cus_for_comm) the grid is 224 workgroups and keeps its solo time."""
     from distributed_llms_amd import _ext
     from distributed_llms_amd.ops import gemm
-    from distributed_llms_amd.parallel.rccl_transport import COMM_CUS, comm_stream
+    from distributed_llms_amd.parallel.rccl_transport import COMM_CUS
     k = _ext.kernels()
     torch.manual_seed(0)
     x = torch.randn(256, 14336, device="cuda", dtype=torch.bfloat16)
@@ -348,7 +356,7 @@ def test_wide_gemm_grids_leave_comm_cus_free(cuda):
         assert gemm.wide_splits(256, 4096, 14336) == 7
         ref = down()
         solo = _time(down, 20)
-        st = comm_stream("cuda", "recv")
+        st = _iso_stream("recv")
         wv, keep = _spinner(k, st, 40, 30.0, channels=4)
         time.sleep(0.05)
         try:
