@@ -53,15 +53,24 @@ class PendingIds:
     ``wait()`` returns the ids tensor once it may be used: on a GPU stage it orders the CURRENT
     stream after the arrival (no host block); on CPU it blocks.  ``host()`` returns them as numpy
     (blocking); with a ``copy_stream`` the device -> pinned copy is queued at post time so the
-    host read later finds it done."""
+    host read later finds it done.
+
+    ``post``: a DEFERRED device receive (RCCL transport).  Nothing is enqueued until the ids are
+    first needed: ``wait()`` runs ``post()`` on the current stream -- the receive lands right in
+    front of its consumer -- and queues the device -> pinned copy behind it; ``host()`` does the same
+    and blocks.  A receive posted early on a stream of its own spins in that stream's hardware
+    queue for a whole pipeline cycle, and HIP shares queues between streams: whatever compute
+    shares it stalls until the ids arrive (pp2 over the device stand-in: stage 0 busy 69 %,
+    76 % of the IPC rehearsal; profiles/round5_pp_rehearsal.md)."""
 
     def __init__(self, tensor: Optional[torch.Tensor] = None, work=None, ready=None, fetch=None,
-                 copy_stream=None, timeout_s: float = 600.0):
+                 copy_stream=None, timeout_s: float = 600.0, post=None):
         self.tensor = tensor
         self.timeout_s = timeout_s
         self._work = work          # torch.distributed Work (NCCL: stream-orders; gloo: blocks)
         self._ready = ready        # torch.cuda.Event recorded when `tensor` was filled
         self._fetch = fetch        # loopback: blocking getter -> (tensor, event or None)
+        self._post = post          # deferred device receive: enqueue on the current stream
         self._host = None
         self._host_ev = None
         self._foreign = False
@@ -73,7 +82,26 @@ class PendingIds:
                 self._host_ev = torch.cuda.Event()
                 self._host_ev.record(copy_stream)
 
+    @property
+    def posted(self) -> bool:
+        return self._post is None
+
+    def post(self):
+        """Enqueue the deferred receive (and the host copy behind it) on the current stream."""
+        if self._post is None:
+            return
+        post, self._post = self._post, None
+        post()
+        cur = torch.cuda.current_stream()
+        self._host = torch.empty(self.tensor.shape, dtype=self.tensor.dtype).pin_memory()
+        self._host.copy_(self.tensor, non_blocking=True)
+        self._host_ev = torch.cuda.Event()
+        self._host_ev.record(cur)
+
     def wait(self) -> torch.Tensor:
+        if self._post is not None:
+            self.post()                # stream-ordered: the receive precedes its consumers
+            return self.tensor
         if self._fetch is not None:
             self.tensor, self._ready = self._fetch()
             self._fetch = None
@@ -92,6 +120,8 @@ class PendingIds:
         return self.tensor
 
     def host(self) -> np.ndarray:
+        if self._post is not None:
+            self.post()
         if self._host_ev is not None:
             sync_event(self._host_ev, self.timeout_s, "sampled ids from the last stage")
             return self._host.numpy()

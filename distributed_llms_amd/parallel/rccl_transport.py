@@ -25,6 +25,8 @@ on the ids ring are bounded the same way (comm.PendingIds).
 """
 from __future__ import annotations
 
+import collections
+
 import torch
 import torch.distributed as dist
 
@@ -172,13 +174,16 @@ class RcclTransport(DistTransport):
         # sampled-ids ring closure: int32 slots of max_ids, deeper than the in-flight window
         self.max_ids = int(max_ids or max_rows)
         self.id_slots = 2 * window + 2
-        self.ring_stream = self._stream("ring") if (self.ring_out or self.ring_in) else None
+        # ring stream: the last stage's ids sends only (stage 0 posts each ids receive lazily on
+        # its compute stream, in front of the consumer: PendingIds(post=...))
+        self.ring_stream = self._stream("ring") if (self.ring_out or (self.ring_in and (loopback or self.host))) else None
         self.ids_tx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_out else None
         self.ids_rx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_in else None
         self._ids_sent = [None] * self.id_slots
         self._ids_users = [None] * self.id_slots   # per rx slot: the PendingIds of its last use
         self._ids_tx_n = self._ids_rx_n = 0
         self._ids_deferred = []
+        self._ids_unposted = collections.deque()   # PendingIds whose receive is not enqueued yet
         self._copy_stream = None
 
     # streams / events of this stage's device (no-op shims on a CPU stage)
@@ -282,10 +287,21 @@ class RcclTransport(DistTransport):
         from .comm import PendingIds
         if n_ids > self.max_ids:
             raise ValueError(f"{n_ids} sampled ids exceed the ring slot ({self.max_ids})")
-        cur = self._cur()
         n = self._ids_rx_n
         self._ids_rx_n += 1
         slot = n % self.id_slots
+        if not self.loopback and not self.host:
+            # deferred: enqueued on the consumer's stream when first needed (wait / host), after
+            # every earlier receive -- p2p receives match in issue order.  The slot's previous
+            # users (lookahead gathers, its host copy) are on that same stream, so stream order
+            # protects the slot
+            buf = self.ids_rx[slot, :n_ids]
+            p = PendingIds(buf, timeout_s=self.timeout_s)
+            p._post = lambda p=p: self._post_ids_through(p)
+            self._ids_unposted.append(p)
+            self._ids_users[slot] = p
+            return p
+        cur = self._cur()
         rs = self.ring_stream
         # the slot's previous ids: consumed by device work enqueued before now (lookahead gathers)
         # and by their host copy
@@ -319,6 +335,19 @@ class RcclTransport(DistTransport):
         self._ids_users[slot] = p
         return p
 
+    def _post_ids_through(self, p):
+        """Enqueue the deferred ids receives up to and including ``p`` on the current stream."""
+        while self._ids_unposted:
+            q = self._ids_unposted[0]
+            if q is not p:
+                q.post()                       # earlier receive first (its own host copy too)
+                continue
+            self._ids_unposted.popleft()
+            cur = torch.cuda.current_stream(self.device)
+            self.ring_in.recv(p.tensor.data_ptr(), p.tensor.numel() * 4, 0, cur.cuda_stream)
+            return
+        raise RuntimeError("ids receive posted twice or out of order")
+
     def _comms(self):
         return list({id(c): c for c in (self.comm_in, self.comm_out, self.ring_in, self.ring_out)
                      if c is not None}.values())
@@ -333,6 +362,8 @@ class RcclTransport(DistTransport):
         return ""
 
     def drain(self):
+        while self._ids_unposted:              # keep the ring's receive sequence complete
+            self._ids_unposted[0].post()
         super().drain()
         for s in (self.send_stream, self.recv_stream, self.ring_stream):
             if s is not None:
