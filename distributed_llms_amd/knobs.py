@@ -92,6 +92,10 @@ class Knobs:
     # high-priority kernel starves the compute queues -- pp2 73 % of IPC, pp4 stalled;
     # parallel/rccl_transport.comm_stream, profiles/round5_comm_queues.md)
     comm_queue: str = "pool"
+    # device RCCL stand-in (parallel/rccl_standin.py, rehearsal only): LDS each channel workgroup
+    # holds (40 KiB keeps a 128 / 144 KiB GEMM workgroup off its CU: the worst case) and channels
+    standin_lds_kib: int = 40
+    standin_channels: int = 4
     # ---- MoE (ops/moe.py)
     moe_variant: int = 0
     moe_wide_min_pairs: int = 8       # token-expert pairs per expert from which the tiled GEMM serves

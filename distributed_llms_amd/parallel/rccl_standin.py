@@ -66,13 +66,13 @@ _D2H, _H2D = 2, 1
 log = logging.getLogger("dllm.rccl_standin")
 _warned = False
 
-# device inbox geometry: SLOTS chunks of CHUNK bytes in flight per edge, CHANNELS workgroups per
-# send / recv kernel (each moves a 1/CHANNELS piece of every chunk; RCCL's p2p channels)
+# device inbox geometry: SLOTS chunks of CHUNK bytes in flight per edge, knobs.standin_channels
+# workgroups per send / recv kernel (each moves a 1/channels piece of every chunk; RCCL's p2p
+# channels), each holding knobs.standin_lds_kib of LDS (default 40 KiB: a co-resident 128 KiB
+# gemm_pf / 144 KiB gemm_wide workgroup cannot share its CU -- the worst case)
 CHUNK = 1 << 20
 SLOTS = 4
 CHANNELS = 4
-# LDS each channel workgroup reserves: 40 KiB keeps a co-resident 128 KiB gemm_pf workgroup off its
-# CU (the worst case a communication kernel can inflict on a persistent GEMM's schedule)
 LDS_BYTES = 40 << 10
 
 
@@ -132,6 +132,8 @@ class RcclComm:
         self._deadline_wait([f"{self._key}/member/{r}" for r in range(self.nranks)], "communicator init")
         for r in range(self.nranks):
             self._peers[r] = int(self._store.get(f"{self._key}/member/{r}"))
+        from .. import knobs
+        self._channels = max(1, int(knobs.K.standin_channels))   # both ends of an edge: one value
         self._words = None
         self._inbox = {}          # peer -> this rank's inbox tensor for messages FROM peer
         self._outbox = {}         # peer -> device pointer of the peer's inbox for messages from here
@@ -195,9 +197,10 @@ class RcclComm:
             r_inbox = self._inbox[rpeer].data_ptr()
             r_seq = self._seq_rx.get(rpeer, 0)
             self._seq_rx[rpeer] = r_seq + -(-int(rbytes) // CHUNK)
+        from .. import knobs
         self._k.p2p_standin(int(sptr) if sbytes else 0, s_inbox, int(sbytes), s_seq, int(rptr) if rbytes else 0,
-                            r_inbox, int(rbytes), r_seq, CHUNK, SLOTS, CHANNELS, self._words, self.timeout_s,
-                            self._words + 4, LDS_BYTES, int(stream))
+                            r_inbox, int(rbytes), r_seq, CHUNK, SLOTS, self._channels, self._words, self.timeout_s,
+                            self._words + 4, knobs.K.standin_lds_kib << 10, int(stream))
 
     def _self_copy(self, dst, src, nbytes, stream):
         from .. import _ext
