@@ -64,8 +64,11 @@ class Knobs:
     pp_proj_min_m: int = 257
     pp_persistent: bool = True
     # gemm_pf pulls its tiles from per-XCD device queues (a workgroup that starts late -- its CU held
-    # by a co-resident RCCL / stand-in kernel -- finds them taken) instead of the static w + i P walk
-    pf_dynamic: bool = True
+    # by a co-resident RCCL / stand-in kernel -- finds them taken) instead of the static w + i P walk:
+    # "on", "off", or "auto" = on while a transport with spinning comm kernels is live
+    # (ops/gemm.reserve_cus_for_comm).  Alone on the GPU the static walk is 0.3 % faster end to end
+    # (TTFT 343 vs 346 ms, two interleaved pairs, gpurun_out/r5j_bench.log)
+    pf_dynamic: str = "auto"
     # gemm_pf main-loop schedule for prefill projections: 0 = the shipped schedule 2 (pieces every 5
     # MFMAs after one mid-K-tile barrier); 9..11 = A / B LDS regions released separately
     pf_schedule: int = 0

@@ -176,6 +176,15 @@ _comm_cus = 0
 _comm_users = 0
 
 
+def pf_dynamic() -> bool:
+    """gemm_pf's dynamic tile queue: knobs.pf_dynamic "on" / "off" / "auto" (on while comm kernels
+    may hold CUs)."""
+    v = str(knobs.K.pf_dynamic).strip().lower()
+    if v == "auto":
+        return _comm_cus > 0
+    return v in ("1", "true", "on", "yes")
+
+
 def reserve_cus_for_comm(n: int) -> None:
     """A transport with spinning comm kernels starts: size gemm_wide grids around ``n`` CUs."""
     global _comm_cus, _comm_users
@@ -286,13 +295,16 @@ def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, variant: i
     y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
     if variant == 0 and knobs.K.pf_schedule:
         variant = knobs.K.pf_schedule  # split-release schedules 9..11 (gemm_pp.hip pf_sched)
+    # the split-release schedules 9..11 exist only in the dynamic-queue form
+    dyn = (pf_dynamic() or variant >= 9) and k >= 128
     if torch.cuda.is_current_stream_capturing():
         # inside a graph: the static tile walk.  A tile queue is per stream and self-resetting, but
         # a replay may run on another stream beside eager launches that use the same queue
-        if variant >= 9:
-            variant = 0
-    elif knobs.K.pf_dynamic and k >= 128 and (variant in (0, 8) or variant >= 9):
+        dyn = False
+    if dyn and (variant in (0, 8) or variant >= 9):
         variant |= 16                  # per-XCD dynamic tile queues (gemm_pp.hip, DYN)
+    elif variant >= 9:
+        variant = 0
     _ext.kernels().gemm_pf(y.data_ptr(), x.data_ptr(), w.data_ptr(), m, n, k, 1 if swiglu else 0, variant,
                            torch.cuda.current_stream().cuda_stream)
     return y

@@ -150,3 +150,20 @@ def test_wide_splits_leave_comm_cus_free():
     finally:
         gemm.release_cus_for_comm()
     assert [gemm.wide_splits(*s) for s in shapes] == base
+
+
+def test_pf_dynamic_auto_follows_comm_reservation():
+    from distributed_llms_amd import knobs
+    from distributed_llms_amd.ops import gemm
+    assert knobs.K.pf_dynamic == "auto" and not gemm.pf_dynamic()
+    gemm.reserve_cus_for_comm(16)
+    try:
+        assert gemm.pf_dynamic()
+        with knobs.override(pf_dynamic="off"):
+            assert not gemm.pf_dynamic()
+    finally:
+        gemm.release_cus_for_comm()
+    with knobs.override(pf_dynamic=True):
+        assert gemm.pf_dynamic()
+    with knobs.override(pf_dynamic=0):
+        assert not gemm.pf_dynamic()
