@@ -36,15 +36,15 @@ class Knobs:
     wide_variant: int = 33
     wide_variant_split: int = 1
     wide_gate_up_max_m: int = 256     # SwiGLU-fused gate|up on gemm_wide up to this M (then hipBLASLt)
-    wide_down_max_m: int = 512        # MLP down (K >= 8192, K > N) up to this M
-    wide_proj_max_m: int = 256        # qkv / o / LM head up to this M (K >= 8192: the down limit)
+    wide_down_max_m: int = 384        # MLP down (K >= 8192, K > N) up to this M (512: split gemm_pp 59 vs 66 us)
+    wide_proj_max_m: int = 256        # qkv / LM head up to this M (o: wide_o_max_m; down: wide_down_max_m)
     wide_target_wgs: int = 256        # split-K: about one workgroup per CU
-    # medium M (mixed prefill + decode steps, short prefills): above the decode cutovers and up to
-    # this M, a projection whose gemm_pf grid would fill less than pf_min_fill of the CUs (256 x 256
-    # tiles: N / 256 x M / 256) runs on gemm_wide (256 x 128 tiles, several row tiles, split-K to fill
-    # the CUs) instead; 0 = off (bench/medium_m_bench.py)
-    wide_mid_max_m: int = 0
-    pf_min_fill: float = 0.75
+    # medium M (mixed prefill + decode steps, short prompts; profiles/round5_medium_m_gemm.md): above
+    # the decode cutovers a projection runs on gemm_pf only where its 256 x 256 grid fills the CUs
+    # (ops/gemm.pf_fills: >= one tile per CU, rounds at least pf_min_eff full or >= 4 rounds), else
+    # on gemm_pp with split-K; the square o-projection stays on gemm_wide up to wide_o_max_m
+    pf_min_eff: float = 0.85
+    wide_o_max_m: int = 512
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),

@@ -40,6 +40,8 @@ def is_down_proj(n: int, k: int) -> bool:
 
 
 def _cus(device) -> int:
+    if torch.device(device).type != "cuda":
+        return 256                     # MI355X (dispatch unit tests on CPU)
     idx = device.index or 0
     n = _CUS.get(idx)
     if n is None:
@@ -50,13 +52,18 @@ def _cus(device) -> int:
 _CUS = {}
 
 
-def _use_wide_mid(m: int, n: int, k: int, x: torch.Tensor, swiglu: bool) -> bool:
-    """knobs.wide_mid_max_m: medium M whose 256 x 256 persistent grid would leave CUs idle."""
-    kn = knobs.K
-    if not (0 < kn.wide_mid_max_m and m <= kn.wide_mid_max_m) or n % 128 or k % 64:
+def pf_fills(m: int, n: int, device) -> bool:
+    """gemm_pf (one 256 x 256 tile per CU per round, no split-K) only where its grid fills the chip:
+    at least one tile per CU and rounds that are mostly full (knobs.pf_min_eff), or many rounds.
+    Below that the split-K gemm_pp grid wins at every measured M from 320 to 2048 -- gemm_pf's
+    single-round grids run one tile's whole K loop: 74-78 us for the 8B o-projection at any
+    M <= 2048, the down projection 250-283 us vs 55-174 us split (profiles/round5_medium_m_gemm.md)."""
+    cus = _cus(device)
+    tiles = (-(-m // 256)) * (n // 256)
+    if tiles < cus:
         return False
-    tiles = (-(-m // 256)) * (n // 256)              # gemm_pf's grid (SwiGLU: N = 2I, also 256-wide)
-    return tiles < kn.pf_min_fill * _cus(x.device)
+    rounds = -(-tiles // cus)
+    return rounds >= 4 or tiles / (rounds * cus) >= knobs.K.pf_min_eff
 
 
 def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
@@ -66,15 +73,15 @@ def _use_wide(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor, swiglu: 
         return False
     if not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
         return False
-    if _use_wide_mid(m, n, k, x, swiglu):
-        return True
     down = is_down_proj(n, k) and not swiglu
     if "all" in roles:
         return m <= 512 or (down and m <= kn.wide_down_max_m)
     if "auto" in roles:
         if swiglu:
             return m <= kn.wide_gate_up_max_m
-        return m <= (kn.wide_down_max_m if down else kn.wide_proj_max_m)
+        if down:
+            return m <= kn.wide_down_max_m
+        return m <= (kn.wide_o_max_m if n <= k else kn.wide_proj_max_m)
     if swiglu:
         return "gate_up" in roles and m <= 512
     return ("down" in roles) if is_down_proj(n, k) else ("proj" in roles and m <= 512)
@@ -116,9 +123,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
     if bias is None and _use_pp(m, n, k, x, w, knobs.K.pp_proj_min_m):
-        if kn.pp_persistent and m * n * 2 < (1 << 31):
+        if kn.pp_persistent and m * n * 2 < (1 << 31) and pf_fills(m, n, x.device):
             return linear_pf(x, w)
-        return linear_pp(x, w, splits=1, variant=PP_PREFILL_VARIANT)
+        # medium M (mixed prefill + decode steps, short prompts): split-K tiles fill the CUs
+        return linear_pp(x, w, variant=PP_PREFILL_VARIANT, defer=defer)
     return F.linear(x, w, bias)
 
 
@@ -378,7 +386,7 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Te
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
     if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):
-        if knobs.K.pp_persistent and m * (n // 2) * 2 < (1 << 31):
+        if knobs.K.pp_persistent and m * (n // 2) * 2 < (1 << 31) and pf_fills(m, n, x.device):
             return linear_pf(x, w_gate_up, swiglu=True)
-        return linear_pp(x, w_gate_up, splits=1, swiglu=True, variant=PP_PREFILL_VARIANT)
+        return linear_pp(x, w_gate_up, swiglu=True, variant=PP_PREFILL_VARIANT)
     return None

@@ -30,7 +30,7 @@ def test_gate_up_cutover(m, expect):
     assert gemm._use_wide(m, w.shape[0], 4096, x, w, swiglu=True) is expect
 
 
-@pytest.mark.parametrize("m,expect", [(1, True), (256, True), (384, True), (512, True), (513, False), (768, False)])
+@pytest.mark.parametrize("m,expect", [(1, True), (256, True), (384, True), (385, False), (512, False), (768, False)])
 def test_down_cutover(m, expect):
     x, w = _xw(m, 4096, 14336)
     assert gemm._use_wide(m, 4096, 14336, x, w) is expect
@@ -46,8 +46,8 @@ def test_proj_cutover(m, expect):
 # are projections ("proj" cutover), only the narrowing 28672 -> 8192 down projection is "down"
 @pytest.mark.parametrize("n,k,m,expect", [
     (10240, 8192, 256, True), (10240, 8192, 257, False), (10240, 8192, 512, False),   # qkv
-    (8192, 8192, 256, True), (8192, 8192, 384, False),                                # o
-    (8192, 28672, 384, True), (8192, 28672, 512, True), (8192, 28672, 513, False),    # down
+    (8192, 8192, 256, True), (8192, 8192, 512, True), (8192, 8192, 513, False),      # o (wide_o_max_m)
+    (8192, 28672, 384, True), (8192, 28672, 385, False), (8192, 28672, 512, False),   # down
 ])
 def test_70b_roles(n, k, m, expect):
     x, w = _xw(m, n, k)
@@ -167,3 +167,25 @@ def test_pf_dynamic_auto_follows_comm_reservation():
         assert gemm.pf_dynamic()
     with knobs.override(pf_dynamic=0):
         assert not gemm.pf_dynamic()
+
+
+def test_medium_m_dispatch_follows_the_measured_table():
+    """profiles/round5_medium_m_gemm.md: between the decode cutovers and a full gemm_pf grid the
+    split-K gemm_pp wins; the o-projection stays on gemm_wide to M = 512, down to M = 384."""
+    import torch
+    from distributed_llms_amd.ops import gemm
+    cpu = torch.device("cpu")
+    # gemm_pf only with a full grid: (M / 256) x (N / 256) tiles >= CUs, rounds mostly full
+    assert not gemm.pf_fills(2048, 6144, cpu)          # 192 tiles
+    assert not gemm.pf_fills(640, 28672, cpu)          # 336 tiles: 2 rounds, 66 % full
+    assert gemm.pf_fills(1024, 28672, cpu)             # 448 tiles: 88 % full
+    assert gemm.pf_fills(4096, 4096, cpu) and gemm.pf_fills(32768, 6144, cpu)
+    assert not gemm.pf_fills(4096, 6144, cpu)          # 384 tiles: 75 % full
+    x, w = _xw(512, 4096, 4096)
+    assert gemm._use_wide(512, 4096, 4096, x, w)       # o
+    x, w = _xw(320, 6144, 4096)
+    assert not gemm._use_wide(320, 6144, 4096, x, w)   # qkv -> split-K gemm_pp
+    x, w = _xw(384, 4096, 14336)
+    assert gemm._use_wide(384, 4096, 14336, x, w)      # down
+    x, w = _xw(512, 4096, 14336)
+    assert not gemm._use_wide(512, 4096, 14336, x, w)
