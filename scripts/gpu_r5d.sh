@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 T="timeout -k 10"
-$T 600 python bench/pp_bench.py --no-decode --prefill 32768 8192 --rounds 3 --pf-variants 9 10 11 > gpurun_out/r5d_pf_sched.txt 2>&1 || { echo "pf schedule sweep failed"; tail -30 gpurun_out/r5d_pf_sched.txt; exit 1; }
+$T 600 python bench/pp_bench.py --no-decode --prefill 32768 8192 --rounds 3 --pf-variants 9 10 11 16 > gpurun_out/r5d_pf_sched.txt 2>&1 || { echo "pf schedule sweep failed"; tail -30 gpurun_out/r5d_pf_sched.txt; exit 1; }
 cat gpurun_out/r5d_pf_sched.txt | grep prefill
 for kn in "moe_persistent=0" ""; do
   DLLM_KNOBS="$kn" $T 400 python bench.py --model mixtral-8x7b --steps 2 --warmup 1 > gpurun_out/r5d_mixtral.log 2>&1 || { echo "mixtral bench failed"; tail -30 gpurun_out/r5d_mixtral.log; exit 1; }
