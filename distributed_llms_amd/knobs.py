@@ -103,8 +103,10 @@ class Knobs:
     moe_variant: int = 0
     moe_wide_min_pairs: int = 8       # token-expert pairs per expert from which the tiled GEMM serves
     moe_fused_router: bool = True
-    # prefill grouped expert GEMMs on the persistent gemm_pf (MOE form) instead of gemm_pp_moe
-    moe_persistent: bool = True
+    # prefill grouped expert GEMMs on the persistent gemm_pf (MOE form) instead of gemm_pp_moe: off --
+    # measured slower in-engine (Mixtral B = 256: TTFT 742 vs 689 ms, 10,070 vs 10,272 tok/s; gate|up
+    # 13.3 ms per layer vs gemm_pp_moe's 11.6, gpurun_out/r5d_mixtral*.txt)
+    moe_persistent: bool = False
     # grouped expert GEMM ring depth: 6 / 5 LDS slots at 64 / 128-row tiles (False: 3 slots)
     moe_deep_ring: bool = True
     # ---- FP8 W8A8 (ops/quant.py)

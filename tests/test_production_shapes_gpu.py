@@ -39,8 +39,16 @@ def _rms(x, w, eps):
     return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * w
 
 
-def _ref_logits(stage: ModelStage, w32, toks: torch.Tensor, chunk: int = 32) -> torch.Tensor:
-    """fp32 forward of ``toks`` [B, T] (all positions, causal); last-position logits [B, V]."""
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _ref_logits(stage: ModelStage, w32, toks: torch.Tensor, chunk: int = 32, rnd=None) -> torch.Tensor:
+    """fp32 forward of ``toks`` [B, T] (all positions, causal); last-position logits [B, V].
+    ``rnd``: applied to every op's output -- ``_bf`` gives the bf16-storage / fp32-compute forward
+    (what an exact bf16 kernel stack would produce): its distance from the fp32 one is the error
+    floor of bf16 activations."""
+    r = rnd or (lambda t: t)
     cfg = stage.cfg
     hq, hkv, d, eps = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, cfg.norm_eps
     out, margin = [], []
@@ -51,16 +59,16 @@ def _ref_logits(stage: ModelStage, w32, toks: torch.Tensor, chunk: int = 32) -> 
         x = w32["embed"][t]
         gap = torch.full((b,), float("inf"), device=t.device)
         for lw in w32["layers"]:
-            h = _rms(x, lw["attn_norm"], eps)
-            qkv = (h @ lw["wqkv"].t()).view(b * n, hq + 2 * hkv, d)
-            q = ref.apply_rope(qkv[:, :hq], pos, stage.cos_sin).view(b, n, hq, d).transpose(1, 2)
-            k = ref.apply_rope(qkv[:, hq:hq + hkv], pos, stage.cos_sin).view(b, n, hkv, d).transpose(1, 2)
+            h = r(_rms(x, lw["attn_norm"], eps))
+            qkv = r(h @ lw["wqkv"].t()).view(b * n, hq + 2 * hkv, d)
+            q = r(ref.apply_rope(qkv[:, :hq], pos, stage.cos_sin)).view(b, n, hq, d).transpose(1, 2)
+            k = r(ref.apply_rope(qkv[:, hq:hq + hkv], pos, stage.cos_sin)).view(b, n, hkv, d).transpose(1, 2)
             v = qkv[:, hq + hkv:].reshape(b, n, hkv, d).transpose(1, 2)
             k = k.repeat_interleave(hq // hkv, dim=1)
             v = v.repeat_interleave(hq // hkv, dim=1)
-            a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=stage.scale)
-            x = x + a.transpose(1, 2).reshape(b, n, hq * d) @ lw["wo"].t()
-            h = _rms(x, lw["mlp_norm"], eps).view(b * n, -1)
+            a = r(F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=stage.scale))
+            x = r(x + a.transpose(1, 2).reshape(b, n, hq * d) @ lw["wo"].t())
+            h = r(_rms(x, lw["mlp_norm"], eps)).view(b * n, -1)
             if cfg.is_moe:
                 probs = torch.softmax(h @ lw["router"].t(), dim=-1)
                 top = probs.view(b, n, -1)[:, -1].topk(cfg.experts_per_token + 1, dim=-1).values
@@ -78,9 +86,9 @@ def _ref_logits(stage: ModelStage, w32, toks: torch.Tensor, chunk: int = 32) -> 
             else:
                 gu = h @ lw["w_gate_up"].t()
                 i = gu.shape[-1] // 2
-                y = (F.silu(gu[:, :i]) * gu[:, i:]) @ lw["w_down"].t()
-            x = x + y.view(b, n, -1)
-        out.append(_rms(x[:, -1], w32["final_norm"], eps) @ w32["lm_head"].t())
+                y = r(F.silu(gu[:, :i]) * gu[:, i:]) @ lw["w_down"].t()
+            x = r(x + y.view(b, n, -1))
+        out.append(r(_rms(x[:, -1], w32["final_norm"], eps)) @ w32["lm_head"].t())
         margin.append(gap)
     return torch.cat(out), torch.cat(margin)
 
@@ -152,7 +160,19 @@ def _run(model: str, layers: int, prompt_len: int, decode_steps: int, max_rel: f
         logits[rows] = out.float()
         eng.scheduler.complete(st, out.argmax(-1).tolist())
         n_prefill += len(st.seqs)
-    agree = [_check(logits, _ref_logits(stage, w32, toks), f"{model} prefill", max_rel, mean_rel)]
+    ref32 = _ref_logits(stage, w32, toks)
+    agree = [_check(logits, ref32, f"{model} prefill", max_rel, mean_rel)]
+    # the error floor of bf16 activations: an exact bf16-storage / fp32-compute forward against the
+    # fp32 one.  Ours (bf16 activations, f16 split-K slabs, bf16 logits) stays within 1.35x of it
+    floor = _ref_logits(stage, w32, toks, rnd=_bf)[0]
+    want, spread = ref32[0], ref32[0].std().item()
+    floor_mean = (floor - want).abs().mean().item() / spread
+    ours_mean = (logits - want).abs().mean().item() / spread
+    print(f"{model} prefill: mean err / spread {ours_mean:.5f}; bf16-activation floor {floor_mean:.5f} "
+          f"({ours_mean / floor_mean:.2f}x)", flush=True)
+    _record({"check": f"{model} prefill bf16 floor", "mean_err_rel": floor_mean, "ours_mean_err_rel": ours_mean})
+    if not cfg.is_moe:                 # MoE: near-tie routing rows differ by O(1) in either forward
+        assert ours_mean <= 1.35 * floor_mean, (ours_mean, floor_mean)
     for step in range(decode_steps):
         toks = torch.cat([toks, logits.argmax(-1, keepdim=True)], dim=1)
         st = eng.scheduler.schedule(0)
