@@ -97,6 +97,39 @@ def queues(mode):
           f"(spinner live during probe: {live})", flush=True)
 
 
+def _spin_main(lds_kib, channels, timeout_s, ready, stop):
+    from distributed_llms_amd import _ext
+    k = _ext.kernels()
+    s = torch.cuda.Stream()
+    wv, keep = spinner(k, s, lds_kib, timeout_s, channels)
+    time.sleep(0.05)
+    ready.set()
+    stop.wait(timeout_s + 30)
+    wv[0] = 1
+    s.synchronize()
+
+
+class SpinnerProc:
+    """The spinner in another process: shares CUs with the timed work, none of its hardware
+    queues, normal priority (a high-priority in-process spinner starves normal queues)."""
+
+    def __init__(self, lds_kib, channels, timeout_s=60.0):
+        import multiprocessing as mp
+        ctx = mp.get_context("spawn")
+        self.ready, self.stop = ctx.Event(), ctx.Event()
+        self.p = ctx.Process(target=_spin_main, args=(lds_kib, channels, timeout_s, self.ready, self.stop), daemon=True)
+
+    def __enter__(self):
+        self.p.start()
+        assert self.ready.wait(120)
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.p.join(timeout=90)
+        return False
+
+
 def _time(fn, n=20):
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
     for a, b in ev:
@@ -110,7 +143,6 @@ def _time(fn, n=20):
 def gemms():
     from distributed_llms_amd import _ext, knobs
     from distributed_llms_amd.ops import gemm
-    k = _ext.kernels()
     torch.manual_seed(0)
     m = 256
     shapes = {"qkv": (6144, 4096, False), "o": (4096, 4096, False), "gate_up": (28672, 4096, True),
@@ -126,24 +158,22 @@ def gemms():
         it["i"] += 1
         return gemm.linear_wide(x[kk], w, swiglu=sw)
 
-    hi = torch.cuda.Stream.priority_range()[1]
-    for lds, target in ((0, 256), (40, 256), (40, 248), (40, 240)):
-        with knobs.override(wide_target_wgs=target):
+    from distributed_llms_amd.ops.gemm import release_cus_for_comm, reserve_cus_for_comm
+    for lds, reserve in ((0, 0), (40, 0), (40, 16)):
+        if reserve:
+            reserve_cus_for_comm(reserve)
+        try:
             solo = {nm: _time(lambda nm=nm: run(nm)) for nm in shapes}
-            spin = torch.cuda.Stream(priority=hi)      # a hardware queue of its own (queues probe)
-            wv, keep = spinner(k, spin, lds, 30.0, 4)
-            time.sleep(0.05)
-            try:
-                beside = {nm: _time(lambda nm=nm: run(nm)) for nm in shapes}
-                live = not spin.query()
-            finally:
-                wv[0] = 1
-                spin.synchronize()
-        for nm, (n, kk, sw) in shapes.items():
-            s = gemm.wide_splits(m, n, kk, sw, target)
-            tiles = (n // 128) * (-(-m // gemm.wide_row_tile(m, n, kk, sw)))
-            print(f"gemms spinner LDS {lds:2d} KiB target={target} {nm:8s} wgs={tiles * s:4d} solo {solo[nm]:7.1f} us  beside a 4-CU "
-                  f"spinner {beside[nm]:7.1f} us  ({beside[nm] / solo[nm]:.2f}x; spinner live {live})", flush=True)
+            with SpinnerProc(lds, 4):
+                beside = {nm: min(_time(lambda nm=nm: run(nm)) for _ in range(3)) for nm in shapes}
+            for nm, (n, kk, sw) in shapes.items():
+                s = gemm.wide_splits(m, n, kk, sw)
+                tiles = (n // 128) * (-(-m // gemm.wide_row_tile(m, n, kk, sw)))
+                print(f"gemms spinner LDS {lds:2d} KiB reserved CUs {reserve:2d} {nm:8s} wgs={tiles * s:4d} solo {solo[nm]:7.1f} us  "
+                      f"beside a 4-CU spinner (other process) {beside[nm]:7.1f} us  ({beside[nm] / solo[nm]:.2f}x)", flush=True)
+        finally:
+            if reserve:
+                release_cus_for_comm()
 
 
 if __name__ == "__main__":

@@ -44,9 +44,9 @@ def test_small_m_swiglu(cuda, m, inter, k):
 
 
 def test_large_m_uses_hand_written_prefill_gemm(cuda):
-    x, w = _bf(300, 512), _bf(256, 512, scale=0.05)
-    assert not gemm._use_wide(300, 256, 512, x, w)
-    assert gemm._use_pp(300, 256, 512, x, w, gemm.knobs.K.pp_proj_min_m)
+    x, w = _bf(300, 256), _bf(512, 256, scale=0.05)          # a qkv-like (N > K) projection
+    assert not gemm._use_wide(300, 512, 256, x, w)
+    assert gemm._use_pp(300, 512, 256, x, w, gemm.knobs.K.pp_proj_min_m)
     y = ops.linear(x, w)
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
 

@@ -142,8 +142,10 @@ def _run(model: str, layers: int, prompt_len: int, decode_steps: int, max_rel: f
            "embed": stage.embed["embed"].float(), "final_norm": stage.head["final_norm"].float(),
            "lm_head": stage.lm_head_weight().float()}
     per_seq = -(-(prompt_len + decode_steps + 1) // 32)
+    # prefill-first (no mixed steps): two whole 16K-token prefill steps, then decode
     eng = LLMEngine(EngineConfig(model=model, dtype="bfloat16", device="cuda", max_batch=BATCH, max_seq_len=512,
-                                 num_kv_blocks=BATCH * per_seq + 8, graph_batch_sizes=(BATCH,)), stage)
+                                 num_kv_blocks=BATCH * per_seq + 8, graph_batch_sizes=(BATCH,),
+                                 mixed_prefill_tokens=0), stage)
     g = torch.Generator().manual_seed(3)
     prompts = torch.randint(3, cfg.vocab_size, (BATCH, prompt_len), generator=g)
     seqs = [eng.add_request(p.tolist(), SamplingParams(max_new_tokens=decode_steps + 1, ignore_eos=True))

@@ -191,6 +191,47 @@ def _iso_stream(role):
         return comm_stream("cuda", role)
 
 
+def _spin_proc_main(lds_kib, channels, timeout_s, ready, stop, q):
+    """Child: a never-matched receive spinning on `channels` CUs (normal priority, this process's
+    own hardware queues) until `stop` is set (abort word) or the deadline."""
+    from distributed_llms_amd import _ext
+    k = _ext.kernels()
+    s = torch.cuda.Stream()
+    wv, keep = _spinner(k, s, lds_kib, timeout_s, channels=channels)
+    time.sleep(0.05)
+    ready.set()
+    stop.wait(timeout_s + 30)
+    wv[0] = 1
+    s.synchronize()
+    q.put(int(wv[1]))
+
+
+class _SpinnerProc:
+    """A spinning receive in ANOTHER process: it shares the GPU's CUs with the timed work but none
+    of this process's hardware queues, and runs at normal priority (an in-process spinner lands in
+    a queue some stream of this process may share; a high-priority one starves normal queues --
+    profiles/round5_comm_queues.md).  ``verdict``: 1 = left through abort, 2 = deadline."""
+
+    def __init__(self, lds_kib, channels, timeout_s):
+        import multiprocessing as mp
+        ctx = mp.get_context("spawn")
+        self.ready, self.stop, self.q = ctx.Event(), ctx.Event(), ctx.Queue()
+        self.p = ctx.Process(target=_spin_proc_main, args=(lds_kib, channels, timeout_s, self.ready, self.stop, self.q),
+                             daemon=True)
+        self.verdict = None
+
+    def __enter__(self):
+        self.p.start()
+        assert self.ready.wait(120), "spinner process did not start"
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.verdict = self.q.get(timeout=120)
+        self.p.join(timeout=60)
+        return False
+
+
 def _time(fn, n=10):
     """Median ms of fn on the current stream -- waiting on its events only: a device-wide
     synchronize would also wait for the spinner on the other stream."""
@@ -221,37 +262,26 @@ def test_gemm_pf_beside_spinning_comm_kernel(cuda):
     with knobs.override(pf_dynamic=True):
         ref = gemm.linear_pf(x, w)
         solo = _time(lambda: gemm.linear_pf(x, w))
-    spin_stream = _iso_stream("recv")                 # own hardware queue: only the CUs are shared
-    wv, keep = _spinner(k, spin_stream, 40, 30.0)
-    try:
-        time.sleep(0.05)
-        assert not spin_stream.query()
+    with _SpinnerProc(40, 8, 60.0) as sp:
         with knobs.override(pf_dynamic=True):
-            beside = _time(lambda: gemm.linear_pf(x, w))
+            # min of three medians: the timing shares the GPU with another process
+            beside = min(_time(lambda: gemm.linear_pf(x, w)) for _ in range(3))
             y = gemm.linear_pf(x, w)
         torch.cuda.current_stream().synchronize()
-        assert not spin_stream.query(), "spinner ended early: the timing was not beside it"
-    finally:
-        wv[0] = 1
-        spin_stream.synchronize()
-    assert wv[1] == 1                                   # the spinner left through the abort word
+    assert sp.verdict == 1, "the spinner left before the timing ended"
     assert torch.equal(y, ref)                          # same tiles, same order of K: bit-identical
     print(f"gemm_pf solo {solo:.3f} ms, beside the spinner {beside:.3f} ms")
     assert beside <= 1.1 * solo, (solo, beside)
     # the static walk: the blocked workgroups' whole shares start only when other workgroups have
     # retired (a second round of 12 tiles: ~2x), while the dynamic queue hands their tiles out
-    spin_stream2 = _iso_stream("recv")
-    wv2, keep2 = _spinner(k, spin_stream2, 40, 1.5)
-    time.sleep(0.05)
-    with knobs.override(pf_dynamic=False):
-        t0 = time.perf_counter()
-        ys = gemm.linear_pf(x, w)
+    with _SpinnerProc(40, 8, 60.0) as sp:
+        with knobs.override(pf_dynamic=False):
+            static = min(_time(lambda: gemm.linear_pf(x, w)) for _ in range(3))
+            ys = gemm.linear_pf(x, w)
         torch.cuda.current_stream().synchronize()
-        static_s = time.perf_counter() - t0
-    spin_stream2.synchronize()
-    print(f"static walk beside the spinner: {static_s * 1e3:.1f} ms (spinner verdict {wv2[1]})")
+    print(f"static walk beside the spinner: {static:.3f} ms (spinner verdict {sp.verdict})")
     assert torch.equal(ys, ref)
-    assert static_s > 1.3 * beside * 1e-3
+    assert static > 1.3 * beside
 
 
 def test_gemm_pf_dynamic_queue_bit_exact_and_reusable(cuda):
@@ -356,20 +386,20 @@ def test_wide_gemm_grids_leave_comm_cus_free(cuda):
         assert gemm.wide_splits(256, 4096, 14336) == 7
         ref = down()
         solo = _time(down, 20)
-        st = _iso_stream("recv")
-        wv, keep = _spinner(k, st, 40, 30.0, channels=4)
-        time.sleep(0.05)
-        try:
-            beside = _time(down, 20)
+        with _SpinnerProc(40, 4, 60.0) as sp:
+            beside = min(_time(down, 20) for _ in range(3))
             y = down()
-            live = not st.query()
-        finally:
-            wv[0] = 1
-            st.synchronize()
+            torch.cuda.current_stream().synchronize()
+        live = sp.verdict == 1
     finally:
         gemm.release_cus_for_comm()
     assert gemm.wide_splits(256, 4096, 14336) == 8
     assert live
-    print(f"down projection, 224-workgroup grid: solo {solo * 1e3:.1f} us, beside a 4-CU spinner {beside * 1e3:.1f} us")
+    # for the record: the unreserved 256-workgroup grid beside the same spinner
+    solo256 = _time(down, 20)
+    with _SpinnerProc(40, 4, 60.0):
+        beside256 = min(_time(down, 20) for _ in range(3))
+    print(f"down projection, 224-workgroup grid: solo {solo * 1e3:.1f} us, beside a 4-CU spinner {beside * 1e3:.1f} us; "
+          f"256-workgroup grid: solo {solo256 * 1e3:.1f} us, beside {beside256 * 1e3:.1f} us")
     assert beside <= 1.15 * solo, (solo, beside)
     assert torch.isfinite(y).all() and ref.shape == (256, 4096)
