@@ -704,7 +704,7 @@ void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintpt
   DLLM_HOST_CHECK(E >= 1 && E <= 256, "1 <= experts <= 256");
   DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
-  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
+  DLLM_HOST_CHECK(mode >= 0 && mode <= 3, "mode: bit 0 SwiGLU, bit 1 static tile walk");
   DLLM_HOST_CHECK(xrows >= 1 && slots >= 1, "rows");
   DLLM_HOST_CHECK((long)xrows * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32), "operands must be < 4 GiB");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -1187,7 +1187,7 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   DLLM_HOST_CHECK(M >= 1, "M >= 1");
   DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
-  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
+  DLLM_HOST_CHECK(mode >= 0 && mode <= 3, "mode: bit 0 SwiGLU, bit 1 static tile walk");
   // the output's byte range must stay below 2^31: rows past M are dropped by giving their stores
   // the offset 0x80000000, which has to lie outside the buffer's range
   DLLM_HOST_CHECK((long)M * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32) &&
@@ -1267,7 +1267,7 @@ void gemm_pf_moe(uintptr_t y, uintptr_t xs, uintptr_t w, uintptr_t counts, uintp
   DLLM_HOST_CHECK(E >= 1 && E <= 16, "1 <= experts <= 16");
   DLLM_HOST_CHECK(K % PBK == 0 && K >= 2 * PBK, "K must be a multiple of 64, >= 128");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
-  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
+  DLLM_HOST_CHECK(mode >= 0 && mode <= 3, "mode: bit 0 SwiGLU, bit 1 static tile walk");
   DLLM_HOST_CHECK(slots >= 1, "slots");
   DLLM_HOST_CHECK((long)slots * K * 2 < (1L << 32) && (long)E * N * K * 2 < (1L << 32) &&
                       (long)slots * (mode == 1 ? N / 2 : N) * 2 < (1L << 31),
@@ -1280,13 +1280,19 @@ void gemm_pf_moe(uintptr_t y, uintptr_t xs, uintptr_t w, uintptr_t counts, uintp
   const long bound = (long)(N / 256) * ((slots + 255) / 256 + E);     // tiles upper bound
   const long grid = ((bound < cus ? bound : cus) + 7) / 8 * 8;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int* q = pf_queue(s);
-  if (mode == 1)
-    hipLaunchKernelGGL((gemm_pf_kernel<2, 0, true, true>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)xs,
-                       (const bf16*)w, (bf16*)y, slots, N, K, q, (const int*)counts, (const int*)offsets, E);
-  else
-    hipLaunchKernelGGL((gemm_pf_kernel<0, 0, true, true>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)xs,
-                       (const bf16*)w, (bf16*)y, slots, N, K, q, (const int*)counts, (const int*)offsets, E);
+  // static walk (mode bit 1): w + i P over the tile space; the workgroups whose share is empty
+  // (the grid is sized from an upper bound of the tiles) return at once
+  int* q = (mode & 2) ? nullptr : pf_queue(s);
+#define DLLM_PFM_GO(MD, DY)                                                                              \
+  hipLaunchKernelGGL((gemm_pf_kernel<MD, 0, DY, true>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)xs, \
+                     (const bf16*)w, (bf16*)y, slots, N, K, q, (const int*)counts, (const int*)offsets, E)
+  switch (mode) {
+    case 0: DLLM_PFM_GO(0, true); break;
+    case 1: DLLM_PFM_GO(2, true); break;
+    case 2: DLLM_PFM_GO(0, false); break;
+    default: DLLM_PFM_GO(2, false); break;
+  }
+#undef DLLM_PFM_GO
   DLLM_HIP_CHECK(hipGetLastError());
 }
 

@@ -127,13 +127,16 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
         slots = t * top_k
         act = torch.empty(slots, inter, dtype=x.dtype, device=dev)
         if knobs.K.moe_persistent and e_loc <= 16 and h >= 128 and inter >= 128:
-            # persistent form (gemm_pf MOE: dynamic tile queue, LDS-DMA ring continuous across tiles):
+            # persistent form (gemm_pf MOE: LDS-DMA ring continuous across tiles; tile queue per knobs.pf_dynamic):
             # the token rows gathered into slot order first (the embedding kernel is a row gather)
             from . import embedding
+            from .gemm import pf_dynamic
+            walk = 0 if pf_dynamic() else 2     # mode bit 1: the static tile walk (knobs.pf_dynamic)
             xs = embedding(sorted_tok, x)
-            k.gemm_pf_moe(act.data_ptr(), xs.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p, e_loc, two_i, h, slots, 1,
+            k.gemm_pf_moe(act.data_ptr(), xs.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p, e_loc, two_i, h, slots,
+                          1 | walk, st)
+            k.gemm_pf_moe(ys.data_ptr(), act.data_ptr(), w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, slots, walk,
                           st)
-            k.gemm_pf_moe(ys.data_ptr(), act.data_ptr(), w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, slots, 0, st)
         else:
             k.gemm_pp_moe(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p,
                           e_loc, two_i, h, t, slots, 1, st)

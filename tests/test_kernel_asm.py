@@ -42,14 +42,16 @@ def test_pf_persistent_kernel_keeps_the_pipeline_full(pp_asm):
         assert scratch == 0, (name, scratch)
         assert "scratch_" not in body
         lines = body.split("\n")
+        # template <MODE, SCH, DYN, MOE> mangles as ILi<MODE>ELi<SCH>ELb<DYN>ELb<MOE>E
+        m = re.search(r"gemm_pf_kernelILi\d+ELi\d+ELb(\d)ELb(\d)E", name)
+        dyn = bool(m and m.group(1) == "1")
         # vmcnt(0) is allowed once (the final drain) -- and, in the dynamic-tile-queue form (template
-        # flag DYN, "Lb1E" in the mangled name), on the queue's own blocking paths (start, steal,
-        # retire: right behind its atomic or relaxed sc1 head load, lane 0 only), never in the
-        # K loop's pipeline itself
+        # flag DYN), on the queue's own blocking paths (start, steal, retire: right behind its atomic
+        # or relaxed sc1 head load, lane 0 only), never in the K loop's pipeline itself
         drains = [i for i, l in enumerate(lines) if "s_waitcnt vmcnt(0)" in l
-                  and not ("Lb1E" in name and any("global_atomic_add" in p or " sc1" in p
-                                                  for p in lines[max(0, i - 4): i]))]
+                  and not (dyn and any("global_atomic_add" in p or " sc1" in p
+                                       for p in lines[max(0, i - 4): i]))]
         assert len(drains) <= 1, (name, [lines[i - 2: i + 1] for i in drains])
-        if "Lb1E" in name:                 # the K loop's fetch is the asynchronous inline-asm one
+        if dyn:                            # the K loop's fetch is the asynchronous inline-asm one
             assert "global_atomic_add" in body and "off sc0" in body
         assert body.count("v_mfma_f32_16x16x32_bf16") >= 128
