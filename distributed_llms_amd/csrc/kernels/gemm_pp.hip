@@ -1270,7 +1270,7 @@ void gemm_pf_moe(uintptr_t y, uintptr_t xs, uintptr_t w, uintptr_t counts, uintp
   DLLM_HOST_CHECK(mode >= 0 && mode <= 3, "mode: bit 0 SwiGLU, bit 1 static tile walk");
   DLLM_HOST_CHECK(slots >= 1, "slots");
   DLLM_HOST_CHECK((long)slots * K * 2 < (1L << 32) && (long)E * N * K * 2 < (1L << 32) &&
-                      (long)slots * (mode == 1 ? N / 2 : N) * 2 < (1L << 31),
+                      (long)slots * ((mode & 1) ? N / 2 : N) * 2 < (1L << 31),
                   "operands must be < 4 GiB, the output < 2 GiB");
   int dev = 0;
   DLLM_HIP_CHECK(hipGetDevice(&dev));
