@@ -704,7 +704,7 @@ void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintpt
   DLLM_HOST_CHECK(E >= 1 && E <= 256, "1 <= experts <= 256");
   DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
-  DLLM_HOST_CHECK(mode >= 0 && mode <= 3, "mode: bit 0 SwiGLU, bit 1 static tile walk");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
   DLLM_HOST_CHECK(xrows >= 1 && slots >= 1, "rows");
   DLLM_HOST_CHECK((long)xrows * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32), "operands must be < 4 GiB");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -1187,7 +1187,7 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   DLLM_HOST_CHECK(M >= 1, "M >= 1");
   DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
-  DLLM_HOST_CHECK(mode >= 0 && mode <= 3, "mode: bit 0 SwiGLU, bit 1 static tile walk");
+  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
   // the output's byte range must stay below 2^31: rows past M are dropped by giving their stores
   // the offset 0x80000000, which has to lie outside the buffer's range
   DLLM_HOST_CHECK((long)M * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32) &&
