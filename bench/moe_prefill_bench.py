@@ -8,6 +8,8 @@ Candidates per projection (gate|up with the SwiGLU fused, then down), us per cal
               through the slot -> token list inside the kernel
   pf_moe      gemm_pf MOE form, static tile walk (rows pre-gathered into slot order)
   pf_moe_dyn  the same with the per-XCD dynamic tile queue
+  pf_moe_g32 / _g16   static walk with 32 / 16 row tiles per group of the tile order (8 default):
+              a group spanning an expert's whole segment reads its weight once
   dense_pf    gemm_pf on ONE expert's weight over all slots: the same FLOPs, no expert segments
 """
 import argparse
@@ -67,8 +69,10 @@ def main():
     def dn_dense():
         gemm.linear_pf(act, wd[0])
 
-    cands = {"gate_up": {"pp_moe": gu_pp, "pf_moe": gu_pf(2), "pf_moe_dyn": gu_pf(0), "dense_pf": gu_dense},
-             "down": {"pp_moe": dn_pp, "pf_moe": dn_pf(2), "pf_moe_dyn": dn_pf(0), "dense_pf": dn_dense}}
+    cands = {"gate_up": {"pp_moe": gu_pp, "pf_moe": gu_pf(2), "pf_moe_dyn": gu_pf(0), "pf_moe_g32": gu_pf(2 | 4),
+                         "pf_moe_g16": gu_pf(2 | 8), "dense_pf": gu_dense},
+             "down": {"pp_moe": dn_pp, "pf_moe": dn_pf(2), "pf_moe_dyn": dn_pf(0), "pf_moe_g32": dn_pf(2 | 4),
+                      "pf_moe_g16": dn_pf(2 | 8), "dense_pf": dn_dense}}
     flops = {"gate_up": 2.0 * slots * 2 * I * H, "down": 2.0 * slots * H * I}
     for proj, fns in cands.items():
         res = {n: [] for n in fns}

@@ -810,6 +810,7 @@ constexpr PfSched pf_sched(int sch) {
        : sch == 4 ? PfSched{40, 96, 0, 8} : sch == 5 ? PfSched{40, 88, 4, 8} : sch == 6 ? PfSched{40, 88, 0, 4}
        : sch == 7 ? PfSched{40, 88, 0, 16} : sch == 9 ? PfSched{40, 88, 0, 8, 20, 6, 6}
        : sch == 10 ? PfSched{40, 88, 0, 8, 20, 5, 6} : sch == 11 ? PfSched{40, 96, 0, 8, 22, 6, 7}
+       : sch == 12 ? PfSched{40, 88, 0, 32}   // MOE: a row group spans a whole expert segment (T = 32K)
        : PfSched{40, 88, 0, 8};
 }
 
@@ -1267,7 +1268,7 @@ void gemm_pf_moe(uintptr_t y, uintptr_t xs, uintptr_t w, uintptr_t counts, uintp
   DLLM_HOST_CHECK(E >= 1 && E <= 16, "1 <= experts <= 16");
   DLLM_HOST_CHECK(K % PBK == 0 && K >= 2 * PBK, "K must be a multiple of 64, >= 128");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
-  DLLM_HOST_CHECK(mode >= 0 && mode <= 3, "mode: bit 0 SwiGLU, bit 1 static tile walk");
+  DLLM_HOST_CHECK(mode >= 0 && mode <= 15, "mode: bit 0 SwiGLU, bit 1 static tile walk, bits 2-3 row group 32 / 16");
   DLLM_HOST_CHECK(slots >= 1, "slots");
   DLLM_HOST_CHECK((long)slots * K * 2 < (1L << 32) && (long)E * N * K * 2 < (1L << 32) &&
                       (long)slots * ((mode & 1) ? N / 2 : N) * 2 < (1L << 31),
@@ -1283,15 +1284,25 @@ void gemm_pf_moe(uintptr_t y, uintptr_t xs, uintptr_t w, uintptr_t counts, uintp
   // static walk (mode bit 1): w + i P over the tile space; the workgroups whose share is empty
   // (the grid is sized from an upper bound of the tiles) return at once
   int* q = (mode & 2) ? nullptr : pf_queue(s);
-#define DLLM_PFM_GO(MD, DY)                                                                              \
-  hipLaunchKernelGGL((gemm_pf_kernel<MD, 0, DY, true>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)xs, \
+#define DLLM_PFM_GO(MD, SC, DY)                                                                          \
+  hipLaunchKernelGGL((gemm_pf_kernel<MD, SC, DY, true>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)xs, \
                      (const bf16*)w, (bf16*)y, slots, N, K, q, (const int*)counts, (const int*)offsets, E)
-  switch (mode) {
-    case 0: DLLM_PFM_GO(0, true); break;
-    case 1: DLLM_PFM_GO(2, true); break;
-    case 2: DLLM_PFM_GO(0, false); break;
-    default: DLLM_PFM_GO(2, false); break;
+#define DLLM_PFM_SCH(SC)                          \
+  switch (mode & 3) {                             \
+    case 0: DLLM_PFM_GO(0, SC, true); break;      \
+    case 1: DLLM_PFM_GO(2, SC, true); break;      \
+    case 2: DLLM_PFM_GO(0, SC, false); break;     \
+    default: DLLM_PFM_GO(2, SC, false); break;    \
   }
+  // row tiles per group of the tile order: 8 (schedule 0), 32 (12) or 16 (7)
+  if (mode & 4) {
+    DLLM_PFM_SCH(12)
+  } else if (mode & 8) {
+    DLLM_PFM_SCH(7)
+  } else {
+    DLLM_PFM_SCH(0)
+  }
+#undef DLLM_PFM_SCH
 #undef DLLM_PFM_GO
   DLLM_HIP_CHECK(hipGetLastError());
 }
