@@ -96,8 +96,10 @@ class Knobs:
     # parallel/rccl_transport.comm_stream, profiles/round5_comm_queues.md)
     comm_queue: str = "pool"
     # device RCCL stand-in (parallel/rccl_standin.py, rehearsal only): LDS each channel workgroup
-    # holds (40 KiB keeps a 128 / 144 KiB GEMM workgroup off its CU: the worst case) and channels
-    standin_lds_kib: int = 40
+    # holds -- 20 KiB like RCCL's own p2p kernel (rcclGenericKernel on gfx950: 19,744 B of LDS,
+    # 261-280 VGPRs, 256 threads; profiles/round5_comm_queues.md), which keeps a 144 KiB gemm_wide
+    # workgroup off its CU -- and channels
+    standin_lds_kib: int = 20
     standin_channels: int = 4
     # ---- MoE (ops/moe.py)
     moe_variant: int = 0

@@ -68,12 +68,11 @@ _warned = False
 
 # device inbox geometry: SLOTS chunks of CHUNK bytes in flight per edge, knobs.standin_channels
 # workgroups per send / recv kernel (each moves a 1/channels piece of every chunk; RCCL's p2p
-# channels), each holding knobs.standin_lds_kib of LDS (default 40 KiB: a co-resident 128 KiB
-# gemm_pf / 144 KiB gemm_wide workgroup cannot share its CU -- the worst case)
+# channels), each holding knobs.standin_lds_kib of LDS (default 20 KiB, RCCL's own p2p kernel's
+# 19,744 B on gfx950: a co-resident 144 KiB gemm_wide workgroup cannot share its CU)
 CHUNK = 1 << 20
 SLOTS = 4
 CHANNELS = 4
-LDS_BYTES = 40 << 10
 
 
 def enabled() -> bool:
