@@ -227,6 +227,20 @@ class DistTransport(Transport):
         self.first = self.ranks[0]
         self.last = self.ranks[-1]
         self._pending = []
+        # GPU stages on the RCCL group: its p2p kernels spin on CUs like the native transport's, so
+        # gemm_wide's split-K grids leave them room (ops/gemm.reserve_cus_for_comm)
+        self._reserved_cus = (device is not None and torch.device(device).type == "cuda" and data_group is None
+                              and dist.is_initialized() and dist.get_backend() == "nccl")
+        if self._reserved_cus:
+            from ..ops import gemm
+            from .rccl_transport import COMM_CUS
+            gemm.reserve_cus_for_comm(COMM_CUS)
+
+    def close(self):
+        if getattr(self, "_reserved_cus", False):
+            from ..ops import gemm
+            gemm.release_cus_for_comm()
+            self._reserved_cus = False
 
     def _reap(self):
         # keep isend handles (and their buffers) alive until the transfer completed

@@ -113,10 +113,7 @@ class RcclTransport(DistTransport):
         if window < 1:
             raise ValueError("in-flight window must be >= 1")
         self.device = dev
-        self._reserved = not self.host and not loopback
-        if self._reserved:
-            from ..ops import gemm
-            gemm.reserve_cus_for_comm(COMM_CUS)
+        self._reserved = False
         self.timeout_s = float(timeout_s)
         self.slots = window + 1
         self.slot_elems = int(max_rows) * int(hidden)
@@ -184,6 +181,12 @@ class RcclTransport(DistTransport):
         self._ids_tx_n = self._ids_rx_n = 0
         self._ids_deferred = []
         self._ids_unposted = collections.deque()   # PendingIds whose receive is not enqueued yet
+        # last: every communicator is built (an init failure above leaves no reservation behind --
+        # the job then falls back to torch.distributed, whose kernels this reservation is not for)
+        if not self.host and not loopback:
+            from ..ops import gemm
+            gemm.reserve_cus_for_comm(COMM_CUS)
+            self._reserved = True
         self._copy_stream = None
 
     # streams / events of this stage's device (no-op shims on a CPU stage)
