@@ -95,6 +95,9 @@ class Knobs:
     # high-priority kernel starves the compute queues -- pp2 73 % of IPC, pp4 stalled;
     # parallel/rccl_transport.comm_stream, profiles/round5_comm_queues.md)
     comm_queue: str = "pool"
+    # CUs a GPU pipeline stage's spinning comm kernels may hold at once (receive + send + ids ring):
+    # gemm_wide's split-K grids leave them free (ops/gemm.reserve_cus_for_comm)
+    comm_reserved_cus: int = 16
     # device RCCL stand-in (parallel/rccl_standin.py, rehearsal only): LDS each channel workgroup
     # holds -- 20 KiB like RCCL's own p2p kernel (rcclGenericKernel on gfx950: 19,744 B of LDS,
     # 261-280 VGPRs, 256 threads; profiles/round5_comm_queues.md), which keeps a 144 KiB gemm_wide

@@ -233,8 +233,8 @@ class DistTransport(Transport):
                               and dist.is_initialized() and dist.get_backend() == "nccl")
         if self._reserved_cus:
             from ..ops import gemm
-            from .rccl_transport import COMM_CUS
-            gemm.reserve_cus_for_comm(COMM_CUS)
+            from .rccl_transport import comm_cus
+            gemm.reserve_cus_for_comm(comm_cus())
 
     def close(self):
         if getattr(self, "_reserved_cus", False):

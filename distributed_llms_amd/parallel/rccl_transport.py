@@ -89,8 +89,15 @@ def comm_stream(device, role: str = "comm"):
 
 
 # CUs a stage's spinning comm kernels may hold at once (receive + send + ids ring, a few channel
-# workgroups each): gemm_wide's split-K grids leave them free (ops/gemm.reserve_cus_for_comm)
+# workgroups each): gemm_wide's split-K grids leave them free (ops/gemm.reserve_cus_for_comm);
+# knobs.comm_reserved_cus overrides it
 COMM_CUS = 16
+
+
+def comm_cus() -> int:
+    """knobs.comm_reserved_cus (default COMM_CUS; 0: no reservation)."""
+    from .. import knobs
+    return max(0, int(knobs.K.comm_reserved_cus))
 
 
 class RcclTransport(DistTransport):
@@ -185,7 +192,7 @@ class RcclTransport(DistTransport):
         # the job then falls back to torch.distributed, whose kernels this reservation is not for)
         if not self.host and not loopback:
             from ..ops import gemm
-            gemm.reserve_cus_for_comm(COMM_CUS)
+            gemm.reserve_cus_for_comm(comm_cus())
             self._reserved = True
         self._copy_stream = None
 
