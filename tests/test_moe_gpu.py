@@ -241,3 +241,40 @@ def test_moe_fp8_prefill_grouped_no_host_sync(cuda):
     tw, tid = ref.moe_route(ref.linear(x, wr).float(), k)
     expect = quant.moe_mlp_ref(x, wgu, wd, tw, tid)
     torch.testing.assert_close(out.float(), expect.float(), atol=3e-2 * expect.abs().max().item(), rtol=5e-2)
+
+
+@pytest.mark.parametrize("swiglu", [True, False])
+def test_pf_moe_tile_walks_bit_exact(cuda, swiglu):
+    """gemm_pf MOE form: the dynamic tile queue, the static walk and the 16 / 32-row-tile group
+    orders (mode bits 1-3) only change which workgroup computes a tile and when -- each tile's K
+    order is the same, so the outputs are bit-identical; ragged expert segments and an empty expert
+    included; and they match the fp32 grouped product."""
+    from distributed_llms_amd import _ext
+    k = _ext.kernels()
+    torch.manual_seed(7)
+    e, h, n = 8, 512, 1024 if swiglu else 768
+    counts_l = [700, 0, 256, 1301, 33, 512, 900, 250]
+    slots = sum(counts_l)
+    counts = torch.tensor(counts_l, dtype=torch.int32, device="cuda")
+    offsets = torch.tensor([sum(counts_l[:x]) for x in range(e)], dtype=torch.int32, device="cuda")
+    xs = _bf(slots, h)
+    w = _bf(e, n, h, scale=0.05)
+    outw = n // 2 if swiglu else n
+    st = torch.cuda.current_stream().cuda_stream
+    outs = {}
+    for walk in (0, 2, 2 | 4, 2 | 8, 4, 8):
+        y = torch.full((slots, outw), float("nan"), device="cuda", dtype=torch.bfloat16)
+        k.gemm_pf_moe(y.data_ptr(), xs.data_ptr(), w.data_ptr(), counts.data_ptr(), offsets.data_ptr(), e, n, h,
+                      slots, (1 if swiglu else 0) | walk, st)
+        outs[walk] = y
+    torch.cuda.synchronize()
+    ref = outs[0]
+    for walk, y in outs.items():
+        assert torch.equal(y, ref), walk
+    exp = torch.empty(slots, outw, device="cuda")
+    for x_ in range(e):
+        a, c = offsets[x_].item(), counts_l[x_]
+        if c:
+            gu = xs[a:a + c].float() @ w[x_].float().t()
+            exp[a:a + c] = torch.nn.functional.silu(gu[:, : n // 2]) * gu[:, n // 2:] if swiglu else gu
+    torch.testing.assert_close(ref.float(), exp, atol=2e-2 * exp.abs().max().item(), rtol=2e-2)
