@@ -28,7 +28,7 @@ def test_loopback_pipeline_gpu(cuda, stages):
     assert drv.num_steps > 0
 
 
-def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fine="0"):
+def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fine="0", small_budget=False):
     import os
     # token-for-token checks run the half-layer plans they were written against: every cut rounds
     # the residual stream to bf16 once more than the fused split-K add + norm of the single engine
@@ -45,7 +45,7 @@ def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fi
     from distributed_llms_amd.parallel.dist_engine import RankRole, init_distributed
     ctx = init_distributed(pp=world)
     assert ctx.device == "cuda:0" and ctx.host_staged
-    role = RankRole(ctx, _mp_ecfg(world))
+    role = RankRole(ctx, _mp_ecfg(world, small_budget))
     if transport == "ipc":
         from distributed_llms_amd.parallel.ipc_transport import IpcTransport
         assert isinstance(role.transport, IpcTransport)
@@ -65,9 +65,12 @@ def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fi
     dist.destroy_process_group()
 
 
-def _mp_ecfg(world):
+def _mp_ecfg(world, small_budget=False):
+    # small_budget: 8 prompt tokens per step -- the prompts are admitted over many steps, most of
+    # them MIXED (decode rows + a prompt chunk), and chunked across steps
+    extra = dict(max_prefill_tokens=8, mixed_prefill_tokens=8) if small_budget else {}
     return EngineConfig(model="tiny-llama-d128", dtype="bfloat16", device="cuda", max_batch=4, max_seq_len=256,
-                        num_kv_blocks=128, graph_batch_sizes=(1, 2, 4), num_workers=world, seed=3)
+                        num_kv_blocks=128, graph_batch_sizes=(1, 2, 4), num_workers=world, seed=3, **extra)
 
 
 @pytest.mark.slow
@@ -81,7 +84,7 @@ def test_multiprocess_gpu_pipeline_host_staged(cuda, world):
     assert res[0] == [ref]
 
 
-def _run_ranks(world, prompts, transport, rounds, fine="0"):
+def _run_ranks(world, prompts, transport, rounds, fine="0", small_budget=False):
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -91,7 +94,7 @@ def _run_ranks(world, prompts, transport, rounds, fine="0"):
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     # daemonic: a rank stuck in a stream wait dies with the test process instead of outliving it
-    procs = [ctxm.Process(target=_gpu_rank_main, args=(r, world, port, prompts, q, transport, rounds, fine),
+    procs = [ctxm.Process(target=_gpu_rank_main, args=(r, world, port, prompts, q, transport, rounds, fine, small_budget),
                             daemon=True)
              for r in range(world)]
     for p in procs:
@@ -192,3 +195,16 @@ def test_sub_layer_stage_chain_gpu(cuda):
         err = (x.float() - ref).abs().max().item()
         assert err < 0.08 * ref.abs().max().item() + 0.05, err
         sch.complete(step, ref.argmax(-1).to(torch.int32).cpu().numpy(), 0.0)
+
+
+@pytest.mark.parametrize("transport", ["rccl-standin", "ipc"])
+def test_multiprocess_gpu_pipeline_mixed_steps(cuda, transport):
+    """Mixed prefill + decode steps through a 2-stage GPU pipeline (the follower splits decode /
+    prefill attention from the wire header's decode-row count; the stand-in's ids ring posts its
+    receives lazily): with an 8-token step budget the prompts are admitted in chunks riding along
+    with decode rows, and the tokens equal the single engine's under the same budget."""
+    prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
+    ref = LLMEngine(_mp_ecfg(1, small_budget=True)).generate(prompts, SamplingParams(max_new_tokens=12,
+                                                                                    ignore_eos=True))
+    res = _run_ranks(2, prompts, transport, rounds=1, small_budget=True)
+    assert res[0][0] == ref
