@@ -204,7 +204,8 @@ def test_multiprocess_gpu_pipeline_mixed_steps(cuda, transport):
     receives lazily): with an 8-token step budget the prompts are admitted in chunks riding along
     with decode rows, and the tokens equal the single engine's under the same budget."""
     prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
-    ref = LLMEngine(_mp_ecfg(1, small_budget=True)).generate(prompts, SamplingParams(max_new_tokens=12,
-                                                                                    ignore_eos=True))
+    eng = LLMEngine(_mp_ecfg(1, small_budget=True))
+    ref = eng.generate(prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
+    assert eng.scheduler.num_mixed > 0          # the budget does force mixed steps (same scheduler)
     res = _run_ranks(2, prompts, transport, rounds=1, small_budget=True)
     assert res[0][0] == ref
