@@ -189,3 +189,21 @@ def test_medium_m_dispatch_follows_the_measured_table():
     assert gemm._use_wide(384, 4096, 14336, x, w)      # down
     x, w = _xw(512, 4096, 14336)
     assert not gemm._use_wide(512, 4096, 14336, x, w)
+
+
+def test_lm_head_leaves_gemm_pp_while_comm_cus_are_reserved():
+    from distributed_llms_amd.ops import gemm
+    x, w = _xw(256, 128256, 4096)
+    assert gemm._use_pp(256, 128256, 4096, x, w, 1)
+    calls = []
+    orig_pp, orig_wide = gemm.linear_pp, gemm.linear_wide
+    gemm.linear_pp = lambda *a, **k: calls.append("pp")
+    gemm.linear_wide = lambda *a, **k: calls.append("wide")
+    try:
+        gemm.linear(x, w)
+        gemm.reserve_cus_for_comm(16)
+        gemm.linear(x, w)
+    finally:
+        gemm.release_cus_for_comm()
+        gemm.linear_pp, gemm.linear_wide = orig_pp, orig_wide
+    assert calls == ["pp", "wide"]
