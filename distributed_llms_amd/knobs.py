@@ -75,6 +75,9 @@ class Knobs:
     # decode LM head (N > 65536) at pp_head_min_m <= M <= 256 on gemm_pp schedule 2 with nontemporal
     # weights: 230 vs 265 us for gemm_sq at M = 256 (Llama-3-8B); 0 = off
     pp_head_min_m: int = 225
+    # the LM head while comm kernels may hold CUs (a GPU pipeline stage with RCCL): "sq" (gemm_sq,
+    # unaffected by a spinning receive) or "pp" (the nontemporal gemm_pp, faster alone)
+    head_beside_comm: str = "sq"
     # ---- attention (ops/__init__.py)
     attn_target_waves: int = 1024     # decode split-KV: waves to aim for (profiles/attn_decode_sweep.txt)
     prefill_attn: int = 4             # prefill kernel version 1..5 (4: LDS-shared K/V tiles)

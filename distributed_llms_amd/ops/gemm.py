@@ -122,8 +122,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     # unless comm kernels may hold CUs: beside a 4-workgroup, 20 KiB-LDS receive spinning in
     # another process it took 284 us, gemm_sq 268 either way (bench/debug/lm_head_bench.py,
     # profiles/round5_raw/r5ae_head.txt) -- the pipeline's last stage holds the head
-    if bias is None and n > 65536 and 0 < kn.pp_head_min_m <= m <= 256 and not _comm_cus \
-            and _use_pp(m, n, k, x, w, 1):
+    if bias is None and n > 65536 and 0 < kn.pp_head_min_m <= m <= 256 \
+            and (not _comm_cus or kn.head_beside_comm == "pp") and _use_pp(m, n, k, x, w, 1):
         return linear_pp(x, w, splits=1, variant=PP_HEAD_VARIANT)           # decode LM head
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
