@@ -60,6 +60,71 @@ class _HostEvent:
 _COMM_STREAMS = {}
 
 
+def shares_queue(spin_stream, others, wait_s: float = 0.05) -> list:
+    """Indices of the streams in ``others`` that share ``spin_stream``'s hardware queue: a receive
+    that is never matched (the device stand-in's kernel: one workgroup, no LDS, released through its
+    host-mapped abort word, 2 s deadline) spins on ``spin_stream`` while one small kernel goes on
+    each other stream; those not finished after ``wait_s`` sit behind the spinner.  A few ms."""
+    import ctypes
+    import time
+    k = _ext.kernels()
+    chunk, nslots = 4096, 2
+    dev = spin_stream.device
+    words = k.p2p_host_words(2)
+    try:
+        wv = (ctypes.c_int * 2).from_address(words)
+        inbox = torch.zeros(k.p2p_inbox_bytes(chunk, nslots), dtype=torch.uint8, device=dev)
+        dst = torch.empty(256, dtype=torch.uint8, device=dev)
+        bufs = [torch.zeros(64, device=dev) for _ in others]
+        torch.cuda.synchronize(dev)
+        k.p2p_standin(0, 0, 0, 0, dst.data_ptr(), inbox.data_ptr(), dst.numel(), 0, chunk, nslots, 1, words, 2.0,
+                      words + 4, 0, spin_stream.cuda_stream)
+        evs = []
+        for b, o in zip(bufs, others):
+            with torch.cuda.stream(o):
+                b.add_(1)
+                e = torch.cuda.Event()
+                e.record(o)
+            evs.append(e)
+        t_end = time.monotonic() + wait_s
+        while time.monotonic() < t_end and not all(e.query() for e in evs):
+            time.sleep(0.001)
+        blocked = [i for i, e in enumerate(evs) if not e.query()]
+        wv[0] = 1                                  # release the spinner
+        spin_stream.synchronize()
+        for e in evs:
+            e.synchronize()
+        return blocked
+    finally:
+        torch.cuda.synchronize(dev)
+        k.p2p_host_words_free(words)
+
+
+def isolated_pool_streams(device, n: int, compute=None, tries: int = 12) -> list:
+    """``n`` torch pool streams on hardware queues shared with neither ``compute`` (default: the
+    current stream) nor each other, picked by probing (:func:`shares_queue`).  HIP deals a
+    process's streams over GPU_MAX_HW_QUEUES queues in creation order, so which pool stream lands
+    where depends on every stream created before -- a receive or a send spinning in the compute
+    stream's queue would stall the stage (profiles/round5_comm_queues.md).  Falls back to the next
+    pool streams, unprobed, when no kernel module or not enough free queues are available."""
+    dev = torch.device(device)
+    compute = compute or torch.cuda.current_stream(dev)
+    chosen = []
+    try:
+        _ext.kernels()
+    except Exception:                    # noqa: BLE001 - no native kernels: unprobed pool streams
+        return [torch.cuda.Stream(device=dev) for _ in range(n)]
+    for _ in range(n):
+        pick = None
+        for _ in range(tries):
+            s = torch.cuda.Stream(device=dev)
+            if not shares_queue(s, [compute] + chosen):
+                pick = s
+                break
+        chosen.append(pick if pick is not None else torch.cuda.Stream(device=dev))
+    return chosen
+
+
 def comm_stream(device, role: str = "comm"):
     """The stream of one communication role ("send", "recv", "ring", "copy").
 
@@ -68,14 +133,12 @@ def comm_stream(device, role: str = "comm"):
     stream-wait on an event holds up every later kernel of every stream sharing that queue.
     Measured on MI355X (scripts/hwq_probe.py, profiles/round5_comm_queues.md):
       * torch pool streams (default, ``knobs.comm_queue = "pool"``): a spinner blocks the pool
-        streams dealt to its queue; pp4 over the device stand-in keeps 97 % of the IPC rehearsal;
+        streams dealt to its queue -- RcclTransport picks its role streams by probing
+        (:func:`isolated_pool_streams`), this function hands out an unprobed one;
       * high-priority streams (``"priority"``: one native stream per role, created once, never
         destroyed) each get a queue of their own -- but a spinning high-priority kernel starves
         normal-priority work: pp2 kept 73 % of IPC, and pp4 stalled until the spinners' deadlines;
-      * CU-masked streams all share ONE queue with the default stream (not offered).
-    So the roles use pool streams; the pipeline's ordering never needs a send to pass a posted
-    receive in one queue (activations flow downstream only, and stage 0 posts a slot's ids receive
-    after that slot's forward)."""
+      * CU-masked streams all share ONE queue with the default stream (not offered)."""
     from .. import knobs
     dev = torch.device(device)
     if knobs.K.comm_queue != "priority":
@@ -163,8 +226,13 @@ class RcclTransport(DistTransport):
                 self.ring_out = self.m.RcclComm(2, 0, mine["ring"], di, self.timeout_s)
             elif first and not last:
                 self.ring_in = self.m.RcclComm(2, 1, table[self.last]["ring"], di, self.timeout_s)
-        self.send_stream = self._stream("send") if self.comm_out is not None else None
-        self.recv_stream = self._stream("recv") if self.comm_in is not None else None
+        # comm role streams on hardware queues of their own (probed; knobs.comm_queue)
+        roles = [r for r, c in (("send", self.comm_out), ("recv", self.comm_in)) if c is not None]
+        if (self.ring_out or self.ring_in) and (loopback or self.host or self.ring_out):
+            roles.append("ring")
+        picked = self._role_streams(roles)
+        self.send_stream = picked.get("send")
+        self.recv_stream = picked.get("recv")
         if loopback:
             self.recv_stream = self.send_stream
         self.tx = torch.empty(self.slots, self.slot_elems, dtype=dtype, device=dev) if self.comm_out else None
@@ -180,7 +248,7 @@ class RcclTransport(DistTransport):
         self.id_slots = 2 * window + 2
         # ring stream: the last stage's ids sends only (stage 0 posts each ids receive lazily on
         # its compute stream, in front of the consumer: PendingIds(post=...))
-        self.ring_stream = self._stream("ring") if (self.ring_out or (self.ring_in and (loopback or self.host))) else None
+        self.ring_stream = picked.get("ring")
         self.ids_tx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_out else None
         self.ids_rx = torch.empty(self.id_slots, self.max_ids, dtype=torch.int32, device=dev) if self.ring_in else None
         self._ids_sent = [None] * self.id_slots
@@ -199,6 +267,12 @@ class RcclTransport(DistTransport):
     # streams / events of this stage's device (no-op shims on a CPU stage)
     def _stream(self, role):
         return _HostStream() if self.host else comm_stream(self.device, role)
+
+    def _role_streams(self, roles) -> dict:
+        from .. import knobs
+        if self.host or knobs.K.comm_queue == "priority" or not roles:
+            return {r: self._stream(r) for r in roles}
+        return dict(zip(roles, isolated_pool_streams(self.device, len(roles))))
 
     def _event(self):
         return _HostEvent() if self.host else torch.cuda.Event()

@@ -403,3 +403,21 @@ def test_wide_gemm_grids_leave_comm_cus_free(cuda):
           f"256-workgroup grid: solo {solo256 * 1e3:.1f} us, beside {beside256 * 1e3:.1f} us")
     assert beside <= 1.15 * solo, (solo, beside)
     assert torch.isfinite(y).all() and ref.shape == (256, 4096)
+
+
+def test_isolated_pool_streams_share_no_queue(cuda):
+    """RcclTransport's role streams (parallel/rccl_transport.isolated_pool_streams): picked by
+    probing so that a receive spinning in any of them blocks neither the compute stream nor another
+    role's stream -- whichever pool streams were created before (here: a burst of other pool
+    streams first, so the pool index is arbitrary)."""
+    from distributed_llms_amd.parallel.rccl_transport import isolated_pool_streams, shares_queue
+    junk = [torch.cuda.Stream() for _ in range(5)]          # shift the pool's round robin
+    roles = isolated_pool_streams("cuda", 3)
+    cur = torch.cuda.current_stream()
+    for i, s in enumerate(roles):
+        others = [cur] + [r for j, r in enumerate(roles) if j != i]
+        assert shares_queue(s, others) == [], i
+    # the probe itself sees a sharing pair: some pool stream shares the spinner's queue
+    pool = [torch.cuda.Stream() for _ in range(8)]
+    assert shares_queue(pool[0], pool[1:]) != [] or shares_queue(pool[1], pool[2:] + [pool[0]]) != []
+    del junk
