@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
-from distributed_llms_amd import ops
+from distributed_llms_amd import knobs, ops
 from distributed_llms_amd.ops import reference as ref
 
 
@@ -59,6 +59,15 @@ def main():
         us = timeit(f, a.iters)
         moved = qkv.numel() * 2 + t * hq * d * 2 + 2 * t * hkv * d * 2
         rows.append(f"{name:8s} {us:8.2f} us  {moved / us / 1e6:6.2f} TB/s (bytes moved {moved / 1e6:.2f} MB)")
+    # the engine's prefill form: K / V only (the attention kernel rotates q), V per token vs grouped
+    for grouped in (False, True):
+        with knobs.override(v_group_append=grouped):
+            f = lambda: ops.rope_cache_append(qkv, pos_pf, cs, kc, vc, slots_pf, hq, hkv, d, write_q=False)  # noqa: E731
+            f()
+            us = timeit(f, a.iters)
+        moved = 2 * t * hkv * d * 2 * 2      # read k, v; write k, v
+        rows.append(f"prefill kv-only {'grouped V' if grouped else 'per-token V'}: {us:8.2f} us  "
+                    f"{moved / us / 1e6:6.2f} TB/s (k/v bytes {moved / 1e6:.2f} MB)")
     print(f"tokens={t} hq={hq} hkv={hkv} d={d}")
     print("\n".join(rows))
 

@@ -17,7 +17,7 @@ void embedding(uintptr_t out, uintptr_t ids, uintptr_t table, int tokens, int hi
                uintptr_t stream);
 void rope_cache_append(uintptr_t q_out, uintptr_t qkv, uintptr_t positions, uintptr_t cos_sin,
                        uintptr_t k_cache, uintptr_t v_cache, uintptr_t slots, int tokens, int hq, int hkv,
-                       int d, int bs, uintptr_t stream);
+                       int d, int bs, int v_groups, uintptr_t stream);
 void silu_mul(uintptr_t out, uintptr_t gu, int tokens, int inter, uintptr_t stream);
 void add_inplace(uintptr_t a, uintptr_t b, long n, uintptr_t stream);
 void argmax(uintptr_t out, uintptr_t logits, int rows, int vocab, long row_stride, uintptr_t stream);

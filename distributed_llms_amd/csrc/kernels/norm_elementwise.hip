@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ q_ou
                                                          const float* __restrict__ cos_sin,
                                                          bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
                                                          const int32_t* __restrict__ slots, int hq, int hkv,
-                                                         int d, int bs) {
+                                                         int d, int bs, int do_v) {
   const int t = blockIdx.x;
   const int half = d >> 1;
   const int qpr = half >> 2;  // threads per head (4 pairs each)
@@ -168,6 +168,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ q_ou
     *reinterpret_cast<bf16x4*>(dst + p) = o1;
     *reinterpret_cast<bf16x4*>(dst + half + p) = o2;
   }
+  if (!do_v) return;  // v_group_kernel appends V
   // v: transposed store into [blk][h][d][bs]
   const bf16* vsrc = row + (hq + hkv) * d;
   for (int i = threadIdx.x; i < hkv * d; i += blockDim.x) {
@@ -176,15 +177,61 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ q_ou
   }
 }
 
+// V append for a prefill batch, eight tokens per workgroup.  The transposed layouts keep a key's
+// 8-aligned group of 8 contiguous per (head, e) -- vofs(off0 + j) = vofs(off0) + j when
+// off0 % 8 == 0 and bs % 8 == 0 -- so when the group's slots are consecutive and 8-aligned (a
+// prompt's tokens: consecutive slots from a block start) a thread writes one 16-byte vector where
+// the per-token path scatters eight 2-byte stores (whole 64-byte lines instead of partial ones).
+// Loads: for a fixed token j, a wave's 64 consecutive e read 128 contiguous bytes.  Any other group
+// (a prompt boundary inside it, a sequence resuming mid-group, the batch tail) takes the per-token
+// scatter.
+__global__ void __launch_bounds__(256) v_group_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ v_cache,
+                                                      const int32_t* __restrict__ slots, int tokens, int hq,
+                                                      int hkv, int d, int bs) {
+  __shared__ int sl[8];
+  const int t0 = blockIdx.x * 8;
+  const int n = min(8, tokens - t0);
+  if (threadIdx.x < 8) sl[threadIdx.x] = threadIdx.x < n ? slots[t0 + threadIdx.x] : -1;
+  __syncthreads();
+  const int width = (hq + 2 * hkv) * d;
+  const bf16* vsrc = qkv + (size_t)t0 * width + (hq + hkv) * d;
+  bool full = n == 8 && sl[0] >= 0 && sl[0] % 8 == 0;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) full = full && sl[j] == sl[0] + j;
+  if (full) {
+    const int blk = sl[0] / bs, off0 = sl[0] % bs;
+    for (int i = threadIdx.x; i < hkv * d; i += blockDim.x) {
+      const int h = i / d, e = i % d;
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = vsrc[(size_t)j * width + i];
+      *reinterpret_cast<bf16x8*>(v_cache + ((size_t)blk * hkv + h) * d * bs + vofs(off0, e, d, bs)) = o;
+    }
+    return;
+  }
+  for (int j = 0; j < n; ++j) {
+    const int blk = sl[j] / bs, off = sl[j] % bs;
+    for (int i = threadIdx.x; i < hkv * d; i += blockDim.x) {
+      const int h = i / d, e = i % d;
+      v_cache[((size_t)blk * hkv + h) * d * bs + vofs(off, e, d, bs)] = vsrc[(size_t)j * width + i];
+    }
+  }
+}
+
 void rope_cache_append(uintptr_t q_out, uintptr_t qkv, uintptr_t positions, uintptr_t cos_sin,
                        uintptr_t k_cache, uintptr_t v_cache, uintptr_t slots, int tokens, int hq, int hkv,
-                       int d, int bs, uintptr_t stream) {
+                       int d, int bs, int v_groups, uintptr_t stream) {
   DLLM_HOST_CHECK(d % 8 == 0 && d <= 256, "head_dim must be a multiple of 8, <= 256");
   DLLM_HOST_CHECK(hq % hkv == 0, "Hq % Hkv");
   if (tokens == 0) return;
+  const bool grouped = v_groups && bs % 8 == 0 && tokens >= 8;
   hipLaunchKernelGGL(rope_cache_kernel, dim3(tokens), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      (bf16*)q_out, (const bf16*)qkv, (const int32_t*)positions, (const float*)cos_sin,
-                     (bf16*)k_cache, (bf16*)v_cache, (const int32_t*)slots, hq, hkv, d, bs);
+                     (bf16*)k_cache, (bf16*)v_cache, (const int32_t*)slots, hq, hkv, d, bs, grouped ? 0 : 1);
+  DLLM_HIP_CHECK(hipGetLastError());
+  if (!grouped) return;
+  hipLaunchKernelGGL(v_group_kernel, dim3((tokens + 7) / 8), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const bf16*)qkv, (bf16*)v_cache, (const int32_t*)slots, tokens, hq, hkv, d, bs);
   DLLM_HIP_CHECK(hipGetLastError());
 }
 

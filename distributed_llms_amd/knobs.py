@@ -115,6 +115,9 @@ class Knobs:
     # measured slower in-engine (Mixtral B = 256: TTFT 742 vs 689 ms, 10,070 vs 10,272 tok/s; gate|up
     # 13.3 ms per layer vs gemm_pp_moe's 11.6, gpurun_out/r5d_mixtral*.txt)
     moe_persistent: bool = False
+    # prefill V append eight tokens per workgroup, 16-byte stores into the transposed V cache
+    # (norm_elementwise.hip v_group_kernel); False = the per-token 2-byte scatter.
+    v_group_append: bool = True
     # grouped expert GEMM ring depth: 6 / 5 LDS slots at 64 / 128-row tiles (False: 3 slots)
     moe_deep_ring: bool = True
     # ---- FP8 W8A8 (ops/quant.py)

@@ -207,7 +207,7 @@ def rope_cache_append(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, n
     _ext.kernels().rope_cache_append(q.data_ptr() if write_q else 0, qkv.data_ptr(), positions.data_ptr(),
                                      0 if cos_sin is None else cos_sin.data_ptr(), k_cache.data_ptr(),
                                      v_cache.data_ptr(), slot_mapping.data_ptr(), t, num_heads, num_kv_heads,
-                                     head_dim, k_cache.shape[2], _stream())
+                                     head_dim, k_cache.shape[2], int(knobs.K.v_group_append), _stream())
     return q
 
 

@@ -78,6 +78,29 @@ def test_rope_cache_append(cuda, hq, hkv, d):
     torch.testing.assert_close(v1, v2, atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("grouped", [True, False])
+def test_rope_cache_append_prefill_groups(cuda, grouped):
+    """Prefill slot patterns for the grouped V append: aligned whole groups (16-byte stores),
+    prompts starting / ending mid-group, a sequence resuming mid-block, non-consecutive slots, a
+    ragged tail -- all bit-identical to the reference scatter."""
+    from distributed_llms_amd import knobs
+    hq, hkv, d, nb = 32, 8, 128, 24
+    runs = [(0, 45), (3 * 32, 32), (5 * 32 + 5, 19), (7 * 32 + 8, 3), (9 * 32, 64)]
+    sl = [s + i for s, n in runs for i in range(n)] + [20 * 32 + 31, 21 * 32 + 2, 22 * 32 + 9]
+    t = len(sl)
+    slots = torch.tensor(sl, dtype=torch.int32, device="cuda")
+    qkv = _bf(t, (hq + 2 * hkv) * d)
+    pos = torch.arange(t, device="cuda", dtype=torch.int32)
+    cs = ref.rope_cos_sin(d, 1024, 500000.0, device="cuda")
+    k1, v1 = _cache(nb, hkv, d)
+    k2, v2 = _cache(nb, hkv, d)
+    with knobs.override(v_group_append=grouped):
+        assert ops.rope_cache_append(qkv, pos, cs, k1, v1, slots, hq, hkv, d, write_q=False) is None
+    ref.rope_cache_append(qkv.float(), pos, cs, k2, v2, slots, hq, hkv, d)
+    torch.testing.assert_close(k1.float(), k2.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(v1, v2, atol=0, rtol=0)
+
+
 def _fill_paged(seq_lens, hkv, d, nb_total=None):
     bs = 32
     nblocks = [(n + bs - 1) // bs for n in seq_lens]
