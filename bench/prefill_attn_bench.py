@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
-from distributed_llms_amd import ops
+from distributed_llms_amd import knobs, ops
+from distributed_llms_amd.ops import reference as ref
 
 
 def main():
@@ -24,6 +25,8 @@ def main():
     ap.add_argument("--shapes", nargs="+", default=["256x128", "32x1024", "8x4096", "1x8192"],
                     help="BATCHxPROMPT_LEN")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rope", action="store_true",
+                    help="the engine's form: q read from the raw qkv projection and rotated in the kernel")
     a = ap.parse_args()
     hq, hkv, d, bs = 32, 8, 128, 32
     print(f"{'shape':>10s} " + " ".join(f"{'v' + v + ' us':>10s} {'TF':>5s}" for v in a.versions))
@@ -36,10 +39,19 @@ def main():
         cu = torch.arange(0, (b + 1) * L, L, dtype=torch.int32, device="cuda")
         sl = torch.full((b,), L, dtype=torch.int32, device="cuda")
         q = torch.randn(b * L, hq, d, device="cuda").to(torch.bfloat16)
+        qkv = torch.randn(b * L, (hq + 2 * hkv) * d, device="cuda").to(torch.bfloat16)
+        pos = torch.arange(L, dtype=torch.int32, device="cuda").repeat(b)
+        cs = ref.rope_cos_sin(d, L, 500000.0, device="cuda")
         flops = 4.0 * b * hq * d * L * (L + 1) / 2
         row = []
         for ver in a.versions:
-            f = lambda: ops.paged_attention_prefill(q, k, v, bt, cu, sl, d ** -0.5, version=int(ver))
+            if a.rope:
+                knobs.update({"prefill_attn": int(ver)})
+            if a.rope:
+                f = lambda: ops.paged_attention_prefill_rope(qkv, pos, cs, k, v, bt, cu, sl, hq, d, d ** -0.5,  # noqa: E731
+                                                             max_q_len=L)
+            else:
+                f = lambda: ops.paged_attention_prefill(q, k, v, bt, cu, sl, d ** -0.5, version=int(ver))  # noqa: E731
             f()
             ts = []
             for _ in range(a.reps):
