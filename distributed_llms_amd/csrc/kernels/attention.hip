@@ -614,11 +614,25 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
   __shared__ __attribute__((aligned(16))) bf16 smem[NB * CH + 2 * kPfMaxChunks];
   int* ids = reinterpret_cast<int*>(smem + NB * CH);
 
-  const int kvh = blockIdx.y, b = blockIdx.z;
+  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs in dispatch order, so the
+  // gridDim.x row tiles of one (sequence, kv head) -- which stream the same K / V chunks -- would
+  // land on gridDim.x different XCDs (each with its own L2).  Renumber so that they share one.
+  int qt = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  {
+    const int nx = gridDim.x, ng = gridDim.y * gridDim.z;
+    const int lin = blockIdx.x + nx * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (ng % 8 == 0) {
+      const int xcd = lin & 7, slot = lin >> 3;            // slot-th workgroup of this XCD
+      const int grp = (slot / nx) * 8 + xcd;
+      qt = slot % nx;
+      kvh = grp % gridDim.y;
+      b = grp / gridDim.y;
+    }
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int qs = cu_seqlens_q[b], ql = cu_seqlens_q[b + 1] - qs;
-  const int wg_row0 = blockIdx.x * WV * R * NT;
+  const int wg_row0 = qt * WV * R * NT;
   if (wg_row0 >= ql) return;                      // workgroup-uniform
   const int row0 = wg_row0 + w * R * NT;
   const bool active = row0 < ql;                  // wave-uniform; inactive waves still stage
