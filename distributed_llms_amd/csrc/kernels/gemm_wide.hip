@@ -451,8 +451,21 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
     const int q = total >> 3, r = total & 7, x = b & 7;
     b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
   }
+  // nsplit < 0: K-slice-major order -- an XCD's contiguous run covers one or two K slices of
+  // many column tiles (its L2 holds those slices of the activations and every line of them is
+  // shared by the run's column tiles) instead of every K slice of a few column tiles
+  const bool kmajor = nsplit < 0;
+  if (kmajor) nsplit = -nsplit;
   int m_t = b % mtiles, rest = b / mtiles;
-  int split = rest % nsplit, n_t = rest / nsplit;
+  int split, n_t;
+  if (kmajor) {
+    const int ng = total / (mtiles * nsplit);
+    n_t = rest % ng;
+    split = rest / ng;
+  } else {
+    split = rest % nsplit;
+    n_t = rest / nsplit;
+  }
   if constexpr ((VAR & 64) != 0) {          // prefill M, no K split (grouped_tile)
     grouped_tile(b, mtiles, ntiles, m_t, n_t);
     split = 0;
@@ -689,6 +702,9 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   const bool swiglu = mode == 1;
   DLLM_HOST_CHECK(swiglu ? (N % 128 == 0) : (N % WBN == 0), "N must be a multiple of 128");
   DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
+  // variant bit 20: K-slice-major workgroup order (gemm_wide_kernel kmajor)
+  const bool kmajor = (variant & (1 << 20)) != 0;
+  variant &= ~(1 << 20);
   // variant bits 8..: optional row tile override (64 / 128 / 192 / 256), 0 = wide_bm(M)
   const int bm_force = variant >> 8;
   variant &= 0xff;
@@ -721,7 +737,7 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   else if (variant == 4) variant = 1;
 #define DLLM_WIDE_GO3(BM_, SPLIT_, SW_, V_)                                                                      \
   hipLaunchKernelGGL((gemm_wide_kernel<BM_, SPLIT_, SW_, 3, V_>), dim3((unsigned)grid), dim3(512), 0, s,          \
-                     (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S)
+                     (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, kmajor && S > 1 ? -S : S)
 #define DLLM_WIDE_GO(BM_, SPLIT_, SW_)                                                                          \
   do {                                                                                                         \
     if (abl == 8) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 10); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 9); } \

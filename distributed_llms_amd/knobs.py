@@ -118,6 +118,8 @@ class Knobs:
     # prefill V append eight tokens per workgroup, 16-byte stores into the transposed V cache
     # (norm_elementwise.hip v_group_kernel); False = the per-token 2-byte scatter.
     v_group_append: bool = True
+    # split-K gemm_wide grids in K-slice-major workgroup order (an XCD's run shares K slices)
+    wide_kmajor: bool = False
     # grouped expert GEMM ring depth: 6 / 5 LDS slots at 64 / 128-row tiles (False: 3 slots)
     moe_deep_ring: bool = True
     # ---- FP8 W8A8 (ops/quant.py)

@@ -247,6 +247,8 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     bm = wide_row_tile(m, n, k, swiglu)
     if bm != wide_bm(m):
         v |= bm << 8
+    if s > 1 and knobs.K.wide_kmajor:
+        v |= 1 << 20
     if defer and not swiglu and s > 1:
         se = _ext.kernels().gemm_wide(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, v, stream)
         return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)

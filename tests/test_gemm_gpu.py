@@ -142,6 +142,26 @@ def test_wide_l2_prefetch_bit_exact(cuda, m, n, k, splits, swiglu):
         assert torch.equal(a, b), v
 
 
+@pytest.mark.parametrize("m,n,k,splits", [(256, 6144, 4096, 5), (256, 4096, 14336, 8), (256, 4096, 4096, 8),
+                                          (300, 4096, 4096, 4), (64, 1024, 512, 3), (1, 2048, 1024, 2)])
+def test_wide_kmajor_order_bit_exact(cuda, m, n, k, splits):
+    """Variant bit 20 (K-slice-major workgroup order on split-K grids) only moves workgroups between
+    XCDs: every (row tile, column tile, K slice) runs the same MFMAs into the same slab, so the
+    reduced and the deferred outputs are bit-identical to the default order."""
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    for v in (1, 33):
+        a = gemm.linear_wide(x, w, splits=splits, variant=v)
+        b = gemm.linear_wide(x, w, splits=splits, variant=v | (1 << 20))
+        assert torch.equal(a, b), v
+    ref = (x.float() @ w.float().t())
+    torch.testing.assert_close(b.float(), ref, atol=5e-2, rtol=5e-2)
+    from distributed_llms_amd import knobs
+    with knobs.override(wide_kmajor=True):
+        pa = gemm.linear_wide(x, w, splits=splits, defer=True)
+        pb = pa.materialize() if hasattr(pa, "materialize") else pa
+    assert torch.equal(pb, gemm.linear_wide(x, w, splits=splits))
+
+
 @pytest.mark.parametrize("m,n,k,swiglu", [(4500, 1024, 512, False), (5000, 2048, 256, True), (2048, 256, 128, False)])
 def test_wide_grouped_tile_order_bit_exact(cuda, m, n, k, swiglu):
     """Variant bit 64 (grouped row-tile order for prefill M) only reorders the workgroups: every
