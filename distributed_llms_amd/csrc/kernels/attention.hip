@@ -65,7 +65,15 @@ __device__ __forceinline__ void load_chunk(KVChunk<D>& c, const bf16* __restrict
 
 // Online-softmax update of the wave's 16 columns with one loaded chunk.
 //   kmax_col : last admissible key index for this lane's column (causal / range), inclusive
-template <int D>
+//   MASK     : false when the caller knows every key of the chunk is admissible for every column
+//              (prefill chunks strictly below the diagonal): no per-score compare / select
+// VALU economy (long prefill is VALU-bound: ~330 VALU per 32 MFMAs, MFMA 25 % busy --
+// profiles/round5_prefill_attn_valu.md): the running max is taken on the raw scores and scaled
+// once (x -> x * scale is monotonic, so the max is the same number), the scale folds into the
+// exponent's FMA, and exp2 is the bare v_exp_f32 (libm's exp2f adds a denormal-range fix-up of
+// four instructions per call; results below 2^-126 of the row max flush to zero), and the
+// accumulator rescale is skipped when no column's max moved.
+template <int D, bool MASK = true>
 __device__ __forceinline__ void compute_chunk(WaveState<D>& st, const bf16x8 (&qf)[D / 32], const KVChunk<D>& c,
                                               int t0, int kmax_col, float scale_log2, int lane) {
   const int g = lane >> 4;
@@ -79,32 +87,43 @@ __device__ __forceinline__ void compute_chunk(WaveState<D>& st, const bf16x8 (&q
   float cm = -INFINITY;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int k0 = t0 + 8 * g + i, k1 = t0 + 8 * g + 4 + i;   // S^T rows 4g+i / 16+4g+i (krow32)
-    p[i] = (k0 <= kmax_col) ? s0[i] * scale_log2 : -INFINITY;
-    p[4 + i] = (k1 <= kmax_col) ? s1[i] * scale_log2 : -INFINITY;
+    if constexpr (MASK) {
+      const int k0 = t0 + 8 * g + i, k1 = t0 + 8 * g + 4 + i;   // S^T rows 4g+i / 16+4g+i (krow32)
+      p[i] = (k0 <= kmax_col) ? s0[i] : -INFINITY;
+      p[4 + i] = (k1 <= kmax_col) ? s1[i] : -INFINITY;
+    } else {
+      p[i] = s0[i];
+      p[4 + i] = s1[i];
+    }
     cm = fmaxf(cm, fmaxf(p[i], p[4 + i]));
   }
   cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
   cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+  cm *= scale_log2;
   // No early exit here: MFMA reads all 64 lanes' operands regardless of EXEC, so every
   // lane must run the same instruction stream. A fully masked column uses mref = 0,
   // which turns its probabilities (and its alpha) into exact zeros.
   const float mn = fmaxf(st.m, cm);
   const float mref = (mn == -INFINITY) ? 0.f : mn;
-  const float alpha = exp2f(st.m - mref);
+  const float alpha = __builtin_amdgcn_exp2f(st.m - mref);
   st.m = mn;
   bf16x8 pb;
   float ps = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float e = exp2f(p[j] - mref);
+    const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(p[j], scale_log2, -mref));
     ps += e;
     pb[j] = f2bf(e);
   }
   st.lsum = st.lsum * alpha + ps;
+  // alpha is exactly 1 wherever the running max did not move (exp2(0)), the common case once a
+  // row's max has settled: skip the accumulator rescale when that holds for the whole wave (bit-exact)
+  if (__any(alpha != 1.f)) {
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) st.acc[dt] *= alpha;
+  }
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt) {
-    st.acc[dt] *= alpha;
     const bf16x8 va = c.v[dt];
     st.acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, st.acc[dt], 0, 0, 0);
   }
@@ -660,6 +679,9 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
   const int wg_kmax = qpos0 + min(wg_row0 + WV * R * NT, ql) - 1;
   const int nch = wg_kmax / kBS + 1;
   const int wave_kmax = active ? qpos0 + min(row0 + R * NT, ql) - 1 : -1;
+  // the smallest admissible key bound over the wave's columns (wave-uniform): -1 when any of its
+  // rows is past the sequence (those columns take the masked path to stay exactly zero)
+  const int wave_kmin = row0 + R * NT <= ql ? qpos0 + row0 : -1;
   const int32_t* bt = block_tables + (size_t)b * max_blocks;
   for (int i = threadIdx.x; i < nch; i += WV * 64) ids[i] = bt[i];
   // retire the q and block-id loads before the first LDS-DMA: their uses inside the loop
@@ -721,7 +743,10 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
     // buffer (c + 2) % NB was read in iteration c - 1, which every wave finished before the
     // barrier above (its fragments were consumed by MFMAs)
     if (c + 2 < nch) stage(c + 2, buf == 0 ? NB - 1 : buf - 1);
-    if (c * kBS <= wave_kmax) {
+    if (c * kBS + kBS - 1 <= wave_kmin) {         // below every column's diagonal: no mask
+#pragma unroll
+      for (int t = 0; t < NT; ++t) compute_chunk<D, false>(st[t], qf[t], kc, c * kBS, kmax_col[t], scale_log2, lane);
+    } else if (c * kBS <= wave_kmax) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) compute_chunk<D>(st[t], qf[t], kc, c * kBS, kmax_col[t], scale_log2, lane);
     }
