@@ -752,23 +752,63 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
     }
     buf = buf == NB - 1 ? 0 : buf + 1;
   }
+  // Output through a wave-private LDS image (the K / V ring is free once every wave is past its
+  // last chunk): a lane holds 4 dims of one column per fragment, so direct stores write 32 bytes
+  // into each of 16 rows per instruction; read back as whole 16-byte pieces of a column, a store
+  // instruction covers 512 / D complete columns -- with G heads of a row contiguous, whole lines.
+  constexpr int OLD = D + 8;                        // padded image row (bf16): 16-B aligned, 2-way banks
+  if constexpr (WV * NT * 16 * OLD > NB * CH) {     // (4 tiles per wave at D = 64: direct stores)
+    if (!active) return;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float lt = st[t].lsum;
+      lt += __shfl_xor(lt, 16, 64);
+      lt += __shfl_xor(lt, 32, 64);
+      const int crow = row0 + t * R + r / G, ch = r % G;
+      if (crow < ql) {
+        const float inv = lt > 0.f ? 1.f / lt : 0.f;
+        bf16* orow = out + ((size_t)(qs + crow) * hq + kvh * G + ch) * D;
+#pragma unroll
+        for (int dt = 0; dt < D / 16; ++dt) {
+          bf16x4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = f2bf(st[t].acc[dt][i] * inv);
+          *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = o;
+        }
+      }
+    }
+    return;
+  }
+  __syncthreads();
   if (!active) return;
+  bf16* img = smem + w * (NT * 16 * OLD);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     float lt = st[t].lsum;
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
-    const int crow = row0 + t * R + r / G, ch = r % G;
-    if (crow < ql) {
-      const float inv = lt > 0.f ? 1.f / lt : 0.f;
-      bf16* orow = out + ((size_t)(qs + crow) * hq + kvh * G + ch) * D;
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
 #pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) {
-        bf16x4 o;
+    for (int dt = 0; dt < D / 16; ++dt) {
+      bf16x4 o;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = f2bf(st[t].acc[dt][i] * inv);
-        *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = o;
-      }
+      for (int i = 0; i < 4; ++i) o[i] = f2bf(st[t].acc[dt][i] * inv);
+      *reinterpret_cast<bf16x4*>(img + (t * 16 + r) * OLD + dt * 16 + 4 * g) = o;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): the wave's own image writes landed
+  __builtin_amdgcn_wave_barrier();
+  constexpr int PPC = D / 8;                        // 16-byte pieces per column
+  constexpr int CPI = 64 / PPC;                     // columns per store instruction
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int j = 0; j < 16 / CPI; ++j) {
+      const int col = j * CPI + lane / PPC, piece = lane % PPC;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + (t * 16 + col) * OLD + piece * 8);
+      const int crow = row0 + t * R + col / G, ch = col % G;
+      if (crow < ql)
+        *reinterpret_cast<bf16x8*>(out + ((size_t)(qs + crow) * hq + kvh * G + ch) * D + piece * 8) = v;
     }
   }
 }
