@@ -660,6 +660,28 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
   bf16x8 qf[NT][D / 32];
   int kmax_col[NT];
   WaveState<D> st[NT];
+  // q through a wave-private LDS image, the mirror of the output path below: loaded as whole
+  // 16-byte pieces of columns (G heads of a row contiguous: whole lines per instruction) where the
+  // fragment layout reads 64 bytes of each of 16 rows; the ring is not in use before the first
+  // stage() (behind the __syncthreads below)
+  constexpr int QLD = D + 8;
+  constexpr bool QIMG = WV * NT * 16 * QLD <= NB * CH;
+  if constexpr (QIMG) {
+    bf16* img = smem + w * (NT * 16 * QLD);
+    constexpr int PPC = D / 8, CPI = 64 / PPC;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int j = 0; j < 16 / CPI; ++j) {
+        const int col = j * CPI + lane / PPC, piece = lane % PPC;
+        const int crow = row0 + t * R + col / G, ch = col % G;
+        const int tok = qs + (crow < ql ? crow : 0);
+        *reinterpret_cast<bf16x8*>(img + (t * 16 + col) * QLD + piece * 8) =
+            *reinterpret_cast<const bf16x8*>(q + (size_t)tok * q_stride + (size_t)(kvh * G + ch) * D + piece * 8);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int crow = row0 + t * R + r / G, ch = r % G;
@@ -667,9 +689,11 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
     kmax_col[t] = ok ? qpos0 + crow : -1;
     const int tok = qs + (ok ? crow : 0);
     const bf16* qrow = q + (size_t)tok * q_stride + (size_t)(kvh * G + ch) * D;
+    const bf16* irow = smem + w * (NT * 16 * QLD) + (t * 16 + r) * QLD;
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
+      bf16x8 v = QIMG ? *reinterpret_cast<const bf16x8*>(irow + ks * 32 + 8 * g)
+                      : *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
       if (!ok) v = bf16x8{};
       qf[t][ks] = v;
     }
