@@ -180,67 +180,6 @@ __device__ __forceinline__ void wide_epilogue(const f32x4 (&acc)[BM / 64][4], bf
   }
 }
 
-// The same epilogue through an LDS image of the workgroup's output tile (the staging ring is free
-// once every wave is past the K loop).  A lane's accumulators hold one column of 4 consecutive rows
-// per fragment, so direct stores write 2 bytes per lane -- 32 bytes into each of 4 rows per
-// instruction, 64 (plain / split) or 32 (SwiGLU) instructions per lane; they cost 13-22 % of the
-// M = 256 decode GEMMs (bench/debug/wide_store_cost.py, profiles/round5_raw/r5av_store_cost.txt).
-// Here a lane writes its 16-bit outputs into the image and the workgroup then stores whole 16-byte
-// pieces of rows (a wave covers 4 rows x 256 bytes: whole lines), 8 (4) instructions per lane.
-// Same values bit for bit (each element is converted exactly as wide_epilogue converts it).
-// Not for a split SwiGLU grid (its columns interleave the gate and up halves).
-template <int BM, bool SPLIT, bool SWIGLU>
-__device__ __forceinline__ void wide_epilogue_img(bf16* smem, const f32x4 (&acc)[BM / 64][4], bf16* __restrict__ C,
-                                                  float* __restrict__ P, int M, int N, int m0, int n_t, int split,
-                                                  int wm, int wn, int lane, int tid) {
-  static_assert(!(SPLIT && SWIGLU), "split SwiGLU grids use wide_epilogue");
-  constexpr int RT = BM / 64;
-  constexpr int W = SWIGLU ? 64 : WBN;              // output columns of the tile
-  constexpr int LD = W + 8;                         // padded image row (16-bit elements)
-  const int fr = lane & 15, fq = lane >> 4;
-  __syncthreads();                                  // every wave is done reading the ring
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ml = wm * (BM / 4) + rt * 16 + 4 * fq + i;
-      uint16_t* row = reinterpret_cast<uint16_t*>(smem) + ml * LD;
-      if constexpr (SWIGLU) {
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const bf16 o = f2bf(silu_f(acc[rt][2 * p][i]) * acc[rt][2 * p + 1][i]);
-          row[(wn * 2 + p) * 16 + fr] = __builtin_bit_cast(uint16_t, o);
-        }
-      } else {
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          const float v = acc[rt][ct][i];
-          uint16_t bits;
-          if constexpr (SPLIT) bits = __builtin_bit_cast(uint16_t, (_Float16)(v * kPartScale));
-          else bits = __builtin_bit_cast(uint16_t, f2bf(v));
-          row[wn * 64 + ct * 16 + fr] = bits;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  constexpr int PR = W / 8;                         // 16-byte pieces per row
-  constexpr int PIECES = BM * PR;
-  static_assert(PIECES % 512 == 0, "pieces per thread");
-#pragma unroll
-  for (int k = 0; k < PIECES / 512; ++k) {
-    const int pidx = tid + k * 512, rl = pidx / PR, pc = pidx % PR;
-    const int m = m0 + rl;
-    if (m >= M) continue;
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + rl * LD + pc * 8);
-    bf16* dst;
-    if constexpr (SWIGLU) dst = C + (size_t)m * (N / 2) + n_t * 64 + pc * 8;
-    else if constexpr (SPLIT) dst = reinterpret_cast<bf16*>(reinterpret_cast<_Float16*>(P) + ((size_t)split * M + m) * N + n_t * WBN + pc * 8);
-    else dst = C + (size_t)m * N + n_t * WBN + pc * 8;
-    *reinterpret_cast<bf16x8*>(dst) = v;
-  }
-}
-
 // The K loop shared by the dense and the grouped (MoE) wide kernels: stages A/B tiles through
 // NBUF LDS buffers (LDS-DMA, counted vmcnt, raw barrier) and accumulates acc = A_tile B_tile^T
 // over `nt` 64-deep K-tiles.  srcA/srcB: this lane's staging source for K-tile 0.
@@ -557,12 +496,6 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
   f32x4 acc[RT][4];
   wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, nt, acc, wv, lane, pfB, smem + NBUF * BUF);
   if ((VAR & 8) && nsplit >= 0) return;
-#if DLLM_PART_TYPE == 2
-  if constexpr (!(SPLIT && SWIGLU) && (VAR & 64) == 0) {
-    wide_epilogue_img<BM, SPLIT, SWIGLU>(smem, acc, C, P, M, N, m0, n_t, split, wm, wn, lane, tid);
-    return;
-  }
-#endif
   wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
 }
 
