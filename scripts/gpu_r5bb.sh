@@ -1,0 +1,15 @@
+#!/bin/bash
+# Prefill attention q / O images with swizzled aligned rows (D = 128): numerics, LDS-conflict
+# counters, kernel A/B against HEAD (_old/).
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_engine_gpu.py tests/test_production_shapes_gpu.py > gpurun_out/r5bb_tests.txt 2>&1 || { tail -30 gpurun_out/r5bb_tests.txt; exit 1; }
+tail -1 gpurun_out/r5bb_tests.txt
+for i in 1 2; do
+  echo "== old"; (cd _old && timeout -k 10 200 python -u bench/prefill_attn_bench.py --rope --versions 4 --shapes 256x128 32x1024 8x4096 --reps 10) || exit 1
+  echo "== new"; timeout -k 10 200 python -u bench/prefill_attn_bench.py --rope --versions 4 --shapes 256x128 32x1024 8x4096 --reps 10 || exit 1
+done 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r5bb_ab.txt
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/bbctr -o run --output-format csv -- python bench/prefill_attn_bench.py --rope --versions 4 --shapes 256x128 --reps 2 > gpurun_out/bbctr.log 2>&1
+echo "ctr rc=$?"
