@@ -75,6 +75,8 @@ class MasterNode:
         self.proto = MessageProtocol()
         self.state = "idle"                       # idle | ready | degraded | failed
         self._recovering = False                  # a recovery thread is running (guarded by _lock)
+        self._recovery_gen = 0                    # bumped per recovery thread: only the newest clears
+        #                                           _recovering or gives up (advisor round 5)
         self.recoveries = 0                       # completed re-plans after a stage loss
         self.recover_timeout = 600.0              # seconds a recovery waits for replacement workers
         self.metrics = RequestMetrics()
@@ -243,7 +245,9 @@ class MasterNode:
                         self.proto.send_message(ww["socket"], "UNLOAD_SHARD", metadata={"pipeline": True})
                 if self.auto_recover:
                     self._recovering = True
-                    threading.Thread(target=self._recover_when_possible, daemon=True).start()
+                    self._recovery_gen += 1
+                    threading.Thread(target=self._recover_when_possible, kwargs={"gen": self._recovery_gen},
+                                     daemon=True).start()
 
     def _fail_all(self, exc: Exception):
         with self._lock:
@@ -468,7 +472,7 @@ class MasterNode:
         log.info("pipeline ready: %s", {w: a.get("layer_range") for w, a in acks.items()})
         return acks
 
-    def _recover_when_possible(self, timeout: Optional[float] = None):
+    def _recover_when_possible(self, timeout: Optional[float] = None, gen: Optional[int] = None):
         """Re-admit a full set of stage workers (waits for replacements), reload the plan, then
         re-run the parked requests from their prompts.  Failed attempts back off exponentially.
 
@@ -477,9 +481,18 @@ class MasterNode:
         parked requests, on give-up together with the state change to "failed" and the swap-out of
         the parked list -- so a concurrent submit() either parks before that swap (and is failed or
         resubmitted with the rest) or sees "failed" / "ready" and never parks into a list that
-        nobody will drain."""
+        nobody will drain.
+
+        ``gen``: this thread's recovery generation.  A stage worker evicted after this thread has
+        re-admitted the pipeline (e.g. while it re-submits the parked requests) starts a newer
+        thread; this one then leaves ``_recovering``, the state and the newly parked requests to
+        that thread instead of declaring the pipeline failed from the state it now sees."""
         t_end = time.time() + (self.recover_timeout if timeout is None else timeout)
         backoff = 0.5
+        if gen is None:
+            with self._lock:
+                gen = self._recovery_gen
+        recovered = False
         try:
             while self.running and time.time() < t_end and self.state == "degraded":
                 with self._lock:
@@ -489,6 +502,7 @@ class MasterNode:
                         self.shard_assignments = {}
                         self.assign_shards()
                         self.distribute_shards()
+                        recovered = True
                         self.recoveries += 1
                         log.info("pipeline recovered onto %s", self.stage_workers)
                         self._resubmit_parked()
@@ -501,8 +515,10 @@ class MasterNode:
                 time.sleep(0.5)
         finally:
             with self._lock:
-                self._recovering = False
-                gave_up = self.state != "ready"
+                newest = gen == self._recovery_gen
+                gave_up = newest and not recovered
+                if newest:
+                    self._recovering = False
                 if gave_up:
                     self.state = "failed"
             if gave_up:

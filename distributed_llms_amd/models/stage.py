@@ -315,7 +315,8 @@ class ModelStage:
                                                 cfg.head_dim, self.scale, max_ctx=meta.max_ctx or None,
                                                 workspace=meta.attn_workspace)
             return o.view(o.shape[0], self.q_size_local)
-        if meta.is_prefill and not meta.num_decode and qkv.is_cuda and ops.prefill_rope_in_attention():
+        if meta.is_prefill and not meta.num_decode and qkv.is_cuda and \
+                ops.prefill_rope_in_attention(meta.block_tables.shape[1]):
             ops.rope_cache_append(qkv, meta.positions, self.cos_sin, k_cache, v_cache, meta.slot_mapping,
                                   self.hq, self.hkv, cfg.head_dim, write_q=False)
             o = ops.paged_attention_prefill_rope(qkv, meta.positions, self.cos_sin, k_cache, v_cache,

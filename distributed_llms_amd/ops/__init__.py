@@ -373,8 +373,16 @@ def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq
     return out
 
 
-def prefill_rope_in_attention() -> bool:
-    """Prefill q-RoPE inside the attention kernel (knobs.prefill_fused_rope; LDS kernel versions)."""
+PF_MAX_CHUNKS = 1024    # attention.hip kPfMaxChunks: the LDS prefill kernel stages <= 32k tokens of block ids
+
+
+def prefill_rope_in_attention(max_blocks: Optional[int] = None) -> bool:
+    """Prefill q-RoPE inside the attention kernel (knobs.prefill_fused_rope; LDS kernel versions).
+    ``max_blocks``: the batch's block-table width -- beyond ``PF_MAX_CHUNKS`` (32k-token sequences)
+    the launcher falls back to the register-tiled kernel, which reads a rotated q, so the caller
+    must take ``rope_cache_append(write_q=True)`` + the plain prefill kernel instead."""
+    if max_blocks is not None and max_blocks > PF_MAX_CHUNKS:
+        return False
     return knobs.K.prefill_fused_rope and knobs.K.prefill_attn in (4, 5)
 
 
@@ -401,8 +409,9 @@ def paged_attention_prefill_rope(qkv, positions, cos_sin, k_cache, v_cache, bloc
         raise ValueError("qkv width mismatch")
     if cos_sin is not None:
         _ck(cos_sin, "cos_sin", torch.float32)
-    if not prefill_rope_in_attention():
-        raise ValueError("in-kernel prefill RoPE needs the LDS prefill kernel (knobs.prefill_attn 4 / 5)")
+    if not prefill_rope_in_attention(block_tables.shape[1]):
+        raise ValueError("in-kernel prefill RoPE needs the LDS prefill kernel (knobs.prefill_attn 4 / 5) and "
+                         f"block tables of <= {PF_MAX_CHUNKS} blocks")
     b = seq_lens.shape[0]
     if max_q_len is None:
         max_q_len = int((cu_seqlens_q[1:] - cu_seqlens_q[:-1]).max().item()) if b else 0

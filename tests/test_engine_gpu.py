@@ -146,3 +146,26 @@ def test_mixed_prefill_decode_steps_gpu(cuda):
     assert n0 == 0 and n1 > 0
     assert all(len(o) == 12 for o in out)
     assert sum(a == b for a, b in zip(out, ref)) >= 11, (out, ref)
+
+
+def test_prefill_with_block_table_wider_than_lds_kernel(cuda):
+    """A prefill whose block table is wider than the LDS prefill kernel stages (> 1024 blocks, i.e.
+    sequences past 32k tokens) must not take the in-kernel q-RoPE path: the launcher falls back to
+    the register-tiled kernel, which reads a rotated q.  The stage then appends with write_q=True
+    and runs the plain prefill kernel -- same logits as the narrow table, within the kernels' bf16
+    difference."""
+    from distributed_llms_amd import knobs, ops
+    assert not ops.prefill_rope_in_attention(ops.PF_MAX_CHUNKS + 1)
+    _, e_gpu = _engines("tiny-llama-d128", graphs=False)
+    prompts = [[1, 5, 9, 200, 37, 44, 45, 46, 47, 48], list(range(10, 80))]
+    for p in prompts:
+        e_gpu.add_request(p, SamplingParams(max_new_tokens=1))
+    st = e_gpu.scheduler.schedule(0)
+    outs = []
+    with knobs.override(prefill_attn=4, prefill_fused_rope=True):
+        for width in (None, ops.PF_MAX_CHUNKS + 76):
+            hb = build_host_batch(st, e_gpu.bm, 32, max_blocks=width)
+            if width is not None:
+                assert hb.block_tables.shape[1] == width
+            outs.append(e_gpu.runner.execute(hb).float().cpu())
+    torch.testing.assert_close(outs[1], outs[0], atol=3e-2, rtol=3e-2)

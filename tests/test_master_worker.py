@@ -231,6 +231,66 @@ def test_recovery_timeout_fails_parked_and_later_requests():
         m.stop(shutdown_workers=False)
 
 
+def test_eviction_during_resubmit_leaves_the_newer_recovery_in_charge():
+    """Advisor round 5: a stage worker evicted while a recovery thread re-submits the parked requests
+    starts a second recovery.  The first thread, finishing, must neither clear ``_recovering`` nor
+    declare the pipeline failed (which would fail the newly parked requests): the newer thread
+    recovers and re-submits them."""
+    import concurrent.futures as cf
+    from distributed_llms_amd.master.node import MasterNode
+    m = MasterNode("127.0.0.1", 0, auto_recover=True).start()
+    try:
+        m.num_shards = 1
+        m.workers["w9"] = {"socket": None, "last_heartbeat": time.time()}   # a registered spare
+        sent = []
+        m.assign_shards = lambda: None
+        m._send_request = lambda ids, params, fut, stream, hint, attempts: (sent.append(ids), fut.set_result(ids))
+        calls = {"n": 0}
+
+        def distribute_shards(*a, **k):
+            calls["n"] += 1
+            m.state = "ready"
+
+        m.distribute_shards = distribute_shards
+        orig_resubmit = m._resubmit_parked
+        late = cf.Future()
+
+        def resubmit_with_eviction():
+            orig_resubmit()
+            if calls["n"] == 1:            # what _evict does when a re-admitted stage worker dies now
+                with m._lock:
+                    m.state = "degraded"
+                    m._recovering = True
+                    m._recovery_gen += 1
+                    m._retry.append({"ids": [7, 8], "params": {}, "attempts": 0, "hint": None,
+                                     "future": late, "stream": None})
+
+        m._resubmit_parked = resubmit_with_eviction
+        first = cf.Future()
+        with m._lock:
+            m.state = "degraded"
+            m._recovering = True
+            m._recovery_gen += 1
+            m._retry.append({"ids": [1, 2], "params": {}, "attempts": 0, "hint": None, "future": first,
+                             "stream": None})
+        th1 = threading.Thread(target=m._recover_when_possible, kwargs={"timeout": 5.0, "gen": m._recovery_gen},
+                               daemon=True)
+        th1.start()
+        th1.join(10)
+        assert not th1.is_alive() and first.result(timeout=1) == [1, 2]
+        # the older thread left the newer recovery's state alone
+        assert m.state == "degraded" and m._recovering and not late.done()
+        th2 = threading.Thread(target=m._recover_when_possible, kwargs={"timeout": 5.0, "gen": m._recovery_gen},
+                               daemon=True)
+        th2.start()
+        th2.join(10)
+        assert m.state == "ready" and not m._recovering
+        assert late.result(timeout=1) == [7, 8] and sent == [[1, 2], [7, 8]]
+    finally:
+        m.workers.pop("w9", None)
+        m.stop(shutdown_workers=False)
+
+
 def test_degraded_without_recovery_thread_does_not_park():
     from distributed_llms_amd.master.node import MasterNode, WorkerFailure
     m = MasterNode("127.0.0.1", 0, auto_recover=True).start()

@@ -207,3 +207,15 @@ def test_lm_head_leaves_gemm_pp_while_comm_cus_are_reserved():
         gemm.release_cus_for_comm()
         gemm.linear_pp, gemm.linear_wide = orig_pp, orig_wide
     assert calls == ["pp", "wide"]
+
+
+def test_prefill_rope_in_attention_gated_on_block_table_width():
+    """Advisor round 5: block tables wider than the LDS prefill kernel stages (sequences past 32k
+    tokens) must take the write_q=True append + plain prefill kernel, not the in-kernel q-RoPE."""
+    from distributed_llms_amd import knobs, ops
+    with knobs.override(prefill_attn=4, prefill_fused_rope=True):
+        assert ops.prefill_rope_in_attention()
+        assert ops.prefill_rope_in_attention(ops.PF_MAX_CHUNKS)
+        assert not ops.prefill_rope_in_attention(ops.PF_MAX_CHUNKS + 1)
+    with knobs.override(prefill_attn=3, prefill_fused_rope=True):
+        assert not ops.prefill_rope_in_attention(16)
