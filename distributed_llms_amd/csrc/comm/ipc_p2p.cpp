@@ -104,6 +104,16 @@ uintptr_t priority_stream(int device) {
   return reinterpret_cast<uintptr_t>(st);
 }
 
+// A non-blocking stream at normal priority, owned by the caller (not torch's stream pool, which hands
+// its 32 streams out round-robin: a pool stream probed onto a queue of its own could later be handed
+// to another user and put that user's work behind a spinning receive).
+uintptr_t plain_stream(int device) {
+  ipc_check(hipSetDevice(device), "hipSetDevice");
+  hipStream_t st = nullptr;
+  ipc_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+  return reinterpret_cast<uintptr_t>(st);
+}
+
 void stream_destroy(uintptr_t st) { ipc_check(hipStreamDestroy(reinterpret_cast<hipStream_t>(st)), "hipStreamDestroy"); }
 
 bool can_wait_value(int device) {
@@ -127,5 +137,7 @@ void register_ipc(py::module_& m) {
         "a HIP stream on a hardware queue of its own (CU mask; empty = all CUs)");
   m.def("priority_stream", &priority_stream, py::arg("device"),
         "a non-blocking stream at the greatest priority (a hardware queue of its own, up to the queue limit)");
+  m.def("plain_stream", &plain_stream, py::arg("device"),
+        "a non-blocking normal-priority stream owned by the caller (outside torch's stream pool)");
   m.def("stream_destroy", &stream_destroy, py::arg("stream"));
 }

@@ -23,6 +23,7 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("splitk_add_rms_norm", &dllm::splitk_add_rms_norm);
   m.def("splitk_reduce", &dllm::splitk_reduce);
   m.def("gemm_wide", &dllm::gemm_wide);
+  m.def("gemm_wide_sk", &dllm::gemm_wide_sk);
   m.def("gemm_wide_fp8", &dllm::gemm_wide_fp8);
   m.def("quant_fp8_rows", &dllm::quant_fp8_rows);
   m.def("rms_norm_q8", &dllm::rms_norm_q8);

@@ -29,6 +29,8 @@ void splitk_reduce_ex(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M,
                       uintptr_t stream);
 int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
               int mode, int variant, uintptr_t stream);
+int gemm_wide_sk(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t part, long part_floats, uintptr_t sk, long sk_words,
+                 int M, int N, int K, int mode, int P, int test, uintptr_t stream);
 int gemm_wide_fp8(uintptr_t c, uintptr_t a, uintptr_t a_scale, uintptr_t b, uintptr_t b_scale, uintptr_t ws,
                   long ws_floats, int M, int N, int K, int splits, int mode, int variant, uintptr_t stream);
 void quant_fp8_rows(uintptr_t q, uintptr_t scale, uintptr_t x, int M, int K, uintptr_t stream);

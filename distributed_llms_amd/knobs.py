@@ -122,6 +122,12 @@ class Knobs:
     wide_kmajor: bool = False
     # grouped expert GEMM ring depth: 6 / 5 LDS slots at 64 / 128-row tiles (False: 3 slots)
     moe_deep_ring: bool = True
+    # unsplit gemm_wide grids with fewer column tiles than CUs (the 8B gate|up: 224 tiles on 256 CUs)
+    # run stream-K: every CU takes an equal share of tiles x K-tiles, partial tiles handed over in the
+    # launch (gemm_wide.hip gemm_wide_sk_kernel; profiles/round6_streamk.md).  wide_streamk_max_fill:
+    # only while tiles / CUs is below this (a nearly full grid has nothing to gain)
+    wide_streamk: bool = False
+    wide_streamk_max_fill: float = 0.94
     # ---- FP8 W8A8 (ops/quant.py)
     fp8_bm128: bool = True
     fp8_group_m: int = 4096

@@ -131,7 +131,10 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
             # the token rows gathered into slot order first (the embedding kernel is a row gather)
             from . import embedding
             from .gemm import pf_dynamic
-            walk = 0 if pf_dynamic() else 2     # mode bit 1: the static tile walk (knobs.pf_dynamic)
+            # mode bit 1: the static tile walk (knobs.pf_dynamic off, and always inside a graph
+            # capture -- as linear_pf: a tile queue is per stream, and a replay may run beside eager
+            # launches that use the same queue; pf_queue() also refuses to create one mid-capture)
+            walk = 0 if (pf_dynamic() and not torch.cuda.is_current_stream_capturing()) else 2
             xs = embedding(sorted_tok, x)
             k.gemm_pf_moe(act.data_ptr(), xs.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p, e_loc, two_i, h, slots,
                           1 | walk, st)

@@ -100,28 +100,51 @@ def shares_queue(spin_stream, others, wait_s: float = 0.05) -> list:
         k.p2p_host_words_free(words)
 
 
+_HELD_STREAMS = []         # native streams made by isolated_pool_streams (probe candidates too): never freed
+
+
+def _native_stream(dev):
+    """A normal-priority stream outside torch's pool (torch's 32 pool streams are dealt out
+    round-robin, so a probed pool stream could later be handed to another user -- a graph capture
+    stream, a ``torch.cuda.Stream()`` -- whose work would then queue behind a spinning receive).
+    Held for the life of the process; None without the native comm module."""
+    try:
+        h = _ext.rccl_native().plain_stream(dev.index or 0)
+    except Exception:                    # noqa: BLE001 - older module / no RCCL: pool stream
+        return None
+    st = torch.cuda.ExternalStream(h, device=dev)
+    _HELD_STREAMS.append(st)
+    return st
+
+
 def isolated_pool_streams(device, n: int, compute=None, tries: int = 12) -> list:
-    """``n`` torch pool streams on hardware queues shared with neither ``compute`` (default: the
-    current stream) nor each other, picked by probing (:func:`shares_queue`).  HIP deals a
-    process's streams over GPU_MAX_HW_QUEUES queues in creation order, so which pool stream lands
-    where depends on every stream created before -- a receive or a send spinning in the compute
-    stream's queue would stall the stage (profiles/round5_comm_queues.md).  Falls back to the next
-    pool streams, unprobed, when no kernel module or not enough free queues are available."""
+    """``n`` streams on hardware queues shared with neither ``compute`` (default: the current
+    stream) nor each other, picked by probing (:func:`shares_queue`).  HIP deals a process's
+    streams over GPU_MAX_HW_QUEUES queues in creation order, so which stream lands where depends
+    on every stream created before -- a receive or a send spinning in the compute stream's queue
+    would stall the stage (profiles/round5_comm_queues.md).  The candidates are native streams
+    owned here (:func:`_native_stream`; torch pool streams only without the native module), so
+    a chosen stream is never handed to anyone else.  Falls back to unprobed streams when no kernel
+    module or not enough free queues are available."""
     dev = torch.device(device)
     compute = compute or torch.cuda.current_stream(dev)
+
+    def make():
+        return _native_stream(dev) or torch.cuda.Stream(device=dev)
+
     chosen = []
     try:
         _ext.kernels()
-    except Exception:                    # noqa: BLE001 - no native kernels: unprobed pool streams
-        return [torch.cuda.Stream(device=dev) for _ in range(n)]
+    except Exception:                    # noqa: BLE001 - no native kernels: unprobed streams
+        return [make() for _ in range(n)]
     for _ in range(n):
         pick = None
         for _ in range(tries):
-            s = torch.cuda.Stream(device=dev)
+            s = make()
             if not shares_queue(s, [compute] + chosen):
                 pick = s
                 break
-        chosen.append(pick if pick is not None else torch.cuda.Stream(device=dev))
+        chosen.append(pick if pick is not None else make())
     return chosen
 
 
@@ -230,7 +253,10 @@ class RcclTransport(DistTransport):
         roles = [r for r, c in (("send", self.comm_out), ("recv", self.comm_in)) if c is not None]
         if (self.ring_out or self.ring_in) and (loopback or self.host or self.ring_out):
             roles.append("ring")
+        if self.ring_in is not None and not self.host:
+            roles.append("copy")                  # the sampled ids' copy-out (PendingIds), probed too
         picked = self._role_streams(roles)
+        self._copy_stream = picked.get("copy")
         self.send_stream = picked.get("send")
         self.recv_stream = picked.get("recv")
         if loopback:
@@ -262,7 +288,6 @@ class RcclTransport(DistTransport):
             from ..ops import gemm
             gemm.reserve_cus_for_comm(comm_cus())
             self._reserved = True
-        self._copy_stream = None
 
     # streams / events of this stage's device (no-op shims on a CPU stage)
     def _stream(self, role):

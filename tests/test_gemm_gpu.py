@@ -427,3 +427,63 @@ def test_pf_split_release_schedules_bit_exact(cuda, sched):
     with knobs.override(pf_schedule=sched):
         assert torch.equal(gemm.linear_pf(x, w), ref)
         assert torch.equal(gemm.linear_pf(xs, ws, swiglu=True), ref_s)
+
+
+# ---- stream-K gemm_wide (knobs.wide_streamk; csrc/kernels/gemm_wide.hip gemm_wide_sk_kernel)
+@pytest.mark.parametrize("m", [1, 37, 64, 128, 200, 256])
+@pytest.mark.parametrize("n,k,swiglu,grid", [(28672, 4096, True, 256), (28672, 4096, True, 240),
+                                             (2048, 1024, True, 20), (4096, 2048, False, 37),
+                                             (3072, 512, False, 29)])
+def test_streamk_wide_matches_fp32(cuda, m, n, k, swiglu, grid):
+    """Every CU takes an equal share of tiles x K-tiles; tiles split between workgroups are
+    finished by the workgroup holding their end, which adds the others' published partials.  Grids
+    that put one, two or three segments in a tile, every row tile (64 / 128 / 192 / 256), SwiGLU
+    and plain."""
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    y = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)
+    r = x.float() @ w.float().t()
+    if swiglu:
+        r = F.silu(r[:, : n // 2]) * r[:, n // 2:]
+    torch.testing.assert_close(y.float(), r, atol=3e-2, rtol=3e-2)
+    assert int(gemm._sk_block(x.device)[2]) == 0, "a stream-K poll hit its deadline"
+
+
+@pytest.mark.parametrize("m,n,k,swiglu,grid", [(256, 28672, 4096, True, 256), (128, 28672, 4096, True, 250),
+                                               (64, 4096, 2048, False, 37), (200, 3072, 512, False, 29)])
+def test_streamk_steal_and_replay_bit_exact(cuda, m, n, k, swiglu, grid):
+    """Deterministic whoever computes a segment: odd workgroups leaving their partial to the
+    finisher (which then computes it itself) give bit-identical outputs; so do repeated calls (the
+    epoch advances each time, no memset) and a HIP-graph replay."""
+    x, w = _bf(m, k), _bf(n, k, scale=0.05)
+    sk = gemm._sk_block(x.device)
+    e0 = int(sk[0])
+    a = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)
+    b = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid, test=1)
+    c = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(a, c)
+    assert int(sk[0]) == e0 + 3 and int(sk[1]) == 0 and int(sk[2]) == 0
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)      # warm the capture stream's blocks
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, a)
+
+
+def test_streamk_dispatch_for_the_8b_gate_up(cuda):
+    """With knobs.wide_streamk the M <= 256 8B gate|up (224 column tiles) runs stream-K over every CU
+    through the default dispatch, and agrees with the unsplit kernel to bf16 rounding."""
+    from distributed_llms_amd import knobs
+    x, w = _bf(256, 4096), _bf(28672, 4096, scale=0.05)
+    base = gemm.linear_wide(x, w, swiglu=True)
+    with knobs.override(wide_streamk=True):
+        assert gemm.streamk_grid(256, 28672, 4096, True, x.device) == torch.cuda.get_device_properties(0).multi_processor_count
+        y = gemm.linear_swiglu(x, w)
+    torch.testing.assert_close(y.float(), base.float(), atol=2e-2, rtol=2e-2)
