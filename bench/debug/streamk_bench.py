@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, nargs="+", default=[64, 128, 256])
     ap.add_argument("--shapes", nargs="+", default=["gate_up_8b"])
-    ap.add_argument("--grids", type=int, nargs="+", default=[256, 240])
+    ap.add_argument("--grids", type=int, nargs="+", default=[256, 240, 224])
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--calls", type=int, default=8)
     a = ap.parse_args()
@@ -36,6 +36,7 @@ def main():
             fns = {"wide": lambda w: gemm.linear_wide(x, w, splits=1, swiglu=sw)}
             for g in a.grids:
                 fns[f"sk{g}"] = lambda w, g=g: gemm.linear_wide_sk(x, w, swiglu=sw, grid=g)
+            fns["sk256_nopart"] = lambda w: gemm.linear_wide_sk(x, w, swiglu=sw, grid=256, test=2)
             res = {key: [] for key in fns}
             for fn in fns.values():
                 fn(ws[0])
@@ -49,8 +50,9 @@ def main():
                     e1.record()
                     e1.synchronize()
                     res[key].append(e0.elapsed_time(e1) * 1e3 / a.calls)
-            print(f"{name} M={m:4d}  " + "  ".join(f"{key} {statistics.median(v):6.1f}" for key, v in res.items()),
-                  flush=True)
+            sk = gemm._sk_block(x.device).cpu()
+            print(f"{name} M={m:4d}  " + "  ".join(f"{key} {statistics.median(v):6.1f}" for key, v in res.items())
+                  + f"   steals {int(sk[3])}", flush=True)
             assert int(gemm._sk_block(x.device)[2]) == 0
         del ws
 

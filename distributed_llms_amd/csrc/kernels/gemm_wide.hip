@@ -524,7 +524,8 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
 //  * flag = epoch << 2 | state (1 claimed, 2 published, 3 stolen); the epoch lives in ctl[0] on the
 //    device and the last workgroup to retire advances it, so there is no per-call memset and a graph
 //    replay sees a fresh epoch every time.  One control block per stream (ops/gemm.py).
-// test & 1 (tests only): odd workgroups skip their publishing segment, so finishers steal it.
+// test & 1 (tests only): odd workgroups skip their publishing segment, so finishers steal it;
+// test & 2 (timing ablation, wrong results): no partial stores / loads, flags only.
 template <int BM, bool SWIGLU, int NBUF, int VAR>
 __global__ void __launch_bounds__(512, 1) gemm_wide_sk_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                               bf16* __restrict__ C, float* __restrict__ part,
@@ -548,7 +549,9 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_sk_kernel(const bf16* __rest
   const int mtiles = (M + BM - 1) / BM;
   const int ntiles = SWIGLU ? (N / 2) / 64 : N / WBN;
   const long U = (long)mtiles * ntiles * KT;
-  unsigned* ctl = sk;            // [0] epoch, [1] retired workgroups, [2] error: a poll hit its deadline
+  // [0] epoch, [1] retired workgroups, [2] error: a poll hit its deadline; [3] segments stolen
+  // (diagnostics, never reset)
+  unsigned* ctl = sk;
   unsigned* flags = sk + 64;     // one word per workgroup (its publishing segment)
   auto ubeg = [&](int x) { return (long)x * U / P; };
 
@@ -647,7 +650,7 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_sk_kernel(const bf16* __rest
     }
     run(jt, j0, j1);
     if (stage == 0) {
-      store_part(part + (size_t)w * PSZ);
+      if (!(test & 2)) store_part(part + (size_t)w * PSZ);
       __syncthreads();
       if (tid == 0) __hip_atomic_store(flags + w, (e << 2) | 2u, RLX, AG);
       stage = 1;
@@ -670,7 +673,11 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_sk_kernel(const bf16* __rest
           const bool now = (cur >> 2) == e && (cur & 3u) != 0;
           if (now && (cur & 3u) == 2u) { st = 2; break; }                       // published
           if (!now) {                                                           // untouched: steal it
-            if (__hip_atomic_compare_exchange_strong(flags + c, &cur, (e << 2) | 3u, RLX, RLX, AG)) { st = 3; break; }
+            if (__hip_atomic_compare_exchange_strong(flags + c, &cur, (e << 2) | 3u, RLX, RLX, AG)) {
+              __hip_atomic_fetch_add(ctl + 3, 1u, RLX, AG);                      // diagnostics: steals
+              st = 3;
+              break;
+            }
             continue;
           }
           if ((cur & 3u) == 3u || __builtin_amdgcn_s_memrealtime() > t_end) {   // (never: one finisher per segment)
@@ -686,7 +693,7 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_sk_kernel(const bf16* __rest
       const unsigned st = bc[2];
       __syncthreads();           // every wave has read bc[2] before the next contributor's poll rewrites it
       if (st == 2) {
-        add_part(part + (size_t)c * PSZ);
+        if (!(test & 2)) add_part(part + (size_t)c * PSZ);
       } else if (st == 3) {
         store_part(scr);         // own sum so far -> scratch; the stolen segment runs from a zero accumulator
         stole = true;
