@@ -4,6 +4,12 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...        (driver form for N > 1)
 
+``python bench.py --gpus N`` (N > 1) with no launcher environment (WORLD_SIZE unset) launches
+itself: the parent process touches no GPU API, starts N rank processes of this script (RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, one process per GPU), passes
+rank 0's JSON line through, and exits non-zero if any rank fails or the job outlives
+``--launch-timeout``.
+
 One *step* = one serving round: ``batch x N`` fresh requests (synthetic prompt ids of
 ``--prompt-len`` tokens) are submitted at once and the engine runs until every one of
 them has produced ``--gen-len`` new tokens (prefill + continuous-batched decode, greedy,
@@ -71,6 +77,9 @@ def parse(argv=None):
     ap.add_argument("--mixed-tokens", type=int, default=None,
                     help="EngineConfig.mixed_prefill_tokens: prompt tokens a step may add to running decode "
                          "rows (0 = prefill-first steps; default: the config's)")
+    ap.add_argument("--launch-timeout", type=float, default=3600.0,
+                    help="self-launched multi-GPU runs (--gpus N > 1 without torchrun): kill every rank and "
+                         "exit non-zero after this many seconds")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace", default=None, metavar="DIR",
                     help="record a roctx/host/GPU timeline of the timed steps: DIR/trace_rank<r>.json "
@@ -116,6 +125,9 @@ def emit(args, world, elapsed, lat, extra, global_batch=None):
         "dtype": "bf16" if args.quant == "none" else "fp8 (W8A8 projections, bf16 rest)",
         "data": "synthetic (random-init weights, random prompt ids)",
         "p50_latency_ms": round(1000 * statistics.median(lat), 3) if lat else None,
+        # closed loop: every request of a round is submitted at once and the round ends when the
+        # last one finishes, so a request's latency is its round's (prefill + gen_len steps)
+        "latency_kind": "round (closed loop: all requests of a round submitted together)",
         "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.prompt_len + args.gen_len,
                    "prompt_len": args.prompt_len, "gen_len": args.gen_len,
                    "parallelism": _par_name(args, world)},
@@ -248,6 +260,7 @@ def run_open_loop(args):
            "requests": n, "offered_rate_rps": args.rate, "achieved_rate_rps": round(n / elapsed, 3),
            "p50_latency_ms": round(1000 * percentile(lat, 50), 3),
            "p99_latency_ms": round(1000 * percentile(lat, 99), 3),
+           "latency_kind": "request (open loop: scheduled arrival -> last token)",
            "output_tok_per_s": round(n * args.gen_len / elapsed, 2), "dtype": "bf16" if args.quant == "none" else "fp8",
            "data": "synthetic (random-init weights, random prompt ids)",
            "config": {"model": args.model, "max_batch": args.batch, "prompt_len": args.prompt_len,
@@ -259,6 +272,77 @@ def run_open_loop(args):
     if args.json_out:
         with open(args.json_out, "w") as f:
             f.write(line + "\n")
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """``--gpus N`` without a launcher: start N rank processes of this script (subprocess, never
+    exec; this process imports nothing that initialises HIP), rank r on GPU r.  Rank 0's stdout
+    (the JSON line) passes through; the other ranks' stdout goes to stderr.  The first rank to fail
+    ends the job: the others are terminated and its exit code is returned; so is 124 when the job
+    outlives ``--launch-timeout``."""
+    import signal
+    import subprocess
+    n = args.gpus
+    port = _free_port()
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(sys.argv[1:] if argv is None else argv)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else sys.stderr))
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except OSError:
+                    pass
+
+    def on_signal(signum, _frame):
+        stop_all()
+        raise SystemExit(128 + signum)
+
+    old = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGTERM, signal.SIGINT)}
+    t_end = time.monotonic() + args.launch_timeout if args.launch_timeout > 0 else None
+    rc = 0
+    clean = False
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                print(f"bench.py: a rank exited with {rc}; stopping the others", file=sys.stderr, flush=True)
+                break
+            if all(c == 0 for c in codes):
+                clean = True
+                break
+            if t_end is not None and time.monotonic() > t_end:
+                rc = 124
+                print(f"bench.py: ranks still running after --launch-timeout {args.launch_timeout:.0f} s",
+                      file=sys.stderr, flush=True)
+                break
+            time.sleep(0.2)
+    finally:
+        if not clean:
+            stop_all()
+            deadline = time.monotonic() + 20
+            while time.monotonic() < deadline and any(p.poll() is None for p in procs):
+                time.sleep(0.2)
+            stop_all(signal.SIGKILL)
+        for p in procs:
+            p.wait()
+        for sg, h in old.items():
+            signal.signal(sg, h)
+    return rc
 
 
 def main(argv=None):
@@ -273,6 +357,11 @@ def main(argv=None):
         if world > 1 or args.gpus > 1:
             raise SystemExit("--rate (open-loop latency mode) runs on one GPU")
         return run_open_loop(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        rc = launch_ranks(args, argv)
+        if rc:
+            raise SystemExit(rc)
+        return None
     if world > 1 or args.gpus > 1:
         from distributed_llms_amd.parallel.bench_dist import run_distributed
         return run_distributed(args, emit, make_prompts, start_trace, finish_trace)

@@ -204,9 +204,16 @@ PRESETS: Dict[str, ModelConfig] = {
 
 
 def get_model_config(spec: str) -> ModelConfig:
-    """Resolve ``spec``: a preset name, ``synthetic:<preset>``, or a directory with ``config.json``."""
+    """Resolve ``spec``: a preset name, ``synthetic:<preset>``, or a directory with ``config.json``.
+    ``<preset>@<N>l``: the preset's dimensions with N layers (full-size layer shapes at a depth a
+    test or a one-GPU rehearsal can afford, e.g. ``llama3-70b@4l``)."""
     if spec.startswith("synthetic:"):
         spec = spec.split(":", 1)[1]
+    if "@" in spec and spec.rsplit("@", 1)[0] in PRESETS:
+        base, depth = spec.rsplit("@", 1)
+        if not (depth.endswith("l") and depth[:-1].isdigit() and int(depth[:-1]) >= 1):
+            raise KeyError(f"model {spec!r}: expected <preset>@<layers>l, e.g. {base}@4l")
+        return dataclasses.replace(PRESETS[base], name=spec, num_layers=int(depth[:-1]))
     if spec in PRESETS:
         return dataclasses.replace(PRESETS[spec])
     for cand in (os.path.join(spec, "config.json"), os.path.join(spec, "shards", "config.json"), spec):

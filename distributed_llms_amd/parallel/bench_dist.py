@@ -107,6 +107,11 @@ def run_distributed(args, emit, make_prompts, start_trace=None, finish_trace=Non
         extra["stage_busy_frac"] = busy
         kinds = sorted({i["transport"] for i in info})
         extra["transport"] = kinds[0] if len(kinds) == 1 else kinds
+        # a pipeline run names the RCCL data plane only when every rank sat on an RCCL edge:
+        # otherwise the field says how many did (never a bare "rccl" over a partial plane)
+        n_rccl = sum(1 for i in info if i["rccl_comm_ranks"])
+        if ctx.pp > 1 and extra["transport"] in ("rccl", "rccl-standin") and n_rccl != world:
+            extra["transport"] = f"{extra['transport']} on {n_rccl} of {world} ranks"
         # every native RCCL communicator appears on both of its ranks: count them once.  The
         # pipeline data plane is built from 2-rank EDGE communicators (stage s <-> s + 1, plus
         # the ids ring closure last -> first), so rccl_comm_nranks is [2] at any N -- the number

@@ -134,3 +134,34 @@ def test_pp_stage_times_cpu():
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "pp2 half-layer" in r.stdout and "pp2 sub-layer" in r.stdout and r.stdout.count("stage us") == 2
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n", [2, 4])
+def test_plain_bench_gpus_n_launches_its_own_ranks_cpu(n):
+    """The literal `python bench.py --gpus N` (no torchrun, no launcher environment) starts its N
+    rank processes itself and relays rank 0's single JSON line (review round 5, item 1)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                               "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "1", "--warmup", "1",
+           "--model", "tiny-llama", "--batch", "3", "--prompt-len", "6", "--gen-len", "4"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    rec = lines[0]
+    assert KEYS <= set(rec) and rec["n_gpus"] == n and rec["value"] > 0
+    assert rec["config"]["parallelism"] == f"pp{n}" and rec["latency_kind"].startswith("round")
+    assert len(rec["stage_busy_frac"]) == n
+
+
+def test_plain_bench_gpus_n_fails_loudly_when_a_rank_fails_cpu():
+    """A rank that cannot start (here: an unknown model) makes the self-launched job exit non-zero
+    with no JSON line, instead of hanging the others."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--model", "no-such-model", "--launch-timeout", "300"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode != 0 and not _json_lines(r.stdout)

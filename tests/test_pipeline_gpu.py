@@ -28,7 +28,8 @@ def test_loopback_pipeline_gpu(cuda, stages):
     assert drv.num_steps > 0
 
 
-def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fine="0", small_budget=False):
+def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fine="0", small_budget=False,
+                   model="tiny-llama-d128"):
     import os
     # token-for-token checks run the half-layer plans they were written against: every cut rounds
     # the residual stream to bf16 once more than the fused split-K add + norm of the single engine
@@ -45,7 +46,7 @@ def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fi
     from distributed_llms_amd.parallel.dist_engine import RankRole, init_distributed
     ctx = init_distributed(pp=world)
     assert ctx.device == "cuda:0" and ctx.host_staged
-    role = RankRole(ctx, _mp_ecfg(world, small_budget))
+    role = RankRole(ctx, _mp_ecfg(world, small_budget, model))
     if transport == "ipc":
         from distributed_llms_amd.parallel.ipc_transport import IpcTransport
         assert isinstance(role.transport, IpcTransport)
@@ -65,11 +66,11 @@ def _gpu_rank_main(rank, world, port, prompts, out_q, transport="", rounds=1, fi
     dist.destroy_process_group()
 
 
-def _mp_ecfg(world, small_budget=False):
+def _mp_ecfg(world, small_budget=False, model="tiny-llama-d128"):
     # small_budget: 8 prompt tokens per step -- the prompts are admitted over many steps, most of
     # them MIXED (decode rows + a prompt chunk), and chunked across steps
     extra = dict(max_prefill_tokens=8, mixed_prefill_tokens=8) if small_budget else {}
-    return EngineConfig(model="tiny-llama-d128", dtype="bfloat16", device="cuda", max_batch=4, max_seq_len=256,
+    return EngineConfig(model=model, dtype="bfloat16", device="cuda", max_batch=4, max_seq_len=256,
                         num_kv_blocks=128, graph_batch_sizes=(1, 2, 4), num_workers=world, seed=3, **extra)
 
 
@@ -84,7 +85,8 @@ def test_multiprocess_gpu_pipeline_host_staged(cuda, world):
     assert res[0] == [ref]
 
 
-def _run_ranks(world, prompts, transport, rounds, fine="0", small_budget=False):
+def _run_ranks(world, prompts, transport, rounds, fine="0", small_budget=False, model="tiny-llama-d128",
+               timeout_s=240):
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -94,14 +96,15 @@ def _run_ranks(world, prompts, transport, rounds, fine="0", small_budget=False):
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     # daemonic: a rank stuck in a stream wait dies with the test process instead of outliving it
-    procs = [ctxm.Process(target=_gpu_rank_main, args=(r, world, port, prompts, q, transport, rounds, fine, small_budget),
-                            daemon=True)
+    procs = [ctxm.Process(target=_gpu_rank_main,
+                          args=(r, world, port, prompts, q, transport, rounds, fine, small_budget, model),
+                          daemon=True)
              for r in range(world)]
     for p in procs:
         p.start()
     import queue
     import time
-    res, deadline = {}, time.monotonic() + 240
+    res, deadline = {}, time.monotonic() + timeout_s
     while len(res) < world:             # fail fast (and loudly) when a rank dies instead of reporting
         try:
             r, o = q.get(timeout=2)
@@ -109,7 +112,7 @@ def _run_ranks(world, prompts, transport, rounds, fine="0", small_budget=False):
         except queue.Empty:
             dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
             assert not dead, f"stage process exited with {dead}"
-            assert time.monotonic() < deadline, "stage processes did not finish within 240 s"
+            assert time.monotonic() < deadline, f"stage processes did not finish within {timeout_s} s"
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -138,6 +141,21 @@ def test_multiprocess_gpu_pipeline_rccl_transport_standin(cuda, world):
     prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
     ref = LLMEngine(_mp_ecfg(1)).generate(prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
     res = _run_ranks(world, prompts, "rccl-standin", rounds=2)
+    assert res[0] == [ref, ref]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("model,world", [("llama3-70b@4l", 4), ("mixtral-8x7b@4l", 4), ("llama3-70b@8l", 8)])
+def test_multiprocess_gpu_pipeline_standin_big_model_dims(cuda, model, world):
+    """BASELINE configs 4 and 5 at pipeline depth on the RCCL transport's multi-rank path (device
+    stand-in, stage processes sharing the one GPU): Llama-3-70B and Mixtral-8x7B layer shapes
+    (hidden 8192 / 28672-wide MLP / 128k vocab; 8 experts of 14336, top-2) at reduced depth, so the
+    reference engine and the stage processes fit beside each other.  Two rounds reproduce the
+    single-process engine token for token."""
+    prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
+    ref = LLMEngine(_mp_ecfg(1, model=model)).generate(prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
+    torch.cuda.empty_cache()
+    res = _run_ranks(world, prompts, "rccl-standin", rounds=2, model=model, timeout_s=420)
     assert res[0] == [ref, ref]
 
 

@@ -318,3 +318,17 @@ def test_master_plans_carry_the_unit_group(monkeypatch):
     assert [p["unit_group"] for p in plans] == [5, 5]
     assert [p["unit_range"] for p in plans] == [[0, 31], [31, 60]]
     assert [p["layer_range"] for p in plans] == [[0, 7], [6, 12]]
+
+
+def test_reduced_depth_preset_keeps_layer_shapes():
+    """``<preset>@<N>l``: a preset's full-size layer dimensions at N layers (GPU tests and one-GPU
+    pipeline rehearsals of the 70B / Mixtral configs)."""
+    from distributed_llms_amd.config import PRESETS, get_model_config
+    c = get_model_config("synthetic:llama3-70b@4l")
+    full = PRESETS["llama3-70b"]
+    assert c.num_layers == 4 and c.name == "llama3-70b@4l"
+    assert (c.hidden_size, c.intermediate_size, c.num_heads, c.num_kv_heads, c.vocab_size) == \
+        (full.hidden_size, full.intermediate_size, full.num_heads, full.num_kv_heads, full.vocab_size)
+    assert get_model_config("mixtral-8x7b@2l").num_experts == 8
+    with pytest.raises(KeyError):
+        get_model_config("llama3-70b@x")
