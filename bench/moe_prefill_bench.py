@@ -1,4 +1,4 @@
-"""Grouped expert prefill GEMMs in isolation (Mixtral-8x7B shapes): why is the persistent form slower?
+"""Grouped expert prefill GEMMs in isolation (Mixtral-8x7B shapes): gemm_pp_moe vs the dense kernel.
 
     python bench/moe_prefill_bench.py [--tokens 32768] [--rounds 5]
 
@@ -6,10 +6,8 @@ T tokens routed top-2 over 8 experts with equal counts (T * 2 / 8 rows each), ex
 Candidates per projection (gate|up with the SwiGLU fused, then down), us per call and TF/s:
   pp_moe      gemm_pp_moe: one 256 x 256 tile per workgroup over the slot space, rows gathered
               through the slot -> token list inside the kernel
-  pf_moe      gemm_pf MOE form, static tile walk (rows pre-gathered into slot order)
-  pf_moe_dyn  the same with the per-XCD dynamic tile queue
-  pf_moe_g32 / _g16   static walk with 32 / 16 row tiles per group of the tile order (8 default):
-              a group spanning an expert's whole segment reads its weight once
+  (a persistent gemm_pf MOE form, with static and dynamic tile walks and 8 / 16 / 32-row-tile
+  groups, was measured slower in round 5 -- profiles/round5_moe_prefill.md -- and removed)
   dense_pf    gemm_pf on ONE expert's weight over all slots: the same FLOPs, no expert segments
 """
 import argparse
@@ -51,10 +49,6 @@ def main():
         k.gemm_pp_moe(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), wgu.data_ptr(), counts.data_ptr(),
                       offsets.data_ptr(), E, 2 * I, H, T, slots, 1, st)
 
-    def gu_pf(walk):
-        return lambda: k.gemm_pf_moe(act.data_ptr(), xs.data_ptr(), wgu.data_ptr(), counts.data_ptr(),
-                                     offsets.data_ptr(), E, 2 * I, H, slots, 1 | walk, st)
-
     def gu_dense():
         gemm.linear_pf(xs, wgu[0], swiglu=True)
 
@@ -62,17 +56,11 @@ def main():
         k.gemm_pp_moe(ys.data_ptr(), act.data_ptr(), 0, wd.data_ptr(), counts.data_ptr(), offsets.data_ptr(),
                       E, H, I, slots, slots, 0, st)
 
-    def dn_pf(walk):
-        return lambda: k.gemm_pf_moe(ys.data_ptr(), act.data_ptr(), wd.data_ptr(), counts.data_ptr(),
-                                     offsets.data_ptr(), E, H, I, slots, walk, st)
-
     def dn_dense():
         gemm.linear_pf(act, wd[0])
 
-    cands = {"gate_up": {"pp_moe": gu_pp, "pf_moe": gu_pf(2), "pf_moe_dyn": gu_pf(0), "pf_moe_g32": gu_pf(2 | 4),
-                         "pf_moe_g16": gu_pf(2 | 8), "dense_pf": gu_dense},
-             "down": {"pp_moe": dn_pp, "pf_moe": dn_pf(2), "pf_moe_dyn": dn_pf(0), "pf_moe_g32": dn_pf(2 | 4),
-                      "pf_moe_g16": dn_pf(2 | 8), "dense_pf": dn_dense}}
+    cands = {"gate_up": {"pp_moe": gu_pp, "dense_pf": gu_dense},
+             "down": {"pp_moe": dn_pp, "dense_pf": dn_dense}}
     flops = {"gate_up": 2.0 * slots * 2 * I * H, "down": 2.0 * slots * H * I}
     for proj, fns in cands.items():
         res = {n: [] for n in fns}

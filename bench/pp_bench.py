@@ -87,7 +87,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--pf-variants", type=int, nargs="*", default=[], help="gemm_pf variants 1-11 (8: nontemporal stores; 9-11: split A / B release; SwiGLU: 8-11)")
+    ap.add_argument("--pf-variants", type=int, nargs="*", default=[], help="gemm_pf variants (8: nontemporal output stores)")
     a = ap.parse_args()
     torch.manual_seed(0)
     for name in ([] if a.no_decode else a.shapes):
@@ -127,7 +127,7 @@ def main():
                     impls[f"pp{bn}g{'S2' if grp & 64 else ''}"] = (lambda w, v=v: gemm.linear_pp(
                         x, w, splits=1, swiglu=sw, variant=v))
             impls["pf"] = lambda w: gemm.linear_pf(x, w, swiglu=sw)   # persistent schedule 2
-            for v in ([u for u in a.pf_variants if u == 8 or u >= 9] if sw else a.pf_variants):
+            for v in [u for u in a.pf_variants if u == 8]:
                 impls[f"pf{v}"] = lambda w, v=v: gemm.linear_pf(x, w, swiglu=sw, variant=v)
             graphs = {key: graph_of(f, [w], 2) for key, f in impls.items()}
             res = {key: [] for key in graphs}

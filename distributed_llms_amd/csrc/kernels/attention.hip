@@ -129,16 +129,6 @@ __device__ __forceinline__ void compute_chunk(WaveState<D>& st, const bf16x8 (&q
   }
 }
 
-// Load + compute one chunk (prefill: its chunks are issued by 4 waves in turn).
-template <int D>
-__device__ __forceinline__ void attend_chunk(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
-                                             const bf16* __restrict__ kblk, const bf16* __restrict__ vblk,
-                                             int t0, int kmax_col, float scale_log2, int lane) {
-  KVChunk<D> c;
-  load_chunk<D>(c, kblk, vblk, lane);
-  compute_chunk<D>(st, qf, c, t0, kmax_col, scale_log2, lane);
-}
-
 template <int D>
 __device__ __forceinline__ void init_state(WaveState<D>& st) {
 #pragma unroll
@@ -449,67 +439,17 @@ __global__ void __launch_bounds__(D) attn_split_reduce_kernel(bf16* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// Prefill (causal, varlen, context already in the paged cache): grid
-// (q_tiles, Hkv, B). Each wave owns R = 16/G query rows x G heads; rows of
-// sequence b are its LAST q_len tokens of ctx (chunked prefill supported).
+// Prefill (causal, varlen, context already in the paged cache): grid (q_tiles, Hkv, B); each wave
+// owns 16/G query rows x G heads per column tile, the rows of sequence b being its LAST q_len tokens
+// of ctx (chunked prefill).  Two kernels remain: the LDS-shared v4 below (default) and v3 here, its
+// fallback beyond the 32k tokens of block ids v4 stages.  The first design (v1: one tile per wave,
+// load -> compute per chunk, 563 us per 8B layer for 256 x 128-token prompts), v2 at one tile per
+// wave and v4 at four tiles per wave (one wave per SIMD, slower) were measured and removed.
 // ---------------------------------------------------------------------------
-template <int D, int G>
-__global__ void __launch_bounds__(256) attn_prefill_kernel(
-    bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
-    const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
-    const int32_t* __restrict__ cu_seqlens_q, const int32_t* __restrict__ seq_lens, int hq, int hkv,
-    int max_blocks, float scale_log2) {
-  constexpr int R = 16 / G;
-  const int kvh = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int qs = cu_seqlens_q[b], ql = cu_seqlens_q[b + 1] - qs;
-  const int row0 = (blockIdx.x * kWaves + w) * R;
-  if (row0 >= ql) return;
-  const int ctx = seq_lens[b];
-  const int qpos0 = ctx - ql;  // position of row 0
-  const int crow = row0 + r / G, ch = r % G;
-  const bool col_ok = crow < ql;
-  const int kmax_col = col_ok ? qpos0 + crow : -1;
-  bf16x8 qf[D / 32];
-  const bf16* qrow = q + ((size_t)(qs + (col_ok ? crow : 0)) * hq + kvh * G + ch) * D;
-#pragma unroll
-  for (int ks = 0; ks < D / 32; ++ks) {
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
-    if (!col_ok) v = bf16x8{};
-    qf[ks] = v;
-  }
-  WaveState<D> st;
-  init_state(st);
-  const int wave_kmax = qpos0 + min(row0 + R, ql) - 1;
-  const int32_t* bt = block_tables + (size_t)b * max_blocks;
-  const size_t kv_head_stride = (size_t)kBS * D;
-  for (int c = 0; c * kBS <= wave_kmax; ++c) {
-    const int blk = bt[c];
-    const size_t base = ((size_t)blk * hkv + kvh) * kv_head_stride;
-    attend_chunk<D>(st, qf, k_cache + base, v_cache + base, c * kBS, kmax_col, scale_log2, lane);
-  }
-  float lt = st.lsum;
-  lt += __shfl_xor(lt, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
-  if (!col_ok) return;
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  bf16* orow = out + ((size_t)(qs + crow) * hq + kvh * G + ch) * D;
-#pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt) {
-    bf16x4 o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = f2bf(st.acc[dt][i] * inv);
-    *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = o;
-  }
-}
-
 // ---------------------------------------------------------------------------
-// Prefill v2: each wave owns NT column tiles (NT x 16/G query rows x G heads) and walks the
+// Prefill v3: each wave owns NT column tiles (NT x 16/G query rows x G heads) and walks the
 // KV chunks with the decode kernel's depth-2 pipeline (chunk c+1's K/V loads in flight while
 // chunk c's MFMAs run), so every loaded chunk serves NT tiles and its load latency is hidden.
-// The v1 kernel above (one tile per wave, load -> compute per chunk) exposed one HBM/L2
-// latency per chunk per 16/G rows: 563 us per Llama-3-8B layer for 256 prompts of 128 tokens.
 // ---------------------------------------------------------------------------
 template <int D, int G, int NT>
 __global__ void __launch_bounds__(256, NT == 1 ? 2 : 1) attn_prefill2_kernel(
@@ -916,9 +856,8 @@ template <int D>
 static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv, hipStream_t s, uintptr_t out,
                            uintptr_t q, uintptr_t k_cache, uintptr_t v_cache, uintptr_t bt, uintptr_t cu, uintptr_t sl,
                            int hq, int max_blocks, float sl2, uintptr_t pos, uintptr_t cs, int q_stride) {
-  // version 1: v1 kernel; 2: v2 with one tile per wave (2 waves/SIMD); 3: v2 with two tiles per wave;
-  // 4 / 5: the LDS-shared kernel with two / four tiles per wave
-  const int nt = version == 5 ? 4 : (version == 3 || version == 4) ? 2 : 1;
+  // version 3: the register-tiled kernel, two tiles per wave; 4: the LDS-shared kernel, two tiles per wave
+  const int nt = 2;
   const int rows_per_wg = kWaves * (16 / g) * nt;
   const dim3 grid((max_q_len + rows_per_wg - 1) / rows_per_wg, hkv, batch);
 #define DLLM_PF(GG)                                                                                         \
@@ -928,21 +867,8 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
                          (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,      \
                          (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2,                   \
                          (const int32_t*)pos, (const float*)cs, q_stride);                                   \
-    else if (version == 5)                                                                                  \
-      hipLaunchKernelGGL((attn_prefill_lds_kernel<D, GG, 4>), grid, dim3(256), 0, s, (bf16*)out,              \
-                         (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,      \
-                         (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2,                   \
-                         (const int32_t*)pos, (const float*)cs, q_stride);                                   \
-    else if (version == 3)                                                                                  \
-      hipLaunchKernelGGL((attn_prefill2_kernel<D, GG, 2>), grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,  \
-                         (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt, (const int32_t*)cu,   \
-                         (const int32_t*)sl, hq, hkv, max_blocks, sl2);                                      \
-    else if (version == 2)                                                                                  \
-      hipLaunchKernelGGL((attn_prefill2_kernel<D, GG, 1>), grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,  \
-                         (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt, (const int32_t*)cu,   \
-                         (const int32_t*)sl, hq, hkv, max_blocks, sl2);                                      \
     else                                                                                                    \
-      hipLaunchKernelGGL((attn_prefill_kernel<D, GG>), grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,     \
+      hipLaunchKernelGGL((attn_prefill2_kernel<D, GG, 2>), grid, dim3(256), 0, s, (bf16*)out, (const bf16*)q,  \
                          (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt, (const int32_t*)cu,   \
                          (const int32_t*)sl, hq, hkv, max_blocks, sl2);                                      \
   } while (0)
@@ -958,7 +884,7 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
 }
 
 // positions / cos_sin / q_stride: q is the raw qkv projection (row stride q_stride elements) and RoPE
-// is applied in the kernel (LDS kernel, versions 4 / 5); cos_sin = 0: q is [T, hq, D], rotated
+// is applied in the kernel (LDS kernel, version 4); cos_sin = 0: q is [T, hq, D], rotated
 void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache,
                              uintptr_t block_tables, uintptr_t cu_seqlens_q, uintptr_t seq_lens, int batch,
                              int hq, int hkv, int d, int block_size, int max_blocks, int max_q_len, float scale,
@@ -974,12 +900,11 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float sl2 = scale * 1.4426950408889634f;
   // version (knobs.prefill_attn): 4 = the LDS-shared kernel (default; bench/prefill_attn_bench.py:
-  // 1.6-1.7x v3 from 128- to 8192-token prompts); 5 = the same at 4 tiles per wave (one wave per
-  // SIMD: slower); 1-3 = the earlier register-tiled kernels (tests)
-  DLLM_HOST_CHECK(version >= 1 && version <= 5, "prefill attention version 1..5");
-  // the LDS kernel stages the block ids of a whole sequence: fall back beyond 32k context
-  if (version >= 4 && max_blocks > kPfMaxChunks) version = 3;
-  DLLM_HOST_CHECK(q_stride == hq * d || version >= 4, "in-kernel RoPE / strided q: LDS kernel only (<= 32k context)");
+  // 1.6-1.7x v3 from 128- to 8192-token prompts); 3 = the register-tiled kernel, which also serves
+  // block tables wider than the 32k tokens of block ids the LDS kernel stages
+  DLLM_HOST_CHECK(version == 3 || version == 4, "prefill attention version 3 or 4");
+  if (version == 4 && max_blocks > kPfMaxChunks) version = 3;
+  DLLM_HOST_CHECK(q_stride == hq * d || version == 4, "in-kernel RoPE / strided q: LDS kernel only (<= 32k context)");
   if (d == 128)
     launch_prefill<128>(G, version, max_q_len, batch, hkv, s, out, q, k_cache, v_cache, block_tables, cu_seqlens_q,
                         seq_lens, hq, max_blocks, sl2, positions, cos_sin, q_stride);

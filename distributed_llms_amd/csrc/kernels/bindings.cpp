@@ -23,7 +23,6 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("splitk_add_rms_norm", &dllm::splitk_add_rms_norm);
   m.def("splitk_reduce", &dllm::splitk_reduce);
   m.def("gemm_wide", &dllm::gemm_wide);
-  m.def("gemm_wide_sk", &dllm::gemm_wide_sk);
   m.def("gemm_wide_fp8", &dllm::gemm_wide_fp8);
   m.def("quant_fp8_rows", &dllm::quant_fp8_rows);
   m.def("rms_norm_q8", &dllm::rms_norm_q8);
@@ -33,7 +32,6 @@ PYBIND11_MODULE(_C_kernels, m) {
   m.def("gemm_pp_moe", &dllm::gemm_pp_moe);
   m.def("gemm_pp", &dllm::gemm_pp);
   m.def("gemm_pf", &dllm::gemm_pf);
-  m.def("gemm_pf_moe", &dllm::gemm_pf_moe);
   m.def("moe_combine", &dllm::moe_combine);
   m.def("moe_wide_gemm", &dllm::moe_wide_gemm);
   m.def("moe_router_route", &dllm::moe_router_route);

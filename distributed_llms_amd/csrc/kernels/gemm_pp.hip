@@ -739,11 +739,11 @@ void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintpt
 // w = (b % 8) (P / 8) + b / 8), so each XCD's L2 serves 32 consecutive tiles of the grouped order
 // (8 row tiles x 4 column tiles) at a time.
 // MODE 0: C bf16 [M, N];  2: SwiGLU C [M, N / 2] with B = [Bg; Bu] (row groups as pp_b_row).
-// SCH: schedule variant (0 = the shipped one; others for bench/pp_bench.py sweeps): see pf_sched;
-// 8 = the shipped schedule with nontemporal output stores (large SwiGLU outputs)
+// SCH 8: nontemporal output stores (large SwiGLU outputs), else 0.  The schedule sweeps of rounds 3-5
+// (barrier positions, piece spacing, row-group widths, and the split A / B LDS release of round 5,
+// all within 0.5 % of this schedule: profiles/round5_raw/r5d_pf_sched.txt) were removed.
 struct PfSched {
   int ib1, ib3, ge, gm;
-  int ibb = 0, geb = 0, gea = 0;   // split release: barrier after the B reads, B / A piece spacing
 };
 
 // ---- gemm_pf's dynamic tile queue (DYN).  The grouped tile order is cut into chunks of PF_CH
@@ -799,31 +799,14 @@ __device__ void pf_retire(int* q, int grid) {                      // lane 0, on
     __hip_atomic_store(q + 256, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-constexpr PfSched pf_sched(int sch) {
-  // {barrier after set-1 reads (MFMA), barrier before set-0 reads, MFMAs between pieces (0 = spread
-  // over the rest of the K-tile), row tiles per group of the tile order}
-  // 9 / 10 / 11: the A and B LDS regions released separately (hipBLASLt's loop): a barrier once every
-  // wave has read its B fragments (after MFMA ibb) frees the B half of the slot, whose pieces then
-  // go out every geb MFMAs; the A pieces follow every gea MFMAs after the barrier at ib1 -- the
-  // 16 pieces spread over ~90 MFMAs instead of ~75, each with more MFMA cycles to hide its issue
-  return sch == 1 ? PfSched{36, 88, 0, 8} : sch == 2 ? PfSched{48, 88, 0, 8} : sch == 3 ? PfSched{40, 80, 0, 8}
-       : sch == 4 ? PfSched{40, 96, 0, 8} : sch == 5 ? PfSched{40, 88, 4, 8} : sch == 6 ? PfSched{40, 88, 0, 4}
-       : sch == 7 ? PfSched{40, 88, 0, 16} : sch == 9 ? PfSched{40, 88, 0, 8, 20, 6, 6}
-       : sch == 10 ? PfSched{40, 88, 0, 8, 20, 5, 6} : sch == 11 ? PfSched{40, 96, 0, 8, 22, 6, 7}
-       : sch == 12 ? PfSched{40, 88, 0, 32}   // MOE: a row group spans a whole expert segment (T = 32K)
-       : PfSched{40, 88, 0, 8};
-}
+// {barrier after set-1 reads (MFMA), barrier before set-0 reads, MFMAs between pieces (0 = spread
+// over the rest of the K-tile), row tiles per group of the tile order}
+constexpr PfSched kPfSched{40, 88, 0, 8};
 
-// MOE: the grouped expert GEMM of the prefill (Mixtral) in this persistent form: A is the
-// expert-sorted activation [slots, K] (M = slots), B = W [E, N, K], C [slots, N (SwiGLU N / 2)];
-// the row tiles are every expert's segment of the slot space (counts read on the device into an
-// LDS table at the start -- no host sync), walked exactly as the dense tiles, with the expert's
-// weight selected by the B staging offset and rows past the segment dropped by the epilogue.
-template <int MODE, int SCH = 0, bool DYN = false, bool MOE = false>
+template <int MODE, int SCH = 0, bool DYN = false>
 __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                          bf16* __restrict__ C, int M, int N, int K,
-                                                         int* __restrict__ queue, const int* __restrict__ counts,
-                                                         const int* __restrict__ offsets, int E) {
+                                                         int* __restrict__ queue) {
   constexpr int NW = 4, NWN = 2, BM = 256, BN = 256, TM = 128, TN = BN / NWN;
   constexpr int RT = TM / 16, CT = TN / 16;            // 8 x 8 accumulators per wave
   constexpr int SLOT = (BM + BN) * PBK, NB = 2;        // 2 x 64 KiB ring
@@ -834,28 +817,12 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) bf16 smem[NB * SLOT];
   __shared__ int tq[4];                                // DYN: tile of local ordinal i at [i & 3]
-  __shared__ int seg[3 * 17];                          // MOE: first row tile, slot offset, count per expert
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv / NWN, wn = wv % NWN;
   const int ldc = SWIGLU ? N / 2 : N;
-  int mtiles = (M + BM - 1) / BM;
-  if constexpr (MOE) {
-    if (tid == 0) {
-      int t0 = 0;
-      for (int x = 0; x < E; ++x) {
-        const int c = counts[x];
-        seg[x] = t0;
-        seg[17 + x] = offsets[x];
-        seg[34 + x] = c;
-        t0 += (c + BM - 1) / BM;
-      }
-      seg[E] = t0;
-    }
-    __syncthreads();
-    mtiles = seg[E];
-  }
+  const int mtiles = (M + BM - 1) / BM;
   const int ntn = N / BN, tiles = ntn * mtiles;
   const int P = gridDim.x;                             // a multiple of 8 (host)
   const int w = (int)(blockIdx.x & 7) * (P >> 3) + (int)(blockIdx.x >> 3);
@@ -876,7 +843,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
     mine = w < tiles ? (tiles - 1 - w) / P + 1 : 0;
     if (mine == 0) return;                             // uniform: before any load or barrier
   }
-  constexpr int GM = pf_sched(SCH).gm;                // row tiles per group of the tile order
+  constexpr int GM = kPfSched.gm;                      // row tiles per group of the tile order
   const int nt = K / PBK, per = GM * ntn;
   auto tile_of = [&](int i) { return DYN ? tq[i & 3] : w + i * P; };   // my i-th tile (grouped order)
   auto tile_mn = [&](int tau, int& m_t, int& n_t) {
@@ -884,29 +851,13 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
     m_t = first + q % gsz;
     n_t = q / gsz;
   };
-  // the rows of (virtual) row tile m_t: [r0, min(r0 + BM, rcnt)) of the segment starting at slot
-  // roff, weight of expert ex (dense: one segment, rows 0 .. M)
-  auto rows_of = [&](int m_t, int& r0, int& rcnt, int& roff, int& ex) {
-    if constexpr (MOE) {
-      ex = 0;
-      for (int x = 1; x < E; ++x) ex = m_t >= seg[x] ? x : ex;
-      r0 = (m_t - seg[ex]) * BM;
-      roff = seg[17 + ex];
-      rcnt = seg[34 + ex];
-    } else {
-      r0 = m_t * BM;
-      roff = 0;
-      rcnt = M;
-      ex = 0;
-    }
-  };
 
   // ---- staging side: tile s_i's K-tile s_kt; per-lane A row offsets of that tile (rows past M
   // clamp to M - 1), B rows through the SGPR offset (uniform per piece)
   const __amdgpu_buffer_rsrc_t rsA =
       __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)(unsigned)((long)M * K * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)B, (short)0, (int)(unsigned)((long)(MOE ? E : 1) * N * K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)(unsigned)((long)N * K * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsC =
       __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, (int)(unsigned)((long)M * ldc * 2), 0x00020000);
   uint32_t chunk_q[2];
@@ -917,19 +868,16 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   for (int par = 0; par < 2; ++par) offB[par] = (uint32_t)(lane >> 3) * (uint32_t)(K * 2) + chunk_q[par];
   uint32_t offA[GA];
   int s_i = 0, s_kt = 0, s_n = 0;
-  uint32_t s_boff = 0;                                 // MOE: byte offset of the staging tile's expert weight
   int pend = -1, pend_i = 0;                           // DYN (lane 0): fetch in flight, its ordinal
   auto set_stage = [&](int tau) {
     int m_t, n_t;
     tile_mn(tau, m_t, n_t);
     s_n = n_t;
-    int r0, rcnt, roff, ex;
-    rows_of(m_t, r0, rcnt, roff, ex);
-    if constexpr (MOE) s_boff = (uint32_t)ex * (uint32_t)N * (uint32_t)(K * 2);
+    const int r0 = m_t * BM;
 #pragma unroll
     for (int j = 0; j < GA; ++j) {
       const int q = wv * GA + j, r = 8 * q + (lane >> 3);
-      offA[j] = (uint32_t)(roff + min(r0 + r, rcnt - 1)) * (uint32_t)(K * 2) + chunk_q[q & 1];
+      offA[j] = (uint32_t)min(r0 + r, M - 1) * (uint32_t)(K * 2) + chunk_q[q & 1];
     }
   };
   // piece p of the staging K-tile into ring slot `slot`
@@ -942,7 +890,7 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
       const int q = wv * GB + p - GA;
       const uint32_t brow = (uint32_t)pp_b_row<BN, SWIGLU>(8 * q, s_n, N / 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_vptr_p)(base + BM * PBK + q * 512), 16, (int)offB[q & 1],
-                                               (int)(brow * (uint32_t)(K * 2) + (uint32_t)(s_kt * PBK * 2) + s_boff),
+                                               (int)(brow * (uint32_t)(K * 2) + (uint32_t)(s_kt * PBK * 2)),
                                                0, 0);
     }
   };
@@ -992,23 +940,12 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
   f32x4 acc[RT][CT];
   bf16x8 fa0[RT], fb0[CT], fa1[RT], fb1[CT];
   constexpr int NMF = RT * CT, NR = RT + CT;
-  constexpr PfSched SC = pf_sched(SCH);
+  constexpr PfSched SC = kPfSched;
   constexpr int IB1 = SC.ib1;
   constexpr int GE = SC.ge ? SC.ge : ((2 * NMF - 4 - IB1 - 1) / G > 1 ? (2 * NMF - 4 - IB1 - 1) / G : 1);
   constexpr int IB3 = SC.ib3;
   static_assert(IB1 > 2 * NR - 1 && IB1 < NMF && IB3 >= NMF, "schedule 2 barriers");
-  // split release (SC.ibb > 0): B pieces p = GA .. G-1 at IBB + 1 + GEB k, A pieces p = 0 .. GA-1 at
-  // A0 + GEA k; NA = A-fragment reads issued after the last B read up to MFMA IBB (lgkmcnt(NA) then
-  // means every B read of this wave is done)
-  constexpr bool SPLIT = SC.ibb > 0;
-  constexpr int IBB = SC.ibb, GEB = SC.geb > 0 ? SC.geb : 1, GEA = SC.gea > 0 ? SC.gea : 1;
-  constexpr int BEND = IBB + 1 + GEB * (GB - 1);
-  constexpr int A0 = SPLIT ? (BEND + GEA > IB1 + 1 ? BEND + GEA : IB1 + 1) : IB1 + 1;
-  constexpr int NA = SPLIT ? ((IBB - 1) / 2 - CT + 1 > 0 ? (IBB - 1) / 2 - CT + 1 : 0) : 0;
-  constexpr int PB3S = (BEND <= IB3 ? GB : (IB3 - IBB - 1) / GEB + 1) +
-                       (A0 > IB3 ? 0 : ((IB3 - A0) / GEA + 1 < GA ? (IB3 - A0) / GEA + 1 : GA));
-  static_assert(!SPLIT || (IBB > 2 * CT && IBB < IB1 && A0 + GEA * (GA - 1) < 2 * NMF), "split release schedule");
-  constexpr int PB3 = SPLIT ? PB3S : ((IB3 - IB1 - 1) / GE + 1 < G ? (IB3 - IB1 - 1) / GE + 1 : G);
+  constexpr int PB3 = (IB3 - IB1 - 1) / GE + 1 < G ? (IB3 - IB1 - 1) / GE + 1 : G;
   constexpr int VC = (NB - 2) * G + PB3;
   static_assert(IB1 + 1 + GE * (G - 1) < 2 * NMF && IB3 + 1 + 2 * (NR - 1) < 2 * NMF, "schedule 2 fits a K-tile");
   static_assert(VC <= 63, "vmcnt");
@@ -1065,23 +1002,12 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
         else
           acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[c], fa1[r], acc[r][c], 0, 0, 0);
         if constexpr (i % 2 == 1 && i / 2 < NR) rd1(base1, std::integral_constant<int, i / 2>{});
-        if constexpr (SPLIT && i == IBB) {                 // every wave's B reads of this slot done
-          asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(NA) : "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          __builtin_amdgcn_s_barrier();
-        }
         if constexpr (i == IB1) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (SPLIT) {
-          if constexpr (i > IBB && (i - IBB - 1) % GEB == 0 && (i - IBB - 1) / GEB < GB)
-            piece(slot, GA + (i - IBB - 1) / GEB);
-          if constexpr (i >= A0 && (i - A0) % GEA == 0 && (i - A0) / GEA < GA) piece(slot, (i - A0) / GEA);
-        } else {
-          if constexpr (i > IB1 && (i - IB1 - 1) % GE == 0 && (i - IB1 - 1) / GE < G) piece(slot, (i - IB1 - 1) / GE);
-        }
+        if constexpr (i > IB1 && (i - IB1 - 1) % GE == 0 && (i - IB1 - 1) / GE < G) piece(slot, (i - IB1 - 1) / GE);
         if constexpr (i == IB3) {
           pp_vm<VC>();
           __builtin_amdgcn_sched_barrier(0);
@@ -1103,8 +1029,6 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
     // accumulator reads over.
     int m_t, n_t;
     tile_mn(tile_of(ti), m_t, n_t);
-    int e_r0, e_rcnt, e_roff, e_ex;
-    rows_of(m_t, e_r0, e_rcnt, e_roff, e_ex);
     const uint32_t colb = (uint32_t)(n_t * OUTW + wn * (OUTW / NWN) + 16 * (lq & 1) + 8 * (lq >> 1)) * 2;
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
@@ -1112,8 +1036,8 @@ __global__ void __launch_bounds__(256, 1) gemm_pf_kernel(const bf16* __restrict_
       // at the K loop's exit (and spill, draining the pipeline with vmcnt(0) waits)
 #pragma unroll
       for (int c = 0; c < CT; ++c) asm volatile("" : "+a"(acc[r][c]));
-      const int row = e_r0 + wm * TM + r * 16 + lr;       // row within the segment
-      const uint32_t vo = row < e_rcnt ? (uint32_t)(e_roff + row) * (uint32_t)(ldc * 2) + colb : 0x80000000u;
+      const int row = m_t * BM + wm * TM + r * 16 + lr;
+      const uint32_t vo = row < M ? (uint32_t)row * (uint32_t)(ldc * 2) + colb : 0x80000000u;
       constexpr int NQ = SWIGLU ? CT / 2 : CT;         // bf16 quads per lane in this row group
       u32x2 q[NQ];
 #pragma unroll
@@ -1180,7 +1104,8 @@ int* pf_queue(hipStream_t s) {
 
 // Persistent prefill GEMM: C = A B^T (mode 0) or SwiGLU (mode 1, C [M, N / 2], B = [Bg; Bu]),
 // 256 x 256 tiles, grid = min(tiles, CUs) rounded up to a multiple of 8.  variant bit 16: the
-// dynamic tile queue (DYN; needs K >= 128) instead of the static tile = w + i P walk.
+// dynamic tile queue (DYN; needs K >= 128) instead of the static tile = w + i P walk; variant 8:
+// nontemporal output stores (by default: SwiGLU outputs > 256 MiB).
 void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mode, int variant, uintptr_t stream) {
   const bool dyn = (variant & 16) != 0;
   variant &= ~16;
@@ -1189,6 +1114,7 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   DLLM_HOST_CHECK(K % PBK == 0 && K >= PBK, "K must be a positive multiple of 64");
   DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
   DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
+  DLLM_HOST_CHECK(variant == 0 || variant == 8, "variant 0 or 8 (nontemporal output stores)");
   // the output's byte range must stay below 2^31: rows past M are dropped by giving their stores
   // the offset 0x80000000, which has to lie outside the buffer's range
   DLLM_HOST_CHECK((long)M * K * 2 < (1L << 32) && (long)N * K * 2 < (1L << 32) &&
@@ -1208,102 +1134,20 @@ void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mod
   const long tiles = (long)(N / 256) * ((M + 255) / 256);
   DLLM_HOST_CHECK(tiles < (1L << 30), "tiles");
   const long grid = ((tiles < cus ? tiles : cus) + 7) / 8 * 8;
-  DLLM_HOST_CHECK(variant >= 0 && variant <= 11 && (mode == 0 || variant == 0 || variant == 8 || variant >= 9),
-                  "variant 0..11 (SwiGLU: 0, 8 or the split-release schedules 9..11)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int* q = dyn ? pf_queue(s) : nullptr;
-#define DLLM_PF_GO(MODE_, SCH_)                                                                               \
-  hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a,     \
-                     (const bf16*)b, (bf16*)c, M, N, K, q, (const int*)nullptr, (const int*)nullptr, 1)
-#define DLLM_PF_GO_DYN(MODE_, SCH_)                                                                           \
-  hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_, true>), dim3((unsigned)grid), dim3(256), 0, s,               \
-                     (const bf16*)a, (const bf16*)b, (bf16*)c, M, N, K, q, (const int*)nullptr, (const int*)nullptr, 1)
-  const bool nt_store = variant == 8 || (variant == 0 && (long)M * (N / 2) * 2 > (256L << 20));
-  DLLM_HOST_CHECK(dyn || variant <= 8, "the split-release schedules (9..11) run with the dynamic tile queue");
-  if (dyn) {
-    DLLM_HOST_CHECK(variant == 0 || variant == 8 || variant >= 9,
-                    "the dynamic tile queue runs the shipped schedule (0 / 8) or a split-release one (9..11)");
-    if (mode == 1) {
-      if (variant == 9) DLLM_PF_GO_DYN(2, 9);
-      else if (variant == 10) DLLM_PF_GO_DYN(2, 10);
-      else if (variant == 11) DLLM_PF_GO_DYN(2, 11);
-      else if (nt_store) DLLM_PF_GO_DYN(2, 8);
-      else DLLM_PF_GO_DYN(2, 0);
-    } else {
-      if (variant == 8) DLLM_PF_GO_DYN(0, 8);
-      else if (variant == 9) DLLM_PF_GO_DYN(0, 9);
-      else if (variant == 10) DLLM_PF_GO_DYN(0, 10);
-      else if (variant == 11) DLLM_PF_GO_DYN(0, 11);
-      else DLLM_PF_GO_DYN(0, 0);
-    }
-  } else if (mode == 1) {
-    // variant 8 forces the nontemporal stores; by default they go with outputs > 256 MiB
-    if (nt_store) DLLM_PF_GO(2, 8);
-    else DLLM_PF_GO(2, 0);
+#define DLLM_PF_GO(MODE_, SCH_, DYN_)                                                                         \
+  hipLaunchKernelGGL((gemm_pf_kernel<MODE_, SCH_, DYN_>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)a, \
+                     (const bf16*)b, (bf16*)c, M, N, K, q)
+  const bool nt_store = variant == 8 || (mode == 1 && (long)M * (N / 2) * 2 > (256L << 20));
+  if (mode == 1) {
+    if (dyn) { if (nt_store) DLLM_PF_GO(2, 8, true); else DLLM_PF_GO(2, 0, true); }
+    else { if (nt_store) DLLM_PF_GO(2, 8, false); else DLLM_PF_GO(2, 0, false); }
   } else {
-    switch (variant) {
-      case 1: DLLM_PF_GO(0, 1); break;
-      case 2: DLLM_PF_GO(0, 2); break;
-      case 3: DLLM_PF_GO(0, 3); break;
-      case 4: DLLM_PF_GO(0, 4); break;
-      case 5: DLLM_PF_GO(0, 5); break;
-      case 6: DLLM_PF_GO(0, 6); break;
-      case 7: DLLM_PF_GO(0, 7); break;
-      case 8: DLLM_PF_GO(0, 8); break;
-      default: DLLM_PF_GO(0, 0); break;
-    }
+    if (dyn) { if (nt_store) DLLM_PF_GO(0, 8, true); else DLLM_PF_GO(0, 0, true); }
+    else { if (nt_store) DLLM_PF_GO(0, 8, false); else DLLM_PF_GO(0, 0, false); }
   }
 #undef DLLM_PF_GO
-#undef DLLM_PF_GO_DYN
-  DLLM_HIP_CHECK(hipGetLastError());
-}
-
-// Persistent grouped-expert prefill GEMM (gemm_pf MOE): y [slots, N] (SwiGLU [slots, N / 2]) =
-// xs [slots, K] (expert-sorted: slot rows of expert e at [offsets[e], offsets[e] + counts[e]))
-// times W[e]^T ([E, N, K]; SwiGLU [E, 2I, K] = [Wg; Wu] per expert).  Dynamic tile queue,
-// 256 x 256 tiles, counts / offsets read on the device (expert parallelism: the local experts'
-// slices of the routing arrays; other experts' slot rows are left untouched).
-void gemm_pf_moe(uintptr_t y, uintptr_t xs, uintptr_t w, uintptr_t counts, uintptr_t offsets, int E, int N, int K,
-                 int slots, int mode, uintptr_t stream) {
-  DLLM_HOST_CHECK(E >= 1 && E <= 16, "1 <= experts <= 16");
-  DLLM_HOST_CHECK(K % PBK == 0 && K >= 2 * PBK, "K must be a multiple of 64, >= 128");
-  DLLM_HOST_CHECK(N % 256 == 0, "N must be a multiple of 256");
-  DLLM_HOST_CHECK(mode >= 0 && mode <= 15, "mode: bit 0 SwiGLU, bit 1 static tile walk, bits 2-3 row group 32 / 16");
-  DLLM_HOST_CHECK(slots >= 1, "slots");
-  DLLM_HOST_CHECK((long)slots * K * 2 < (1L << 32) && (long)E * N * K * 2 < (1L << 32) &&
-                      (long)slots * ((mode & 1) ? N / 2 : N) * 2 < (1L << 31),
-                  "operands must be < 4 GiB, the output < 2 GiB");
-  int dev = 0;
-  DLLM_HIP_CHECK(hipGetDevice(&dev));
-  int cus = 0;
-  DLLM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  if (cus <= 0) cus = 256;
-  const long bound = (long)(N / 256) * ((slots + 255) / 256 + E);     // tiles upper bound
-  const long grid = ((bound < cus ? bound : cus) + 7) / 8 * 8;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  // static walk (mode bit 1): w + i P over the tile space; the workgroups whose share is empty
-  // (the grid is sized from an upper bound of the tiles) return at once
-  int* q = (mode & 2) ? nullptr : pf_queue(s);
-#define DLLM_PFM_GO(MD, SC, DY)                                                                          \
-  hipLaunchKernelGGL((gemm_pf_kernel<MD, SC, DY, true>), dim3((unsigned)grid), dim3(256), 0, s, (const bf16*)xs, \
-                     (const bf16*)w, (bf16*)y, slots, N, K, q, (const int*)counts, (const int*)offsets, E)
-#define DLLM_PFM_SCH(SC)                          \
-  switch (mode & 3) {                             \
-    case 0: DLLM_PFM_GO(0, SC, true); break;      \
-    case 1: DLLM_PFM_GO(2, SC, true); break;      \
-    case 2: DLLM_PFM_GO(0, SC, false); break;     \
-    default: DLLM_PFM_GO(2, SC, false); break;    \
-  }
-  // row tiles per group of the tile order: 8 (schedule 0), 32 (12) or 16 (7)
-  if (mode & 4) {
-    DLLM_PFM_SCH(12)
-  } else if (mode & 8) {
-    DLLM_PFM_SCH(7)
-  } else {
-    DLLM_PFM_SCH(0)
-  }
-#undef DLLM_PFM_SCH
-#undef DLLM_PFM_GO
   DLLM_HIP_CHECK(hipGetLastError());
 }
 

@@ -451,21 +451,8 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
     const int q = total >> 3, r = total & 7, x = b & 7;
     b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
   }
-  // nsplit < 0: K-slice-major order -- an XCD's contiguous run covers one or two K slices of
-  // many column tiles (its L2 holds those slices of the activations and every line of them is
-  // shared by the run's column tiles) instead of every K slice of a few column tiles
-  const bool kmajor = nsplit < 0;
-  if (kmajor) nsplit = -nsplit;
   int m_t = b % mtiles, rest = b / mtiles;
-  int split, n_t;
-  if (kmajor) {
-    const int ng = total / (mtiles * nsplit);
-    n_t = rest % ng;
-    split = rest / ng;
-  } else {
-    split = rest % nsplit;
-    n_t = rest / nsplit;
-  }
+  int split = rest % nsplit, n_t = rest / nsplit;
   if constexpr ((VAR & 64) != 0) {          // prefill M, no K split (grouped_tile)
     grouped_tile(b, mtiles, ntiles, m_t, n_t);
     split = 0;
@@ -495,228 +482,8 @@ __global__ void __launch_bounds__(512, 1) gemm_wide_kernel(const bf16* __restric
   const bf16* pfB = B + (size_t)wide_b_row<SWIGLU>(16 * wv + (lane & 15), n_t, N / 2) * K + (size_t)kt0 * WBK;
   f32x4 acc[RT][4];
   wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, nt, acc, wv, lane, pfB, smem + NBUF * BUF);
-  if ((VAR & 8) && nsplit >= 0) return;
+  if (VAR & 8) return;
   wide_epilogue<BM, SPLIT, SWIGLU>(acc, C, P, M, N, m0, n_t, split, wm, wn, lane);
-}
-
-// ---- Stream-K form: unsplit decode grids that leave CUs idle ---------------------------------------
-// The 8B MLP gate|up at M <= 256 is 224 column tiles of 128 B-rows: 224 workgroups on 256 CUs, and
-// the kernel is bound per CU -- 192 / 224 / 256 workgroups of full tiles take the same time, 256
-// workgroups at 7/8 of the K loop take 14 % less (bench/debug/wide_cu_scaling.py,
-// profiles/round6_streamk.md).  Here P workgroups (one per CU) share the tiles x K-tiles work units
-// evenly: workgroup w owns units [w U / P, (w + 1) U / P).  At U / P < KT that is the END of one
-// tile, which w finishes (adds the partials of the tile's other segments, then the SwiGLU / bf16
-// epilogue), and the START of the next, which w publishes as an f32 partial for that tile's finisher.
-//  * the publishing segment runs first, so its partial is out long before the finisher (which
-//    computes its own segment meanwhile) needs it;
-//  * hand-off (guide Guideline 16, row 1 of the sc1 table): the partial is stored write-through
-//    (sc1 buffer stores, lane-linear 1 KiB wave pieces), every wave drains vmcnt(0), a workgroup
-//    barrier, then ONE lane sets the owner's flag (agent-scope atomic); the finisher polls that word
-//    relaxed from one lane (s_sleep between polls) and reads the partial with sc1 buffer loads only;
-//  * nothing waits on a workgroup that may not be resident: an owner CLAIMS its segment (flag CAS
-//    untouched -> claimed) before computing it, and a finisher that finds a flag untouched claims
-//    the segment itself (-> stolen) and computes it in its own registers.  A finisher waits only on
-//    a claimed segment, whose owner is running and waits on nothing.  Every poll loop also has a
-//    wall-clock deadline that sets an error word (ctl[2]) instead of hanging;
-//  * deterministic: partials are added in a fixed order, a stolen segment is computed by the same
-//    code from a zero accumulator and combined with the same single commutative f32 add, so the
-//    output is bit-identical whichever workgroup computed which segment;
-//  * flag = epoch << 2 | state (1 claimed, 2 published, 3 stolen); the epoch lives in ctl[0] on the
-//    device and the last workgroup to retire advances it, so there is no per-call memset and a graph
-//    replay sees a fresh epoch every time.  One control block per stream (ops/gemm.py).
-// test & 1 (tests only): odd workgroups skip their publishing segment, so finishers steal it;
-// test & 2 (timing ablation, wrong results): no partial stores / loads, flags only.
-template <int BM, bool SWIGLU, int NBUF, int VAR>
-__global__ void __launch_bounds__(512, 1) gemm_wide_sk_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                              bf16* __restrict__ C, float* __restrict__ part,
-                                                              unsigned* __restrict__ sk, int M, int N, int K,
-                                                              int test) {
-  constexpr int AEL = BM * WBK, BEL = WBN * WBK, BUF = AEL + BEL;   // bf16 elements
-  constexpr int AI = BM / 64, BI = 2, RT = BM / 64, NF = RT * 4;
-  constexpr int PSZ = BM * WBN;                                      // floats per partial tile
-  static_assert(PSZ == 512 * NF * 4, "partial layout: every thread's accumulators, lane-linear");
-  static_assert(NBUF >= 3 && (NBUF * BUF + 64) * 2 <= 160 * 1024, "LDS");
-  // ring + 128 bytes of broadcast words in ONE __shared__ array (guide §5 trap 4a)
-  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * BUF + 64];
-  unsigned* bc = reinterpret_cast<unsigned*>(smem + NBUF * BUF);
-  typedef unsigned u32x4w __attribute__((ext_vector_type(4)));
-  constexpr int RLX = __ATOMIC_RELAXED, AG = __HIP_MEMORY_SCOPE_AGENT;
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
-  const int P = gridDim.x, w = blockIdx.x;
-  const int KT = K / WBK;
-  const int mtiles = (M + BM - 1) / BM;
-  const int ntiles = SWIGLU ? (N / 2) / 64 : N / WBN;
-  const long U = (long)mtiles * ntiles * KT;
-  // [0] epoch, [1] retired workgroups, [2] error: a poll hit its deadline; [3] segments stolen
-  // (diagnostics, never reset)
-  unsigned* ctl = sk;
-  unsigned* flags = sk + 64;     // one word per workgroup (its publishing segment)
-  auto ubeg = [&](int x) { return (long)x * U / P; };
-
-  if (tid == 0) bc[0] = __hip_atomic_load(ctl, RLX, AG) & 0x3fffffffu;
-  __syncthreads();
-  const unsigned e = __builtin_amdgcn_readfirstlane(bc[0]);
-
-  f32x4 acc[RT][4];
-  // this workgroup's accumulators over K-tiles [k0, k1) of tile t (acc zeroed by the main loop)
-  auto run = [&](int t, int k0, int k1) {
-    const int m0 = (t % mtiles) * BM, n_t = t / mtiles;
-    const bf16* srcA[AI];
-    const bf16* srcB[BI];
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-      const int r = 8 * (wv * AI + j) + (lane >> 3);
-      srcA[j] = A + (size_t)min(m0 + r, M - 1) * K + (size_t)k0 * WBK + wswz(r, lane & 7) * 8;
-    }
-#pragma unroll
-    for (int j = 0; j < BI; ++j) {
-      const int r = 8 * (wv * BI + j) + (lane >> 3);
-      srcB[j] = B + (size_t)wide_b_row<SWIGLU>(r, n_t, N / 2) * K + (size_t)k0 * WBK + wswz(r, lane & 7) * 8;
-    }
-    __syncthreads();             // every wave is past the previous segment's LDS reads: the ring restarts
-    wide_mainloop<BM, NBUF, VAR>(smem, srcA, srcB, k1 - k0, acc, wv, lane);
-  };
-  auto rsrc = [&](float* base) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, PSZ * 4, 0x00020000);
-  };
-  // acc -> partial (sc1: write-through, no release fence needed) / partial -> acc += (sc1 loads)
-  auto store_part = [&](float* base) {
-    const __amdgpu_buffer_rsrc_t rs = rsrc(base);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const f32x4 v = acc[rt][ct];
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4w*>(&v), rs,
-                                               ((rt * 4 + ct) * 512 + tid) * 16, 0, 16);
-      }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave drains before the flag
-  };
-  auto add_part = [&](float* base) {
-    const __amdgpu_buffer_rsrc_t rs = rsrc(base);
-    u32x4w v[NF];
-#pragma unroll
-    for (int f = 0; f < NF; ++f) v[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, (f * 512 + tid) * 16, 0, 16);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) acc[rt][ct] += *reinterpret_cast<const f32x4*>(&v[rt * 4 + ct]);
-  };
-
-  const long u0 = ubeg(w), u1 = ubeg(w + 1);
-  // One main-loop call site (a second inlined copy cost ~100 VGPRs and spills at BM = 256): a small
-  // state machine picks the segment to run next.
-  //   stage 0: the publishing segment -- the start (or a middle piece) of the last tile this
-  //            workgroup touches, when its range ends inside that tile;
-  //   stage 1: the own segment of the next tile whose end lies in (u0, u1] (a full tile, or the end
-  //            segment of a tile whose other segments belong to workgroups w - 1, w - 2, ...);
-  //   stage 2: a contributor's segment stolen by this finisher.
-  const int tl = u1 > u0 ? (int)((u1 - 1) / KT) : 0;
-  const bool pub = u1 > u0 && u1 < (long)(tl + 1) * KT && !((test & 1) && (w & 1));
-  int stage = pub ? 0 : 1;
-  int t = (int)(u0 / KT);        // next tile to finish
-  int c = -1;                    // contributor being resolved (stage 2: the stolen one)
-  for (;;) {
-    const long ts = (long)t * KT;
-    int jt, j0, j1;
-    if (stage == 0) {
-      if (tid == 0) {
-        unsigned cur = __hip_atomic_load(flags + w, RLX, AG);
-        unsigned ok = 0;
-        if ((cur >> 2) != e || (cur & 3u) == 0)
-          ok = __hip_atomic_compare_exchange_strong(flags + w, &cur, (e << 2) | 1u, RLX, RLX, AG) ? 1u : 0u;
-        bc[1] = ok;
-      }
-      __syncthreads();
-      if (!bc[1]) {              // its finisher has stolen it already
-        stage = 1;
-        continue;
-      }
-      const long pts = (long)tl * KT;
-      jt = tl;
-      j0 = (int)((u0 > pts ? u0 : pts) - pts);
-      j1 = (int)(u1 - pts);
-    } else if (stage == 1) {
-      if ((long)(t + 1) * KT > u1) break;
-      jt = t;
-      j0 = (int)((u0 > ts ? u0 : ts) - ts);
-      j1 = KT;
-    } else {
-      jt = t;
-      j0 = (int)((ubeg(c) > ts ? ubeg(c) : ts) - ts);
-      j1 = (int)(ubeg(c + 1) - ts);
-    }
-    run(jt, j0, j1);
-    if (stage == 0) {
-      if (!(test & 2)) store_part(part + (size_t)w * PSZ);
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(flags + w, (e << 2) | 2u, RLX, AG);
-      stage = 1;
-      continue;
-    }
-    float* scr = part + (size_t)(P + w) * PSZ;
-    if (stage == 2) {
-      add_part(scr);             // stolen segment + own sum so far: one commutative add
-      --c;
-    } else {
-      c = w - 1;
-    }
-    bool stole = false;
-    for (; c >= 0 && ubeg(c + 1) > ts; --c) {
-      if (tid == 0) {
-        unsigned st = 0;
-        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() + 20000000ull;   // 200 ms (100 MHz)
-        for (;;) {
-          unsigned cur = __hip_atomic_load(flags + c, RLX, AG);
-          const bool now = (cur >> 2) == e && (cur & 3u) != 0;
-          if (now && (cur & 3u) == 2u) { st = 2; break; }                       // published
-          if (!now) {                                                           // untouched: steal it
-            if (__hip_atomic_compare_exchange_strong(flags + c, &cur, (e << 2) | 3u, RLX, RLX, AG)) {
-              __hip_atomic_fetch_add(ctl + 3, 1u, RLX, AG);                      // diagnostics: steals
-              st = 3;
-              break;
-            }
-            continue;
-          }
-          if ((cur & 3u) == 3u || __builtin_amdgcn_s_memrealtime() > t_end) {   // (never: one finisher per segment)
-            __hip_atomic_store(ctl + 2, 1u, RLX, AG);
-            st = 4;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);                                          // claimed: its owner is running
-        }
-        bc[2] = st;
-      }
-      __syncthreads();
-      const unsigned st = bc[2];
-      __syncthreads();           // every wave has read bc[2] before the next contributor's poll rewrites it
-      if (st == 2) {
-        if (!(test & 2)) add_part(part + (size_t)c * PSZ);
-      } else if (st == 3) {
-        store_part(scr);         // own sum so far -> scratch; the stolen segment runs from a zero accumulator
-        stole = true;
-        break;
-      }
-    }
-    if (stole) {
-      stage = 2;
-      continue;
-    }
-    wide_epilogue<BM, false, SWIGLU>(acc, C, nullptr, M, N, (t % mtiles) * BM, t / mtiles, 0, wm, wn, lane);
-    ++t;
-    stage = 1;
-  }
-  // ---- 3. retire; the last workgroup resets the count and advances the epoch
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned n = __hip_atomic_fetch_add(ctl + 1, 1u, RLX, AG);
-    if (n == (unsigned)P - 1) {
-      __hip_atomic_store(ctl + 1, 0u, RLX, AG);
-      __hip_atomic_store(ctl, (e + 1) & 0x3fffffffu, RLX, AG);
-    }
-  }
 }
 
 // FP8 (W8A8) variant: A [M, K] and B [N, K] OCP e4m3 bytes, per-row scales sa [M] (dynamic,
@@ -922,9 +689,6 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   const bool swiglu = mode == 1;
   DLLM_HOST_CHECK(swiglu ? (N % 128 == 0) : (N % WBN == 0), "N must be a multiple of 128");
   DLLM_HOST_CHECK(splits >= 1, "splits >= 1");
-  // variant bit 20: K-slice-major workgroup order (gemm_wide_kernel kmajor)
-  const bool kmajor = (variant & (1 << 20)) != 0;
-  variant &= ~(1 << 20);
   // variant bits 8..: optional row tile override (64 / 128 / 192 / 256), 0 = wide_bm(M)
   const int bm_force = variant >> 8;
   variant &= 0xff;
@@ -957,7 +721,7 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   else if (variant == 4) variant = 1;
 #define DLLM_WIDE_GO3(BM_, SPLIT_, SW_, V_)                                                                      \
   hipLaunchKernelGGL((gemm_wide_kernel<BM_, SPLIT_, SW_, 3, V_>), dim3((unsigned)grid), dim3(512), 0, s,          \
-                     (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, kmajor && S > 1 ? -S : S)
+                     (const bf16*)a, (const bf16*)b, (bf16*)c, (float*)ws, M, N, K, kts, S)
 #define DLLM_WIDE_GO(BM_, SPLIT_, SW_)                                                                          \
   do {                                                                                                         \
     if (abl == 8) { if (variant == 2) DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 10); else DLLM_WIDE_GO3(BM_, SPLIT_, SW_, 9); } \
@@ -989,36 +753,6 @@ int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_float
   if (mode == 2) return S;
   splitk_reduce_ex(c, ws, 0, S, M, N, swiglu ? 1 : 0, stream);
   return S;
-}
-
-// Stream-K launch of the unsplit wide kernel (gemm_wide_sk_kernel): mode 0 = C = A B^T, 1 = SwiGLU.
-// P workgroups (one per CU available); part: >= 2 P partial tiles of BM x 128 floats (published
-// partials + each finisher's scratch); sk: the stream's control block, >= 64 + P words, zeroed once
-// when allocated (the kernel keeps it consistent across calls).  Returns the row tile BM.
-int gemm_wide_sk(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t part, long part_floats, uintptr_t sk, long sk_words,
-                 int M, int N, int K, int mode, int P, int test, uintptr_t stream) {
-  DLLM_HOST_CHECK(M >= 1 && M <= 256, "stream-K wide GEMM: 1 <= M <= 256 (one row tile)");
-  DLLM_HOST_CHECK(K % WBK == 0 && K >= WBK, "K must be a positive multiple of 64");
-  DLLM_HOST_CHECK(mode == 0 || mode == 1, "mode 0 (plain) or 1 (SwiGLU)");
-  DLLM_HOST_CHECK(N % 128 == 0, "N must be a multiple of 128");
-  DLLM_HOST_CHECK(P >= 1 && P <= 4096, "grid");
-  const bool swiglu = mode == 1;
-  const int BM = wide_bm(M);
-  const long U = (long)(swiglu ? (N / 2) / 64 : N / WBN) * (K / WBK);
-  DLLM_HOST_CHECK(U >= 2L * P, "stream-K needs at least two K-tiles of work per workgroup");
-  DLLM_HOST_CHECK(sk != 0 && sk_words >= 64L + P, "stream-K control block too small");
-  DLLM_HOST_CHECK(part != 0 && part_floats >= 2L * P * BM * WBN, "stream-K partial workspace too small");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-#define DLLM_WSK(BM_, SW_)                                                                                        \
-  hipLaunchKernelGGL((gemm_wide_sk_kernel<BM_, SW_, 3, 34>), dim3((unsigned)P), dim3(512), 0, s, (const bf16*)a,     \
-                     (const bf16*)b, (bf16*)c, (float*)part, (unsigned*)sk, M, N, K, test)
-  if (BM == 64) { if (swiglu) DLLM_WSK(64, true); else DLLM_WSK(64, false); }
-  else if (BM == 128) { if (swiglu) DLLM_WSK(128, true); else DLLM_WSK(128, false); }
-  else if (BM == 192) { if (swiglu) DLLM_WSK(192, true); else DLLM_WSK(192, false); }
-  else { if (swiglu) DLLM_WSK(256, true); else DLLM_WSK(256, false); }
-#undef DLLM_WSK
-  DLLM_HIP_CHECK(hipGetLastError());
-  return BM;
 }
 
 // FP8 W8A8 wide GEMM: modes as gemm_wide; K in elements (= bytes), multiple of 128.

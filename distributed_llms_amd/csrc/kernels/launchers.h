@@ -29,8 +29,6 @@ void splitk_reduce_ex(uintptr_t out, uintptr_t ws, uintptr_t bias, int S, int M,
                       uintptr_t stream);
 int gemm_wide(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
               int mode, int variant, uintptr_t stream);
-int gemm_wide_sk(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t part, long part_floats, uintptr_t sk, long sk_words,
-                 int M, int N, int K, int mode, int P, int test, uintptr_t stream);
 int gemm_wide_fp8(uintptr_t c, uintptr_t a, uintptr_t a_scale, uintptr_t b, uintptr_t b_scale, uintptr_t ws,
                   long ws_floats, int M, int N, int K, int splits, int mode, int variant, uintptr_t stream);
 void quant_fp8_rows(uintptr_t q, uintptr_t scale, uintptr_t x, int M, int K, uintptr_t stream);
@@ -39,8 +37,6 @@ int gemm_pp(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats,
 void gemm_pp_moe(uintptr_t y, uintptr_t x, uintptr_t gather, uintptr_t w, uintptr_t counts, uintptr_t offsets, int E,
                  int N, int K, int xrows, int slots, int mode, uintptr_t stream);
 void gemm_pf(uintptr_t c, uintptr_t a, uintptr_t b, int M, int N, int K, int mode, int variant, uintptr_t stream);
-void gemm_pf_moe(uintptr_t y, uintptr_t xs, uintptr_t w, uintptr_t counts, uintptr_t offsets, int E, int N, int K,
-                 int slots, int mode, uintptr_t stream);
 int gemm_sq(uintptr_t c, uintptr_t a, uintptr_t b, uintptr_t ws, long ws_floats, int M, int N, int K, int splits,
             int mode, int variant, uintptr_t stream);
 

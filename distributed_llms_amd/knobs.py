@@ -35,7 +35,7 @@ class Knobs:
     # lgkmcnt per MFMA row) and for split-K grids (1); in-engine A/B 27,123 vs 27,014 / 26,896 tok/s
     wide_variant: int = 33
     wide_variant_split: int = 1
-    wide_gate_up_max_m: int = 256     # SwiGLU-fused gate|up on gemm_wide up to this M (then hipBLASLt)
+    wide_gate_up_max_m: int = 256     # SwiGLU-fused gate|up on gemm_wide up to this M (then split-K gemm_pp / gemm_pf)
     wide_down_max_m: int = 384        # MLP down (K >= 8192, K > N) up to this M (512: split gemm_pp 59 vs 66 us)
     wide_proj_max_m: int = 256        # qkv / LM head up to this M (o: wide_o_max_m; down: wide_down_max_m)
     wide_target_wgs: int = 256        # split-K: about one workgroup per CU
@@ -69,9 +69,6 @@ class Knobs:
     # (ops/gemm.reserve_cus_for_comm).  Alone on the GPU the static walk is 0.3 % faster end to end
     # (TTFT 343 vs 346 ms, two interleaved pairs, gpurun_out/r5j_bench.log)
     pf_dynamic: str = "auto"
-    # gemm_pf main-loop schedule for prefill projections: 0 = the shipped schedule 2 (pieces every 5
-    # MFMAs after one mid-K-tile barrier); 9..11 = A / B LDS regions released separately
-    pf_schedule: int = 0
     # decode LM head (N > 65536) at pp_head_min_m <= M <= 256 on gemm_pp schedule 2 with nontemporal
     # weights: 230 vs 265 us for gemm_sq at M = 256 (Llama-3-8B); 0 = off
     pp_head_min_m: int = 225
@@ -80,7 +77,7 @@ class Knobs:
     head_beside_comm: str = "sq"
     # ---- attention (ops/__init__.py)
     attn_target_waves: int = 1024     # decode split-KV: waves to aim for (profiles/attn_decode_sweep.txt)
-    prefill_attn: int = 4             # prefill kernel version 1..5 (4: LDS-shared K/V tiles)
+    prefill_attn: int = 4             # prefill kernel: 4 = LDS-shared K/V tiles, 3 = register-tiled (> 32k fallback)
     # prefill q-RoPE in the attention kernel's q load (rope_cache appends K / V only): no rotated-q
     # round trip through HBM (268 MB per layer at T = 32768)
     prefill_fused_rope: bool = True
@@ -111,23 +108,11 @@ class Knobs:
     moe_variant: int = 0
     moe_wide_min_pairs: int = 8       # token-expert pairs per expert from which the tiled GEMM serves
     moe_fused_router: bool = True
-    # prefill grouped expert GEMMs on the persistent gemm_pf (MOE form) instead of gemm_pp_moe: off --
-    # measured slower in-engine (Mixtral B = 256: TTFT 742 vs 689 ms, 10,070 vs 10,272 tok/s; gate|up
-    # 13.3 ms per layer vs gemm_pp_moe's 11.6, gpurun_out/r5d_mixtral*.txt)
-    moe_persistent: bool = False
     # prefill V append eight tokens per workgroup, 16-byte stores into the transposed V cache
     # (norm_elementwise.hip v_group_kernel); False = the per-token 2-byte scatter.
     v_group_append: bool = True
-    # split-K gemm_wide grids in K-slice-major workgroup order (an XCD's run shares K slices)
-    wide_kmajor: bool = False
     # grouped expert GEMM ring depth: 6 / 5 LDS slots at 64 / 128-row tiles (False: 3 slots)
     moe_deep_ring: bool = True
-    # unsplit gemm_wide grids with fewer column tiles than CUs (the 8B gate|up: 224 tiles on 256 CUs)
-    # run stream-K: every CU takes an equal share of tiles x K-tiles, partial tiles handed over in the
-    # launch (gemm_wide.hip gemm_wide_sk_kernel; profiles/round6_streamk.md).  wide_streamk_max_fill:
-    # only while tiles / CUs is below this (a nearly full grid has nothing to gain)
-    wide_streamk: bool = False
-    wide_streamk_max_fill: float = 0.94
     # ---- FP8 W8A8 (ops/quant.py)
     fp8_bm128: bool = True
     fp8_group_m: int = 4096

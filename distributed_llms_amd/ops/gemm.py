@@ -224,52 +224,6 @@ def wide_splits(m: int, n: int, k: int, swiglu: bool = False, target_wgs: int = 
     return max(1, min(s, (k // 64) // 8, 16))
 
 
-_sk = {}
-
-
-def _sk_block(device: torch.device) -> torch.Tensor:
-    """The stream-K control block of the current stream (epoch, retire count, error word, one flag
-    per workgroup): zeroed once here, kept consistent by the kernel itself across calls and graph
-    replays (csrc/kernels/gemm_wide.hip gemm_wide_sk_kernel).  One per stream, like the split-K
-    workspace: launches on one stream never overlap."""
-    key = (device.index or 0, torch.cuda.current_stream().cuda_stream)
-    t = _sk.get(key)
-    if t is None:
-        t = _sk[key] = torch.zeros(64 + 4096, dtype=torch.int32, device=device)
-    return t
-
-
-def streamk_grid(m: int, n: int, k: int, swiglu: bool, device) -> int:
-    """Workgroups for a stream-K gemm_wide launch (0: not eligible).  Unsplit grids only (one row
-    tile, M <= 256) whose column tiles leave CUs idle: every CU not reserved for communication then
-    takes an equal share of the tiles x K-tiles (knobs.wide_streamk)."""
-    kn = knobs.K
-    if not kn.wide_streamk or m > 256 or n % 128 or k % 64:
-        return 0
-    tiles = (n // 2) // 64 if swiglu else n // 128
-    p = _cus(device) - _comm_cus
-    if p < 2 or tiles >= kn.wide_streamk_max_fill * p or 2 * tiles < p or tiles * (k // 64) < 2 * p:
-        return 0
-    return p
-
-
-def linear_wide_sk(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, grid: int = 0, test: int = 0):
-    """Stream-K form of the unsplit wide GEMM (see :func:`streamk_grid`): y = x w^T, or the fused
-    SwiGLU (``w`` = [Wg; Wu], y [M, N / 2]).  ``test`` & 1: odd workgroups leave their partial
-    segment to the finisher (tests the stealing path)."""
-    k = x.shape[-1]
-    n = w.shape[0]
-    m = x.numel() // k
-    p = grid or streamk_grid(m, n, k, swiglu, x.device) or _cus(x.device)
-    y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
-    ws = _workspace(x.device)
-    sk = _sk_block(x.device)
-    _ext.kernels().gemm_wide_sk(y.data_ptr(), x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), sk.data_ptr(),
-                                sk.numel(), m, n, k, 1 if swiglu else 0, p, test,
-                                torch.cuda.current_stream().cuda_stream)
-    return y
-
-
 def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = False, defer: bool = False,
                 variant: int = -1):
     """Wide-M decode GEMM (csrc/kernels/gemm_wide.hip): 256 x 128 x 64 tiles, 3-deep LDS-DMA pipeline,
@@ -285,10 +239,6 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     if n % 128 or k % 64:
         raise ValueError("linear_wide: N % 128 and K % 64")
     s = splits or wide_splits(m, n, k, swiglu)
-    if s == 1 and not splits and variant < 0 and x.is_cuda:
-        p = streamk_grid(m, n, k, swiglu, x.device)
-        if p:
-            return linear_wide_sk(x, w, swiglu=swiglu, grid=p)
     ws = _workspace(x.device)
     if s > 1 and s * m * n > ws.numel():
         s = max(1, ws.numel() // (m * n))
@@ -297,8 +247,6 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     bm = wide_row_tile(m, n, k, swiglu)
     if bm != wide_bm(m):
         v |= bm << 8
-    if s > 1 and knobs.K.wide_kmajor:
-        v |= 1 << 20
     if defer and not swiglu and s > 1:
         se = _ext.kernels().gemm_wide(0, x.data_ptr(), w.data_ptr(), ws.data_ptr(), ws.numel(), m, n, k, s, 2, v, stream)
         return SplitKPartial(ws, se, m, n, (*x.shape[:-1], n), x.dtype, x.device)
@@ -347,9 +295,9 @@ def linear_pp(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool = 
 def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, variant: int = 0) -> torch.Tensor:
     """Persistent prefill GEMM (gemm_pf in csrc/kernels/gemm_pp.hip): schedule 2's 256 x 256 tiles,
     one workgroup per CU walking its tiles with the LDS-DMA pipeline running across tile
-    boundaries; optional fused SwiGLU (``w`` = [Wg; Wu], y [M, N / 2]).  ``variant`` 1-7: schedule
-    variants of the plain form for sweeps (csrc/kernels/gemm_pp.hip pf_sched); the tiles come from
-    per-XCD device queues unless knobs.pf_dynamic is off (bit 16 of the launcher's variant)."""
+    boundaries; optional fused SwiGLU (``w`` = [Wg; Wu], y [M, N / 2]).  ``variant`` 8: nontemporal
+    output stores (the default for SwiGLU outputs > 256 MiB); the tiles come from per-XCD device
+    queues while knobs.pf_dynamic says so (bit 16 of the launcher's variant)."""
     k = x.shape[-1]
     n = w.shape[0]
     m = x.numel() // k
@@ -358,18 +306,13 @@ def linear_pf(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, variant: i
     if n % 256 or k % 64:
         raise ValueError("linear_pf: N % 256 and K % 64")
     y = torch.empty(*x.shape[:-1], n // 2 if swiglu else n, dtype=x.dtype, device=x.device)
-    if variant == 0 and knobs.K.pf_schedule:
-        variant = knobs.K.pf_schedule  # split-release schedules 9..11 (gemm_pp.hip pf_sched)
-    # the split-release schedules 9..11 exist only in the dynamic-queue form
-    dyn = (pf_dynamic() or variant >= 9) and k >= 128
+    dyn = pf_dynamic() and k >= 128
     if torch.cuda.is_current_stream_capturing():
         # inside a graph: the static tile walk.  A tile queue is per stream and self-resetting, but
         # a replay may run on another stream beside eager launches that use the same queue
         dyn = False
-    if dyn and (variant in (0, 8) or variant >= 9):
+    if dyn:
         variant |= 16                  # per-XCD dynamic tile queues (gemm_pp.hip, DYN)
-    elif variant >= 9:
-        variant = 0
     _ext.kernels().gemm_pf(y.data_ptr(), x.data_ptr(), w.data_ptr(), m, n, k, 1 if swiglu else 0, variant,
                            torch.cuda.current_stream().cuda_stream)
     return y

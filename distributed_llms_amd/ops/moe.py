@@ -126,25 +126,10 @@ def forward(x: torch.Tensor, w_router: torch.Tensor, w_gate_up: torch.Tensor, w_
         # addresses each A operand with 32-bit buffer offsets: larger batches take the per-expert path)
         slots = t * top_k
         act = torch.empty(slots, inter, dtype=x.dtype, device=dev)
-        if knobs.K.moe_persistent and e_loc <= 16 and h >= 128 and inter >= 128:
-            # persistent form (gemm_pf MOE: LDS-DMA ring continuous across tiles; tile queue per knobs.pf_dynamic):
-            # the token rows gathered into slot order first (the embedding kernel is a row gather)
-            from . import embedding
-            from .gemm import pf_dynamic
-            # mode bit 1: the static tile walk (knobs.pf_dynamic off, and always inside a graph
-            # capture -- as linear_pf: a tile queue is per stream, and a replay may run beside eager
-            # launches that use the same queue; pf_queue() also refuses to create one mid-capture)
-            walk = 0 if (pf_dynamic() and not torch.cuda.is_current_stream_capturing()) else 2
-            xs = embedding(sorted_tok, x)
-            k.gemm_pf_moe(act.data_ptr(), xs.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p, e_loc, two_i, h, slots,
-                          1 | walk, st)
-            k.gemm_pf_moe(ys.data_ptr(), act.data_ptr(), w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, slots, walk,
-                          st)
-        else:
-            k.gemm_pp_moe(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p,
-                          e_loc, two_i, h, t, slots, 1, st)
-            k.gemm_pp_moe(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, slots,
-                          slots, 0, st)
+        k.gemm_pp_moe(act.data_ptr(), x.data_ptr(), sorted_tok.data_ptr(), w_gate_up.data_ptr(), cnt_p, off_p,
+                      e_loc, two_i, h, t, slots, 1, st)
+        k.gemm_pp_moe(ys.data_ptr(), act.data_ptr(), 0, w_down.data_ptr(), cnt_p, off_p, e_loc, h, inter, slots,
+                      slots, 0, st)
     else:
         # odd expert dims (test-size models): per-expert GEMMs, counts read on the host
         xs = x.index_select(0, sorted_tok.long())

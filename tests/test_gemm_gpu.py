@@ -142,26 +142,6 @@ def test_wide_l2_prefetch_bit_exact(cuda, m, n, k, splits, swiglu):
         assert torch.equal(a, b), v
 
 
-@pytest.mark.parametrize("m,n,k,splits", [(256, 6144, 4096, 5), (256, 4096, 14336, 8), (256, 4096, 4096, 8),
-                                          (300, 4096, 4096, 4), (64, 1024, 512, 3), (1, 2048, 1024, 2)])
-def test_wide_kmajor_order_bit_exact(cuda, m, n, k, splits):
-    """Variant bit 20 (K-slice-major workgroup order on split-K grids) only moves workgroups between
-    XCDs: every (row tile, column tile, K slice) runs the same MFMAs into the same slab, so the
-    reduced and the deferred outputs are bit-identical to the default order."""
-    x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    for v in (1, 33):
-        a = gemm.linear_wide(x, w, splits=splits, variant=v)
-        b = gemm.linear_wide(x, w, splits=splits, variant=v | (1 << 20))
-        assert torch.equal(a, b), v
-    ref = (x.float() @ w.float().t())
-    torch.testing.assert_close(b.float(), ref, atol=5e-2, rtol=5e-2)
-    from distributed_llms_amd import knobs
-    with knobs.override(wide_kmajor=True):
-        pa = gemm.linear_wide(x, w, splits=splits, defer=True)
-        pb = pa.materialize() if hasattr(pa, "materialize") else pa
-    assert torch.equal(pb, gemm.linear_wide(x, w, splits=splits))
-
-
 @pytest.mark.parametrize("m,n,k,swiglu", [(4500, 1024, 512, False), (5000, 2048, 256, True), (2048, 256, 128, False)])
 def test_wide_grouped_tile_order_bit_exact(cuda, m, n, k, swiglu):
     """Variant bit 64 (grouped row-tile order for prefill M) only reorders the workgroups: every
@@ -338,14 +318,6 @@ def test_pf_swiglu(cuda, m, inter, k):
     torch.testing.assert_close(y.float(), ref, atol=6e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("variant", range(1, 9))
-def test_pf_schedule_variants_bit_exact(cuda, variant):
-    """The schedule variants (bench sweeps) only move barriers, staging slots, the tile order and
-    the stores' cache policy (8: nontemporal): same K order per output, same bits."""
-    x, w = _bf(2100, 1024), _bf(2048, 1024, scale=0.05)
-    assert torch.equal(gemm.linear_pf(x, w, variant=variant), gemm.linear_pf(x, w))
-
-
 @pytest.mark.parametrize("m", [256, 2100])
 def test_pf_swiglu_nontemporal_stores_bit_exact(cuda, m):
     """SwiGLU with the nontemporal output stores (variant 8; the default above 256 MiB of output):
@@ -412,78 +384,3 @@ def test_pp_graph_replay_and_determinism(cuda):
         g.replay()
     torch.cuda.synchronize()
     assert torch.equal(y, y0)
-
-
-@pytest.mark.parametrize("sched", [9, 10, 11])
-def test_pf_split_release_schedules_bit_exact(cuda, sched):
-    """gemm_pf schedules 9-11 (A / B LDS regions released separately, pieces spread over more
-    MFMAs) change only when the staging loads are issued: same bits as the shipped schedule, plain
-    and SwiGLU, ragged M (knobs.pf_schedule)."""
-    from distributed_llms_amd import knobs
-    x, w = _bf(3000, 4096), _bf(6144, 4096, scale=0.05)
-    xs, ws = _bf(1000, 1024), _bf(2 * 1536, 1024, scale=0.05)
-    with knobs.override(pf_schedule=0):
-        ref, ref_s = gemm.linear_pf(x, w), gemm.linear_pf(xs, ws, swiglu=True, variant=0)
-    with knobs.override(pf_schedule=sched):
-        assert torch.equal(gemm.linear_pf(x, w), ref)
-        assert torch.equal(gemm.linear_pf(xs, ws, swiglu=True), ref_s)
-
-
-# ---- stream-K gemm_wide (knobs.wide_streamk; csrc/kernels/gemm_wide.hip gemm_wide_sk_kernel)
-@pytest.mark.parametrize("m", [1, 37, 64, 128, 200, 256])
-@pytest.mark.parametrize("n,k,swiglu,grid", [(28672, 4096, True, 256), (28672, 4096, True, 240),
-                                             (2048, 1024, True, 20), (4096, 2048, False, 37),
-                                             (3072, 512, False, 29)])
-def test_streamk_wide_matches_fp32(cuda, m, n, k, swiglu, grid):
-    """Every CU takes an equal share of tiles x K-tiles; tiles split between workgroups are
-    finished by the workgroup holding their end, which adds the others' published partials.  Grids
-    that put one, two or three segments in a tile, every row tile (64 / 128 / 192 / 256), SwiGLU
-    and plain."""
-    x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    y = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)
-    r = x.float() @ w.float().t()
-    if swiglu:
-        r = F.silu(r[:, : n // 2]) * r[:, n // 2:]
-    torch.testing.assert_close(y.float(), r, atol=3e-2, rtol=3e-2)
-    assert int(gemm._sk_block(x.device)[2]) == 0, "a stream-K poll hit its deadline"
-
-
-@pytest.mark.parametrize("m,n,k,swiglu,grid", [(256, 28672, 4096, True, 256), (128, 28672, 4096, True, 250),
-                                               (64, 4096, 2048, False, 37), (200, 3072, 512, False, 29)])
-def test_streamk_steal_and_replay_bit_exact(cuda, m, n, k, swiglu, grid):
-    """Deterministic whoever computes a segment: odd workgroups leaving their partial to the
-    finisher (which then computes it itself) give bit-identical outputs; so do repeated calls (the
-    epoch advances each time, no memset) and a HIP-graph replay."""
-    x, w = _bf(m, k), _bf(n, k, scale=0.05)
-    sk = gemm._sk_block(x.device)
-    e0 = int(sk[0])
-    a = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)
-    b = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid, test=1)
-    c = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b) and torch.equal(a, c)
-    assert int(sk[0]) == e0 + 3 and int(sk[1]) == 0 and int(sk[2]) == 0
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)      # warm the capture stream's blocks
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            out = gemm.linear_wide_sk(x, w, swiglu=swiglu, grid=grid)
-    for _ in range(3):
-        out.zero_()
-        g.replay()
-        torch.cuda.synchronize()
-        assert torch.equal(out, a)
-
-
-def test_streamk_dispatch_for_the_8b_gate_up(cuda):
-    """With knobs.wide_streamk the M <= 256 8B gate|up (224 column tiles) runs stream-K over every CU
-    through the default dispatch, and agrees with the unsplit kernel to bf16 rounding."""
-    from distributed_llms_amd import knobs
-    x, w = _bf(256, 4096), _bf(28672, 4096, scale=0.05)
-    base = gemm.linear_wide(x, w, swiglu=True)
-    with knobs.override(wide_streamk=True):
-        assert gemm.streamk_grid(256, 28672, 4096, True, x.device) == torch.cuda.get_device_properties(0).multi_processor_count
-        y = gemm.linear_swiglu(x, w)
-    torch.testing.assert_close(y.float(), base.float(), atol=2e-2, rtol=2e-2)

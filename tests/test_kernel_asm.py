@@ -42,8 +42,8 @@ def test_pf_persistent_kernel_keeps_the_pipeline_full(pp_asm):
         assert scratch == 0, (name, scratch)
         assert "scratch_" not in body
         lines = body.split("\n")
-        # template <MODE, SCH, DYN, MOE> mangles as ILi<MODE>ELi<SCH>ELb<DYN>ELb<MOE>E
-        m = re.search(r"gemm_pf_kernelILi\d+ELi\d+ELb(\d)ELb(\d)E", name)
+        # template <MODE, SCH, DYN> mangles as ILi<MODE>ELi<SCH>ELb<DYN>E
+        m = re.search(r"gemm_pf_kernelILi\d+ELi\d+ELb(\d)E", name)
         dyn = bool(m and m.group(1) == "1")
         # vmcnt(0) is allowed once (the final drain) -- and, in the dynamic-tile-queue form (template
         # flag DYN), on the queue's own blocking paths (start, steal, retire: right behind its atomic

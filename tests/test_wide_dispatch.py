@@ -219,24 +219,3 @@ def test_prefill_rope_in_attention_gated_on_block_table_width():
         assert not ops.prefill_rope_in_attention(ops.PF_MAX_CHUNKS + 1)
     with knobs.override(prefill_attn=3, prefill_fused_rope=True):
         assert not ops.prefill_rope_in_attention(16)
-
-
-def test_streamk_grid_only_for_unsplit_grids_that_leave_cus_idle():
-    """knobs.wide_streamk: the 8B gate|up (224 column tiles) runs stream-K on every CU; grids that
-    already fill the CUs (>= wide_streamk_max_fill), need a K split (fewer than half as many tiles
-    as CUs) or hold more than one row tile do not; reserved comm CUs shrink the grid."""
-    from distributed_llms_amd import knobs
-    cpu = torch.device("cpu")
-    with knobs.override(wide_streamk=True):
-        assert gemm.streamk_grid(256, 28672, 4096, True, cpu) == 256
-        assert gemm.streamk_grid(64, 28672, 4096, True, cpu) == 256
-        assert gemm.streamk_grid(300, 28672, 4096, True, cpu) == 0       # two row tiles
-        assert gemm.streamk_grid(256, 6144, 4096, False, cpu) == 0       # 48 tiles: split-K
-        assert gemm.streamk_grid(256, 32768, 4096, False, cpu) == 0      # 256 tiles: full grid
-        gemm.reserve_cus_for_comm(16)
-        try:
-            assert gemm.streamk_grid(256, 28672, 4096, True, cpu) == 240
-        finally:
-            gemm.release_cus_for_comm()
-    with knobs.override(wide_streamk=False):
-        assert gemm.streamk_grid(256, 28672, 4096, True, cpu) == 0
