@@ -32,6 +32,22 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 
 
+# per-source extra flags.  attention.hip: its softmax takes fmaxf of MFMA results and of
+# v_permlane swap results, which hipcc (IEEE mode) first quiets with a v_max_f32 x, x, x each --
+# 56 of the prefill loop's 88 max instructions; the kernels never produce a NaN (masked scores are
+# -inf and every subtraction keeps a finite reference), so NaN semantics are dropped for that file
+FILE_FLAGS = {"attention.hip": ["-fno-honor-nans"]}
+
+
+def kernel_flags(src: str):
+    """hipcc flags of one csrc/kernels source (without includes / output)."""
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+              "-mcode-object-version=5"]
+    if os.environ.get("DLLM_PART_TYPE"):        # split-K slab type (common.h); rebuild with force=True
+        common.append(f"-DDLLM_PART_TYPE={int(os.environ['DLLM_PART_TYPE'])}")
+    return common + FILE_FLAGS.get(os.path.basename(src), [])
+
+
 def _py_includes():
     import pybind11
     return [pybind11.get_include(), sysconfig.get_paths()["include"]]
@@ -70,17 +86,13 @@ def build_kernels(force=False, jobs=8, verbose=False) -> str:
     headers = glob.glob(os.path.join(src_dir, "*.h"))
     hips = sorted(glob.glob(os.path.join(src_dir, "*.hip")))
     incs = [f"-I{p}" for p in _py_includes()] + [f"-I{src_dir}"]
-    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
-              "-mcode-object-version=5"]
-    if os.environ.get("DLLM_PART_TYPE"):        # split-K slab type (common.h); rebuild with force=True
-        common.append(f"-DDLLM_PART_TYPE={int(os.environ['DLLM_PART_TYPE'])}")
     jobs_list = []
     objs = []
     for src in hips:
         obj = os.path.join(out_dir, os.path.basename(src) + ".o")
         objs.append(obj)
-        if force or _stale(obj, [src] + headers):
-            jobs_list.append([HIPCC, "-c", src, "-o", obj] + common + incs)
+        if force or _stale(obj, [src] + headers + [os.path.abspath(__file__)]):
+            jobs_list.append([HIPCC, "-c", src, "-o", obj] + kernel_flags(src) + incs)
     bind = os.path.join(src_dir, "bindings.cpp")
     bobj = os.path.join(out_dir, "bindings.o")
     objs.append(bobj)

@@ -97,8 +97,7 @@ __device__ __forceinline__ void compute_chunk(WaveState<D>& st, const bf16x8 (&q
     }
     cm = fmaxf(cm, fmaxf(p[i], p[4 + i]));
   }
-  cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-  cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+  cm = rows_max(cm);                                // VALU row swaps, no LDS round trip
   cm *= scale_log2;
   // No early exit here: MFMA reads all 64 lanes' operands regardless of EXEC, so every
   // lane must run the same instruction stream. A fully masked column uses mref = 0,
@@ -107,15 +106,20 @@ __device__ __forceinline__ void compute_chunk(WaveState<D>& st, const bf16x8 (&q
   const float mref = (mn == -INFINITY) ? 0.f : mn;
   const float alpha = __builtin_amdgcn_exp2f(st.m - mref);
   st.m = mn;
+  // exponent arguments two per v_pk_fma_f32 (the same fused multiply-add per element), the
+  // probabilities summed as a pairwise tree on v_pk_add_f32: 4 + 4 VALU where scalar code takes 8 + 8
   bf16x8 pb;
-  float ps = 0.f;
+  f32x2 e2[4];
+  const f32x2 sc2 = {scale_log2, scale_log2}, mr2 = {-mref, -mref};
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(p[j], scale_log2, -mref));
-    ps += e;
-    pb[j] = f2bf(e);
+  for (int j = 0; j < 4; ++j) {
+    const f32x2 x = __builtin_elementwise_fma(f32x2{p[2 * j], p[2 * j + 1]}, sc2, mr2);
+    e2[j] = f32x2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+    pb[2 * j] = f2bf(e2[j][0]);
+    pb[2 * j + 1] = f2bf(e2[j][1]);
   }
-  st.lsum = st.lsum * alpha + ps;
+  const f32x2 s2 = (e2[0] + e2[1]) + (e2[2] + e2[3]);
+  st.lsum = st.lsum * alpha + (s2[0] + s2[1]);
   // alpha is exactly 1 wherever the running max did not move (exp2(0)), the common case once a
   // row's max has settled: skip the accumulator rescale when that holds for the whole wave (bit-exact)
   if (__any(alpha != 1.f)) {
@@ -254,8 +258,15 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
   const int nsplit = gridDim.x;
   const int G = hq / hkv;
   const int r = lane & 15, g = lane >> 4;
+  // the prologue's dependency roots go out first, back to back (vmcnt retires in issue order):
+  // this sequence's position (its cos / sin row), its context length and this split's first 64
+  // block ids -- not guarded by the context, so they need not wait for it -- and one round trip
+  // later every address the prologue loads from is known
+  const int pos_b = FUSED ? ra.positions[b] : 0;
   const int ctx = seq_lens[b];
   const int kbeg = split * split_len;
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  const int blk_first = lane < min(64, max_blocks - kbeg / kBS) ? bt[kbeg / kBS + lane] : 0;
   // FUSED: the new key (ctx - 1) is not in the cache yet: its chunk is loaded as usual and the
   // key's K row / V^T column are replaced in registers by the rotated k and v (the split that
   // owns it also appends them to the cache, after its last KV load)
@@ -263,10 +274,6 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
   const int kend = min(kbeg + split_len, ctx);     // exclusive
   const int c0 = kbeg / kBS, c1 = kend > kbeg ? (kend + kBS - 1) / kBS : c0;
 
-  // the first pass's block ids go out before the q/k/v loads: the first KV chunk's address
-  // then waits on this one load only (vmcnt retires in issue order), not on the qkv row too
-  const int32_t* bt = block_tables + (size_t)b * max_blocks;
-  const int blk_first = lane < min(64, c1 - c0) ? bt[c0 + lane] : 0;
   // Q^T fragments: column r = head kvh*G + r (zero beyond G)
   bf16x8 qf[D / 32];
   const bool col_ok = r < G;
@@ -292,12 +299,12 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     }
   }
   // FUSED: rotate q/k and append k/v AFTER the first KV chunk's loads are issued, so the
-  // positions -> cos/sin -> rotate dependency overlaps the KV stream instead of preceding it
+  // cos / sin -> rotate dependency overlaps the KV stream instead of preceding it
   bool rope_done = !FUSED;
   auto finish_rope = [&]() {
     if (!FUSED || rope_done) return;
     rope_done = true;
-    const float* cs = ra.cos_sin ? ra.cos_sin + (size_t)ra.positions[b] * D : nullptr;
+    const float* cs = ra.cos_sin ? ra.cos_sin + (size_t)pos_b * D : nullptr;   // pos_b: loaded first
     rope_rotate<D, FUSED>(qf, cs, g);
     rope_rotate<D, FUSED>(kn, cs, g);
     if (!col_ok) {
@@ -305,15 +312,17 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
       for (int ks = 0; ks < D / 32; ++ks) qf[ks] = bf16x8{};
     }
   };
-  // FUSED: put the new key into the registers of its chunk (branch-free: lane masks only)
+  // FUSED: put the new key into the registers of its chunk (lane masks inside that chunk only)
   const int cnew = FUSED ? (ctx - 1) / kBS : -1;
   const int noff = FUSED ? (ctx - 1) % kBS : 0;
   auto patch = [&](KVChunk<D>& c, int chunk, size_t cbase) {
     if (!FUSED) return;
-    const bool here = ctx > 0 && chunk == cnew;
+    // wave-uniform (ctx and the chunk index live in SGPRs): every other chunk skips the ~140 lane
+    // selects below on a scalar branch instead of running them as no-ops
+    if (!(ctx > 0 && chunk == cnew)) return;
     // (two static selects: a runtime choice between ka and kb made hipcc index them through scratch)
     const int prow = krow32(noff);                    // physical K row of the new key
-    const bool krow = here && r == (prow & 15);
+    const bool krow = r == (prow & 15);
     const bool ka_row = krow && prow < 16, kb_row = krow && prow >= 16;
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
@@ -322,7 +331,7 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     }
     // V^T fragment of lane group g: keys 8g..8g+7 -> elements 0..7
     const int e = noff & 7;
-    const bool vcol = here && g == (noff >> 3);
+    const bool vcol = g == (noff >> 3);
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt)
 #pragma unroll
@@ -394,8 +403,7 @@ __global__ void __launch_bounds__(WPB * 64, 2) attn_decode_kernel(   // 2nd arg:
     }
   }
   float lt = st.lsum;
-  lt += __shfl_xor(lt, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
+  lt = rows_sum(lt);
   if (!col_ok) return;                              // after the last MFMA: divergence is safe
   const int h = kvh * G + r;
   if (nsplit == 1) {
@@ -519,8 +527,7 @@ __global__ void __launch_bounds__(256, NT == 1 ? 2 : 1) attn_prefill2_kernel(
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     float lt = st[t].lsum;
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    lt = rows_sum(lt);
     const int crow = row0 + t * R + r / G, ch = r % G;
     if (crow < ql) {
       const float inv = lt > 0.f ? 1.f / lt : 0.f;
@@ -726,8 +733,7 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       float lt = st[t].lsum;
-      lt += __shfl_xor(lt, 16, 64);
-      lt += __shfl_xor(lt, 32, 64);
+      lt = rows_sum(lt);
       const int crow = row0 + t * R + r / G, ch = r % G;
       if (crow < ql) {
         const float inv = lt > 0.f ? 1.f / lt : 0.f;
@@ -749,8 +755,7 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     float lt = st[t].lsum;
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    lt = rows_sum(lt);
     const float inv = lt > 0.f ? 1.f / lt : 0.f;
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {

@@ -11,6 +11,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define DLLM_WAVE 64
@@ -39,6 +40,26 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, DLLM_WAVE));
   return v;
+}
+
+// Reduction over a lane's xor-16 and xor-32 partners (the four 16-lane rows of an MFMA 16x16
+// accumulator column) with the gfx950 VALU row swaps instead of __shfl_xor, which lowers to two
+// dependent ds_bpermute LDS round trips.  v_permlane16_swap(x, x) leaves rows (0, 0, 2, 2) in the
+// first result and (1, 1, 3, 3) in the second, v_permlane32_swap(x, x) halves (lo, lo) / (hi, hi):
+// combining the pair is the butterfly step.  Bit-identical to the shuffle form (max and a
+// two-operand add commute).
+__device__ __forceinline__ float rows_max(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+__device__ __forceinline__ float rows_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
 // Block-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats.

@@ -25,4 +25,9 @@ else
   run plain_70b_pp4 420 --gpus 4 --model llama3-70b --batch 64 --steps 1 --warmup 1
   run plain_mixtral_pp4 300 --gpus 4 --model mixtral-8x7b --batch 128 --steps 1 --warmup 1
   run plain_70b_pp8 420 --gpus 8 --model llama3-70b --batch 32 --steps 1 --warmup 1
+  unset DLLM_SHARE_GPU DLLM_DATA_BACKEND DLLM_RCCL_STANDIN DLLM_TRANSPORT
+  # stage-balance tables: every stage of the plan built and timed one at a time (decode graph replay)
+  $T 400 python -u bench/pp_stage_times.py --model llama3-70b --pp 4 8 --batch 64 > gpurun_out/r6e_stages_70b.txt 2>&1 || { tail -30 gpurun_out/r6e_stages_70b.txt; exit 1; }
+  $T 300 python -u bench/pp_stage_times.py --model mixtral-8x7b --pp 4 --batch 128 > gpurun_out/r6e_stages_mixtral.txt 2>&1 || { tail -30 gpurun_out/r6e_stages_mixtral.txt; exit 1; }
+  tail -12 gpurun_out/r6e_stages_70b.txt gpurun_out/r6e_stages_mixtral.txt
 fi

@@ -55,3 +55,52 @@ def test_pf_persistent_kernel_keeps_the_pipeline_full(pp_asm):
         if dyn:                            # the K loop's fetch is the asynchronous inline-asm one
             assert "global_atomic_add" in body and "off sc0" in body
         assert body.count("v_mfma_f32_16x16x32_bf16") >= 128
+
+
+@pytest.fixture(scope="module")
+def attn_asm(tmp_path_factory):
+    from distributed_llms_amd.csrc.build import kernel_flags
+    src = ROOT / "distributed_llms_amd" / "csrc" / "kernels" / "attention.hip"
+    out = tmp_path_factory.mktemp("asm") / "attn.s"
+    subprocess.run([HIPCC, *kernel_flags(str(src)), "--offload-device-only", "-S", str(src), f"-I{src.parent}",
+                    "-o", str(out)], check=True, capture_output=True, timeout=900)
+    return out.read_text()
+
+
+def _kernel_body(s, name):
+    start = s.index(name + ":")
+    return s[start: s.index(".Lfunc_end", start)]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_attention_softmax_stays_in_valu(attn_asm):
+    """The online softmax's column max / sum cross the four 16-lane rows with v_permlane16/32_swap
+    (no ds_bpermute LDS round trip on the dependency chain), its fmaxf calls are not preceded by
+    NaN-quieting self-max instructions (attention.hip builds with -fno-honor-nans), and no decode or
+    prefill kernel spills."""
+    s = attn_asm
+    names = re.findall(r"^(_ZN4dllm(?:18attn_decode_kernel|23attn_prefill_lds_kernel|20attn_prefill2_kernel)\w+):",
+                       s, re.M)
+    assert len(names) >= 20
+    for name in names:
+        body = _kernel_body(s, name)
+        meta = s[s.index(".amdhsa_kernel " + name):]
+        assert int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", meta).group(1)) == 0, name
+        assert "ds_bpermute" not in body, name
+        assert "v_permlane32_swap" in body and "v_permlane16_swap" in body, name
+        quiet = re.findall(r"v_max_f32_e32 (v\d+), (v\d+), (v\d+)", body)
+        assert not [q for q in quiet if q[1] == q[2]], (name, "NaN-quieting v_max x, x")
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_decode_patch_is_a_scalar_branch(attn_asm):
+    """The fused decode kernel patches the new key into ONE chunk's registers: the lane selects sit
+    in blocks behind a wave-uniform branch, apart from the chunk's MFMAs, so the steady-state chunk
+    carries only the softmax's few selects (the branch-free form ran ~140 per chunk)."""
+    name = re.search(r"^(_ZN4dllm18attn_decode_kernelILi128ELi4ELb1ELi5E\w+):", attn_asm, re.M).group(1)
+    blocks = re.split(r"\n(?=\.LBB\w+:|\s*; %bb)", _kernel_body(attn_asm, name))
+    mfma_blocks = [b for b in blocks if "v_mfma" in b]
+    assert mfma_blocks
+    for b in mfma_blocks:
+        assert b.count("v_cndmask_b32") <= 16, b.count("v_cndmask_b32")
+    assert any(b.count("v_cndmask_b32") >= 32 and "v_mfma" not in b for b in blocks)   # the patch itself
