@@ -782,6 +782,357 @@ __global__ void __launch_bounds__(WV * 64, NT >= 4 || WV > 4 ? 1 : 2) attn_prefi
   }
 }
 
+// ---------------------------------------------------------------------------
+// Prefill v6: v4's LDS-shared K / V stream on the 32x32x16 MFMA (v_mfma_f32_32x32x16_bf16).
+// S^T = K Q^T per 64-key tile (two 32-key blocks): a lane holds 32 scores of ONE column (query row
+// x head) -- 16 per block, rows 8 j + 4 hi + i of the 32x32 result -- so the column max is in-lane
+// plus one v_permlane32_swap, and the per-column softmax work (max, alpha, denominator update,
+// accumulator rescale) is paid once per 64 keys x 32 columns where the 16x16 form pays it per
+// 32 keys x 16 columns: about half the VALU per score, and long prefill attention is VALU-bound
+// (profiles/round5_prefill_attn_valu.md).
+// The QK^T A operand loads key pi(m) (m with bits 2 and 3 swapped) into MFMA row m.  That puts a
+// lane's 16 scores of block bb, in register order r = 8 h + 0..7, on keys 16 h + 8 hi + 0..7: the
+// P.V B operand of MFMA (bb, h) is the bf16 conversion of 8 consecutive score registers (P never
+// leaves the lane), and its V^T A operand is one 16-byte read of key group 2 h + hi of the cache's
+// [4][D][8] V^T block.  Workgroup: 8 waves x 32 columns (32 / G query rows x G heads each) of one
+// (sequence, kv head); K / V tiles stream through a 3-deep LDS ring by LDS-DMA with v4's XOR-swizzled
+// K rows, conflict-free for this read pattern as well (the 16 lanes of a ds_read_b128 group hit 16
+// distinct row & 15 values).
+// ---------------------------------------------------------------------------
+constexpr int kW32Waves = 8;
+
+// physical K row (common.h krow32 layout) of the key pi(m) the QK^T A operand puts at MFMA row m
+__device__ __forceinline__ int w32_krow(int m) {
+  return (((m >> 3) & 1) << 4) | ((m >> 4) << 3) | (((m >> 2) & 1) << 2) | (m & 3);
+}
+
+// max / sum with the lane 32 apart (the other half of a 32x32 accumulator column)
+__device__ __forceinline__ float half_max(float v) {
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float half_sum(float v) {
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+template <int G, bool PIPE>
+__global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
+    bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
+    const int32_t* __restrict__ cu_seqlens_q, const int32_t* __restrict__ seq_lens, int hq, int hkv,
+    int max_blocks, float scale_log2, const int32_t* __restrict__ positions, const float* __restrict__ cos_sin,
+    int q_stride) {
+  constexpr int D = 128;
+  constexpr int WV = kW32Waves;
+  constexpr int R = 32 / G;                       // query rows per wave
+  constexpr int TK = 2 * kBS;                     // keys per tile
+  constexpr int BLK = kBS * D;                    // bf16 elements of one K block (= one V^T block)
+  constexpr int TILE = 4 * BLK;                   // K0 K1 V0 V1: 32 KiB
+  constexpr int NB = PIPE ? 4 : 3;                // ring depth
+  constexpr int GL = TILE / 512 / WV;             // 1 KiB LDS-DMA pieces per wave per tile
+  static_assert(GL == 4 && 32 % G == 0, "tile pieces / column tiling");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NB * TILE + 2 * kPfMaxChunks];
+  int* ids = reinterpret_cast<int*>(smem + NB * TILE);
+
+  // XCD-aware order (as v4): the row tiles of one (sequence, kv head) share an XCD's L2
+  int qt = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  {
+    const int nx = gridDim.x, ng = gridDim.y * gridDim.z;
+    const int lin = blockIdx.x + nx * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (ng % 8 == 0) {
+      const int xcd = lin & 7, slot = lin >> 3;
+      const int grp = (slot / nx) * 8 + xcd;
+      qt = slot % nx;
+      kvh = grp % gridDim.y;
+      b = grp / gridDim.y;
+    }
+  }
+  // the wave index through readfirstlane: hipcc then knows it (and every bound derived from it) is
+  // wave-uniform and branches on it with scalar branches instead of EXEC masks
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m = lane & 31, hi = lane >> 5;
+  const int qs = cu_seqlens_q[b], ql = cu_seqlens_q[b + 1] - qs;
+  const int wg_row0 = qt * WV * R;
+  if (wg_row0 >= ql) return;                      // workgroup-uniform
+  const int row0 = wg_row0 + w * R;
+  const bool active = row0 < ql;                  // wave-uniform; inactive waves still stage
+  const int ctx = seq_lens[b];
+  const int qpos0 = ctx - ql;
+  // this lane's column: query row row0 + m / G, head kvh * G + m % G
+  const int crow = row0 + m / G, ch = m % G;
+  const bool ok = crow < ql;
+  const int kmax_col = ok ? qpos0 + crow : -1;
+  const int tok = qs + (ok ? crow : 0);
+  // Q^T fragments (B operand): column m, dims 16 ks + 8 hi + 0..7; RoPE partners (d, d + 64) are
+  // fragments ks and ks + 4 of the same lane
+  bf16x8 qf[D / 16];
+  {
+    const bf16* qrow = q + (size_t)tok * q_stride + (size_t)(kvh * G + ch) * D + 8 * hi;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qrow + 16 * ks);
+    if (cos_sin != nullptr) {
+      const float* cs = cos_sin + (size_t)positions[tok] * D + 8 * hi;
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) {
+        const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + 16 * ks);
+        const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + 16 * ks + 4);
+        const f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + D / 2 + 16 * ks);
+        const f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + D / 2 + 16 * ks + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float c = j < 4 ? c0[j] : c1[j - 4], s = j < 4 ? s0[j] : s1[j - 4];
+          const float a = bf2f(qf[ks][j]), bq = bf2f(qf[ks + D / 32][j]);
+          qf[ks][j] = f2bf(__builtin_fmaf(a, c, -(bq * s)));   // as rope_rotate: explicit FMAs
+          qf[ks + D / 32][j] = f2bf(__builtin_fmaf(bq, c, a * s));
+        }
+      }
+    }
+    if (!ok) {
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) qf[ks] = bf16x8{};
+    }
+  }
+  const int wg_kmax = qpos0 + min(wg_row0 + WV * R, ql) - 1;
+  const int nch = wg_kmax / kBS + 1;              // 32-key blocks the workgroup reads
+  const int ntile = (nch + 1) / 2;
+  const int wave_kmax = active ? qpos0 + min(row0 + R, ql) - 1 : -1;
+  const int wave_kmin = row0 + R <= ql ? qpos0 + row0 : -1;   // -1: a column past the sequence
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  for (int i = threadIdx.x; i < nch; i += WV * 64) ids[i] = bt[i];
+  // retire the q loads before the first LDS-DMA (a use inside the loop would wait vmcnt(0) there)
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) asm volatile("" ::"v"(qf[ks]));
+  __syncthreads();
+
+  const size_t head_off = (size_t)kvh * BLK;
+  const size_t blk_stride = (size_t)hkv * BLK;
+  // wave w stages 1 KiB pieces 4 w .. 4 w + 3 of tile t: pieces 0-7 K block 0, 8-15 K block 1,
+  // 16-23 V^T block 0, 24-31 V^T block 1 (a block past the sequence re-reads the last one: its keys
+  // are masked for every column)
+  auto stage = [&](int t, int buf) {
+    bf16* dst = smem + buf * TILE;
+#pragma unroll
+    for (int j = 0; j < GL; ++j) {
+      const int i = w * GL + j, part = i >> 3;
+      const int c = min(2 * t + (part & 1), nch - 1);
+      const size_t base = (size_t)ids[c] * blk_stride + head_off;
+      const bf16* src;
+      if (part < 2) {
+        const int rr = (i & 7) * 4 + lane / 16, cs = lane % 16;
+        src = k_cache + base + (size_t)rr * D + (cs ^ (rr & 15)) * 8;
+      } else {
+        src = v_cache + base + (size_t)(i & 7) * 512 + lane * 8;
+      }
+      __builtin_amdgcn_global_load_lds((glb_vptr_a)src, (lds_vptr_a)(dst + i * 512), 16, 0, 0);
+    }
+  };
+  const int krow = w32_krow(m), kswz = krow & 15;
+  f32x16 acc[D / 32];                             // O^T: dims 32 dt + 8 (r / 4) + 4 hi + r % 4, column m
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) acc[dt] = f32x16{};
+  float mrun = -INFINITY, lsum = 0.f;
+  const f32x2 sc2 = {scale_log2, scale_log2};
+
+  // S^T of tile tb (two blocks): 16 MFMAs reading K fragments from the ring
+  auto qk = [&](const bf16* tb, f32x16& s0, f32x16& s1) {
+    s0 = f32x16{};
+    s1 = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      const int slot = ((2 * ks + hi) ^ kswz) * 8;
+      const bf16x8 ka = *reinterpret_cast<const bf16x8*>(tb + krow * D + slot);
+      const bf16x8 kb = *reinterpret_cast<const bf16x8*>(tb + BLK + krow * D + slot);
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[ks], s1, 0, 0, 0);
+    }
+  };
+  // causal mask: register r of block bb holds key k0 + 32 bb + 16 (r >> 3) + 8 hi + (r & 7).  Behind a
+  // wave-uniform branch in ONE instantiation: two (masked / unmasked) copies of the tile made hipcc
+  // keep the accumulators in different registers per copy and shuffle all 64 (v_mov_b64 x 32) at merges
+  auto mask = [&](f32x16& s0, f32x16& s1, int k0) {
+    const int kl = kmax_col - k0 - 8 * hi;         // admissible: 16 (r >> 3) + (r & 7) (+ 32) <= kl
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = 16 * (r >> 3) + (r & 7);
+      s0[r] = key <= kl ? s0[r] : -INFINITY;
+      s1[r] = key + kBS <= kl ? s1[r] : -INFINITY;
+    }
+  };
+  // online softmax of one tile's scores: the P.V B operands pb[2 bb + h], the rescale factor
+  auto softmax = [&](const f32x16& s0, const f32x16& s1, bf16x8 (&pb)[4]) {
+    float cm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cm = fmaxf(cm, fmaxf(s0[r], s1[r]));
+    cm = half_max(cm) * scale_log2;
+    const float mn = fmaxf(mrun, cm);
+    const float mref = (mn == -INFINITY) ? 0.f : mn;
+    const float alpha = __builtin_amdgcn_exp2f(mrun - mref);
+    mrun = mn;
+    const f32x2 mr2 = {-mref, -mref};
+    f32x2 sum2 = {0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {                 // score pairs: block p / 8, registers 2 (p % 8) + 0, 1
+      const f32x16& sv = p < 8 ? s0 : s1;
+      const int r = 2 * (p & 7);
+      const f32x2 x = __builtin_elementwise_fma(f32x2{sv[r], sv[r + 1]}, sc2, mr2);
+      const f32x2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+      sum2 += e;
+      pb[p >> 2][r & 7] = f2bf(e[0]);
+      pb[p >> 2][(r & 7) + 1] = f2bf(e[1]);
+    }
+    lsum = lsum * alpha + (sum2[0] + sum2[1]);
+    return alpha;
+  };
+  auto rescale = [&](float alpha) {
+    if (__any(alpha != 1.f)) {                      // exactly 1 wherever no column's max moved
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) acc[dt] *= alpha;
+    }
+  };
+  // O^T += V^T P^T for the tile in ring slot tb: 16 MFMAs reading V^T fragments from the ring
+  auto pv = [&](const bf16* tb, const bf16x8 (&pb)[4]) {
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+      for (int bh = 0; bh < 4; ++bh) {
+        const bf16x8 va = *reinterpret_cast<const bf16x8*>(
+            tb + 2 * BLK + (bh >> 1) * BLK + ((2 * (bh & 1) + hi) * D + 32 * dt + m) * 8);
+        acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[bh], acc[dt], 0, 0, 0);
+      }
+    }
+  };
+
+  stage(0, 0);
+  if (ntile > 1) stage(1, 1);
+  // PIPE: the previous tile's P.V MFMAs go out right behind this tile's QK^T and run while the VALU
+  // does this tile's softmax (MFMA and VALU are separate pipes; without it a wave's P.V waits for
+  // its own softmax, and only the other wave on the SIMD can fill the gap).  The ring is one deeper:
+  // a tile's V^T is still read one iteration after its K.  An active wave runs every tile of the
+  // workgroup (past its own rows' keys the scores are all masked: P = 0, alpha = 1) so that the
+  // accumulators see one straight-line path per iteration -- a skip path made hipcc copy all 64 of
+  // them in and out of the tile code
+  bf16x8 pbp[4] = {};                             // PIPE: P of the previous tile (zeros: a no-op P.V)
+  int vprev = 0;                                  // PIPE: its ring slot
+  for (int t = 0; t < ntile; ++t) {
+    if (t + 1 < ntile) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // slot (t + 2) % NB was last read in iteration t - 1 (PIPE: t - 2's V^T in iteration t - 1), which
+    // every wave finished before the barrier
+    if (t + 2 < ntile) stage(t + 2, (t + 2) % NB);
+    const bf16* tb = smem + (t % NB) * TILE;
+    const int k0 = t * TK;
+    if constexpr (PIPE) {
+      if (!active) continue;
+      f32x16 s0, s1;
+      qk(tb, s0, s1);
+      if (k0 + TK - 1 > wave_kmin) mask(s0, s1, k0);   // unmasked below every column's diagonal
+      // the previous tile's 16 P.V MFMAs with this tile's softmax in their gaps, one slice per gap
+      // (sched_barrier(0) fences each gap): gaps 0-3 the column max over registers 4 k .. 4 k + 3 of
+      // both blocks, gap 4 the cross-half max and the running-max update, gaps 5-15 the 16 score pairs
+      // (FMA, two exp, cvt, sum).  MFMA i: d-tile i & 3 (consecutive MFMAs on different accumulators),
+      // P operand i >> 2; its V^T fragment is read one group of four ahead.
+      const bf16* vt = smem + vprev * TILE;
+      auto vread = [&](int i) {
+        const int dt = i & 3, bh = i >> 2;
+        return *reinterpret_cast<const bf16x8*>(vt + 2 * BLK + (bh >> 1) * BLK +
+                                                ((2 * (bh & 1) + hi) * D + 32 * dt + m) * 8);
+      };
+      bf16x8 va[4], vn[4], pb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) va[j] = vread(j);
+      float cmp[4], alpha = 1.f, mref = 0.f;
+      f32x2 sum2 = {0.f, 0.f};
+      auto pair = [&](int p) {                     // score pair p: block p / 8, registers 2 (p % 8) + 0, 1
+        const f32x16& sv = p < 8 ? s0 : s1;
+        const int r = 2 * (p & 7);
+        const f32x2 x = __builtin_elementwise_fma(f32x2{sv[r], sv[r + 1]}, sc2, f32x2{-mref, -mref});
+        const f32x2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+        sum2 += e;
+        pb[p >> 2][r & 7] = f2bf(e[0]);
+        pb[p >> 2][(r & 7) + 1] = f2bf(e[1]);
+      };
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if ((i & 3) == 0 && i + 4 < 16) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vn[j] = vread(i + 4 + j);
+        }
+        acc[i & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[i & 3], pbp[i >> 2], acc[i & 3], 0, 0, 0);
+        if ((i & 3) == 3 && i + 1 < 16) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) va[j] = vn[j];
+        }
+        if (i < 4) {
+          cmp[i] = fmaxf(fmaxf(fmaxf(s0[4 * i], s0[4 * i + 1]), fmaxf(s0[4 * i + 2], s0[4 * i + 3])),
+                         fmaxf(fmaxf(s1[4 * i], s1[4 * i + 1]), fmaxf(s1[4 * i + 2], s1[4 * i + 3])));
+        } else if (i == 4) {
+          const float cm = half_max(fmaxf(fmaxf(cmp[0], cmp[1]), fmaxf(cmp[2], cmp[3]))) * scale_log2;
+          const float mn = fmaxf(mrun, cm);
+          mref = (mn == -INFINITY) ? 0.f : mn;
+          alpha = __builtin_amdgcn_exp2f(mrun - mref);
+          mrun = mn;
+        } else if (i < 10) {
+          pair(2 * (i - 5));
+          pair(2 * (i - 5) + 1);
+        } else {
+          pair(i);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // pin the probabilities and their sum here: hipcc would otherwise sink the exp / cvt / add work
+      // past the rescale branch below, out of the MFMAs' shadow
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(pb[i]));
+      asm volatile("" : "+v"(sum2));
+      lsum = lsum * alpha + (sum2[0] + sum2[1]);
+      rescale(alpha);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pbp[i] = pb[i];
+      vprev = t % NB;
+    } else if (k0 <= wave_kmax) {
+      f32x16 s0, s1;
+      qk(tb, s0, s1);
+      if (k0 + TK - 1 > wave_kmin) mask(s0, s1, k0);
+      bf16x8 pb[4];
+      rescale(softmax(s0, s1, pb));
+      pv(tb, pb);
+    }
+  }
+  if (PIPE && active) pv(smem + vprev * TILE, pbp);
+  const float lt = half_sum(lsum);
+  // output through a wave-private LDS image (the ring is free once every wave is past its last
+  // tile): whole 16-byte pieces of a column per store, G heads of a row contiguous -- whole lines
+  constexpr int OLD = D + 8;
+  static_assert(WV * 32 * OLD <= NB * TILE, "output image");
+  __syncthreads();
+  if (!active) return;
+  bf16* img = smem + w * (32 * OLD);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = f2bf(acc[dt][4 * j + i] * inv);
+      *reinterpret_cast<bf16x4*>(img + m * OLD + 32 * dt + 8 * j + 4 * hi) = o;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): the wave's own image writes landed
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 32 * (D / 8) / 64; ++it) {
+    const int p = it * 64 + lane, col = p / (D / 8), piece = p % (D / 8);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + col * OLD + piece * 8);
+    const int crow2 = row0 + col / G, ch2 = col % G;
+    if (crow2 < ql)
+      *reinterpret_cast<bf16x8*>(out + ((size_t)(qs + crow2) * hq + kvh * G + ch2) * D + piece * 8) = v;
+  }
+}
+
 // ------------------------------------------------------------------ launchers
 static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache, uintptr_t block_tables,
                           uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml, int batch, int hq, int hkv, int d,
@@ -861,13 +1212,23 @@ template <int D>
 static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv, hipStream_t s, uintptr_t out,
                            uintptr_t q, uintptr_t k_cache, uintptr_t v_cache, uintptr_t bt, uintptr_t cu, uintptr_t sl,
                            int hq, int max_blocks, float sl2, uintptr_t pos, uintptr_t cs, int q_stride) {
-  // version 3: the register-tiled kernel, two tiles per wave; 4: the LDS-shared kernel, two tiles per wave
+  // version 3: the register-tiled kernel, two tiles per wave; 4: the LDS-shared kernel, two tiles per
+  // wave; 6: the LDS-shared kernel on 32x32x16 MFMAs, 8 waves x 32 columns (head_dim 128); 7: 6 with
+  // the previous tile's P.V overlapping this tile's softmax
   const int nt = 2;
-  const int rows_per_wg = kWaves * (16 / g) * nt;
+  const int rows_per_wg = version >= 6 ? kW32Waves * (32 / g) : kWaves * (16 / g) * nt;
   const dim3 grid((max_q_len + rows_per_wg - 1) / rows_per_wg, hkv, batch);
 #define DLLM_PF(GG)                                                                                         \
   do {                                                                                                      \
-    if (version == 4)                                                                                       \
+    if (version >= 6) {                                                                                     \
+      if constexpr (D == 128) {                                                                             \
+        auto kern = version == 7 ? attn_prefill_w32_kernel<GG, true> : attn_prefill_w32_kernel<GG, false>;   \
+        hipLaunchKernelGGL(kern, grid, dim3(kW32Waves * 64), 0, s, (bf16*)out, (const bf16*)q,                \
+                           (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,                    \
+                           (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2,                 \
+                           (const int32_t*)pos, (const float*)cs, q_stride);                                 \
+      }                                                                                                     \
+    } else if (version == 4)                                                                                \
       hipLaunchKernelGGL((attn_prefill_lds_kernel<D, GG, 2>), grid, dim3(256), 0, s, (bf16*)out,              \
                          (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,      \
                          (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2,                   \
@@ -907,9 +1268,10 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
   // version (knobs.prefill_attn): 4 = the LDS-shared kernel (default; bench/prefill_attn_bench.py:
   // 1.6-1.7x v3 from 128- to 8192-token prompts); 3 = the register-tiled kernel, which also serves
   // block tables wider than the 32k tokens of block ids the LDS kernel stages
-  DLLM_HOST_CHECK(version == 3 || version == 4, "prefill attention version 3 or 4");
-  if (version == 4 && max_blocks > kPfMaxChunks) version = 3;
-  DLLM_HOST_CHECK(q_stride == hq * d || version == 4, "in-kernel RoPE / strided q: LDS kernel only (<= 32k context)");
+  DLLM_HOST_CHECK(version == 3 || version == 4 || version == 6 || version == 7, "prefill attention version 3, 4, 6 or 7");
+  if (version >= 6 && (d != 128 || G > 16)) version = 4;           // the 32x32 kernels: head_dim 128, G | 32
+  if (version != 3 && max_blocks > kPfMaxChunks) version = 3;
+  DLLM_HOST_CHECK(q_stride == hq * d || version != 3, "in-kernel RoPE / strided q: LDS kernels only (<= 32k context)");
   if (d == 128)
     launch_prefill<128>(G, version, max_q_len, batch, hkv, s, out, q, k_cache, v_cache, block_tables, cu_seqlens_q,
                         seq_lens, hq, max_blocks, sl2, positions, cos_sin, q_stride);

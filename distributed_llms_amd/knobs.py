@@ -77,7 +77,7 @@ class Knobs:
     head_beside_comm: str = "sq"
     # ---- attention (ops/__init__.py)
     attn_target_waves: int = 1024     # decode split-KV: waves to aim for (profiles/attn_decode_sweep.txt)
-    prefill_attn: int = 4             # prefill kernel: 4 = LDS-shared K/V tiles, 3 = register-tiled (> 32k fallback)
+    prefill_attn: int = 4             # prefill kernel: 4 = LDS-shared K/V tiles (16x16 MFMA), 6 = the same on 32x32x16 MFMAs (head_dim 128), 3 = register-tiled (> 32k fallback)
     # prefill q-RoPE in the attention kernel's q load (rope_cache appends K / V only): no rotated-q
     # round trip through HBM (268 MB per layer at T = 32768)
     prefill_fused_rope: bool = True

@@ -86,8 +86,9 @@ def test_lookahead_decode_matches_synchronous(cuda, graphs):
     assert any(len(o) < n for o, n in zip(sync_e, lens)), "EOS never fired"
 
 
+@pytest.mark.parametrize("attn", [4, 6, 7])
 @pytest.mark.parametrize("name", ["tiny-llama-d128", "tiny-mixtral"])
-def test_chunked_prefill_gpu_matches_cpu_logits(cuda, name):
+def test_chunked_prefill_gpu_matches_cpu_logits(cuda, name, attn):
     """A 300-token prompt prefilled in 64-token chunks on the GPU (each chunk's attention reads the
     earlier chunks from the paged cache) vs the CPU fp32 whole-prompt prefill: the last chunk's
     logits agree."""
@@ -101,11 +102,13 @@ def test_chunked_prefill_gpu_matches_cpu_logits(cuda, name):
                                    use_graphs=False, num_kv_blocks=64, max_prefill_tokens=64),
                       ModelStage(cfg, 0, cfg.num_layers, "cuda", torch.bfloat16).load_hf_state(sd))
     logits = []
+    from distributed_llms_amd import knobs
     for eng in (e_cpu, e_gpu):
         eng.add_request(prompt, SamplingParams(max_new_tokens=1))
         while True:
             st = eng.scheduler.schedule(0)
-            out = eng.runner.execute(build_host_batch(st, eng.bm, 32))
+            with knobs.override(prefill_attn=attn):
+                out = eng.runner.execute(build_host_batch(st, eng.bm, 32))
             final = st.seqs[0].chunk == 0
             eng.scheduler.complete(st, [0])
             if final:

@@ -155,8 +155,9 @@ def test_paged_attention_decode_fused_rope(cuda, hq, hkv, d, lens, rope):
     torch.testing.assert_close(v1.float(), v2, atol=0, rtol=0)
 
 
-@pytest.mark.parametrize("version", ["3", "4"])
-@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 64)])
+@pytest.mark.parametrize("version", ["3", "4", "6", "7"])
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 64), (16, 16, 128),
+                                      (32, 2, 128)])
 def test_paged_attention_prefill(cuda, hq, hkv, d, version):
     ctx = [37, 128, 300, 5]
     qlen = [37, 64, 1, 5]       # second/third: chunked prefill with prior context
@@ -170,7 +171,7 @@ def test_paged_attention_prefill(cuda, hq, hkv, d, version):
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("version", ["3", "4"])
+@pytest.mark.parametrize("version", ["3", "4", "6", "7"])
 def test_paged_attention_prefill_long(cuda, version):
     """Long prompts: > 64 KV chunks per sequence (block-id reloads), many workgroups per
     (sequence, kv head), a chunked prefill that starts mid-block."""
@@ -226,8 +227,9 @@ def test_decode_rope_consumes_splitk_qkv_bit_exact(cuda, b):
     torch.testing.assert_close(v1, v2, atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("version", [4, 6, 7])
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (8, 4, 64)])
-def test_prefill_attention_with_q_rope_in_kernel(cuda, hq, hkv, d):
+def test_prefill_attention_with_q_rope_in_kernel(cuda, hq, hkv, d, version):
     """knobs.prefill_fused_rope: rope_cache_append(write_q=False) appends K / V only and the LDS prefill
     kernel rotates q from the raw qkv projection in registers.  Same cache contents, and the attention
     output matches the two-pass form (rotated q written, then attended) and the fp32 reference."""
@@ -247,7 +249,7 @@ def test_prefill_attention_with_q_rope_in_kernel(cuda, hq, hkv, d):
     qkv = _bf(t, (hq + 2 * hkv) * d)
     cs = ref.rope_cos_sin(d, 1024, 500000.0, device="cuda")
     scale = 1 / math.sqrt(d)
-    with knobs.override(prefill_attn=4, prefill_fused_rope=True):
+    with knobs.override(prefill_attn=version, prefill_fused_rope=True):
         q = ops.rope_cache_append(qkv, pos, cs, k1, v1, slots, hq, hkv, d)
         two_pass = ops.paged_attention_prefill(q, k1, v1, bt, cu, sl, scale)
         assert ops.rope_cache_append(qkv, pos, cs, k2, v2, slots, hq, hkv, d, write_q=False) is None
