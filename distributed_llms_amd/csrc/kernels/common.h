@@ -74,7 +74,11 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+// SiLU with the hardware reciprocal (v_rcp_f32, 1 ulp): hipcc expands x / y into the IEEE division
+// sequence (2 v_div_scale, v_rcp, 4 FMAs, v_div_fmas, v_div_fixup), which made gemm_pf's SwiGLU
+// epilogue ~2,200 VALU per 256x256 tile per wave with the MFMA pipe idle; every caller rounds the
+// result to bf16
+__device__ __forceinline__ float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // f32 -> bf16 via the compiler cast: gfx950 emits v_cvt_pk_bf16_f32 (RNE, NaN-preserving).
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
