@@ -835,7 +835,9 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
   __shared__ __attribute__((aligned(16))) bf16 smem[NB * TILE + 2 * kPfMaxChunks];
   int* ids = reinterpret_cast<int*>(smem + NB * TILE);
 
-  // XCD-aware order (as v4): the row tiles of one (sequence, kv head) share an XCD's L2
+  // XCD-aware order (as v4): the row tiles of one (sequence, kv head) share an XCD's L2; and the
+  // last row tiles -- the most keys under the causal mask -- are dispatched first, so the long
+  // workgroups do not form the launch's tail
   int qt = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   {
     const int nx = gridDim.x, ng = gridDim.y * gridDim.z;
@@ -847,6 +849,7 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
       kvh = grp % gridDim.y;
       b = grp / gridDim.y;
     }
+    qt = nx - 1 - qt;
   }
   // the wave index through readfirstlane: hipcc then knows it (and every bound derived from it) is
   // wave-uniform and branches on it with scalar branches instead of EXEC masks
