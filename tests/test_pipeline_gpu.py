@@ -151,9 +151,19 @@ def test_multiprocess_gpu_pipeline_standin_big_model_dims(cuda, model, world):
     stand-in, stage processes sharing the one GPU): Llama-3-70B and Mixtral-8x7B layer shapes
     (hidden 8192 / 28672-wide MLP / 128k vocab; 8 experts of 14336, top-2) at reduced depth, so the
     reference engine and the stage processes fit beside each other.  Two rounds reproduce the
-    single-process engine token for token."""
+    single-process engine token for token.  The reference runs with the stage processes' GEMM grids:
+    a transport with spinning comm kernels leaves CUs free (ops.gemm.reserve_cus_for_comm), which
+    changes gemm_wide's K split -- and with it the split-K rounding -- at these K (8192 / 28672); with
+    full-chip splits the reference is a different (equally valid) rounding of the same model."""
+    from distributed_llms_amd.ops import gemm
+    from distributed_llms_amd.parallel.rccl_transport import comm_cus
     prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
-    ref = LLMEngine(_mp_ecfg(1, model=model)).generate(prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
+    gemm.reserve_cus_for_comm(comm_cus())
+    try:
+        ref = LLMEngine(_mp_ecfg(1, model=model)).generate(prompts, SamplingParams(max_new_tokens=12,
+                                                                                     ignore_eos=True))
+    finally:
+        gemm.release_cus_for_comm()
     torch.cuda.empty_cache()
     res = _run_ranks(world, prompts, "rccl-standin", rounds=2, model=model, timeout_s=420)
     assert res[0] == [ref, ref]
