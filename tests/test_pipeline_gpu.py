@@ -166,7 +166,18 @@ def test_multiprocess_gpu_pipeline_standin_big_model_dims(cuda, model, world):
         gemm.release_cus_for_comm()
     torch.cuda.empty_cache()
     res = _run_ranks(world, prompts, "rccl-standin", rounds=2, model=model, timeout_s=420)
-    assert res[0] == [ref, ref]
+    assert res[0] == [ref, ref], _diff_report(ref, res[0])
+
+
+def _diff_report(ref, rounds):
+    """Where the pipeline's ids leave the reference's: per round, the differing sequences and the
+    first differing step of each (and whether the rounds agree with each other)."""
+    lines = [f"rounds agree with each other: {all(r == rounds[0] for r in rounds)}"]
+    for i, got in enumerate(rounds):
+        bad = [(j, next(t for t, (a, b) in enumerate(zip(x, y)) if a != b) if x[:len(y)] != y[:len(x)]
+                else min(len(x), len(y))) for j, (x, y) in enumerate(zip(got, ref)) if x != y]
+        lines.append(f"round {i}: {len(bad)} of {len(ref)} sequences differ; (sequence, first step): {bad}")
+    return "\n".join(lines)
 
 
 @pytest.mark.parametrize("units,exact", [("5:0,8;8,11;11,20", True), ("5:0,7;7,12;12,20", True),
