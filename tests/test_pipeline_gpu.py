@@ -158,10 +158,13 @@ def test_multiprocess_gpu_pipeline_standin_big_model_dims(cuda, model, world):
     from distributed_llms_amd.ops import gemm
     from distributed_llms_amd.parallel.rccl_transport import comm_cus
     prompts = [[i + 1, 2 * i + 3, 5, 7, 11 + i] for i in range(10)]
+    # and with the pipeline's microbatches: the driver gives each of its world + 1 slots an even share
+    # of the 10 requests (2), and the MoE layer picks its expert kernel by token count (moe_wide from
+    # knobs.moe_wide_min_pairs token-expert pairs), so the reference decodes 2 sequences at a time too
     gemm.reserve_cus_for_comm(comm_cus())
     try:
-        ref = LLMEngine(_mp_ecfg(1, model=model)).generate(prompts, SamplingParams(max_new_tokens=12,
-                                                                                     ignore_eos=True))
+        ref = LLMEngine(_mp_ecfg(1, model=model).apply_overrides(max_batch=2)).generate(
+            prompts, SamplingParams(max_new_tokens=12, ignore_eos=True))
     finally:
         gemm.release_cus_for_comm()
     torch.cuda.empty_cache()
