@@ -197,8 +197,7 @@ __device__ __forceinline__ void moe_rows(float* red, bf16* __restrict__ y, const
     f32x4 acc[MT][NT];
     sk_mainloop<MT, NT>(acc, xrow, wrow, g0, g1);
     __syncthreads();
-    sk_reduce_lds<MT, NT>(red, acc, lane);
-    __syncthreads();
+    sk_reduce_lds<MT, NT, WAVES>(red, acc, lane, threadIdx.x >> 6);
     if (EPI == MOE_EPI_SWIGLU) {
       constexpr int HB = BN / 2;
       for (int q = threadIdx.x; q < rows * HB; q += NTHR) {

@@ -63,16 +63,27 @@ __device__ __forceinline__ void sk_mainloop(f32x4 (&acc)[MT][NT], const bf16* co
 }
 
 // Sum the 8 waves' partial tiles into red[BM][BN] (zeroed beforehand) with LDS float atomics.
-template <int MT, int NT>
-__device__ __forceinline__ void sk_reduce_lds(float* red, const f32x4 (&acc)[MT][NT], int lane) {
+// Sum of the WAVES waves' partial tiles (each wave ran a K slice) into red (zeroed by the caller,
+// behind a barrier), wave 0 first, then 1, ...: a fixed order, so the result is the same on every
+// run.  (LDS atomicAdd summed them in arrival order: the MoE expert GEMM's bf16 outputs changed
+// from run to run, and a pipeline over Mixtral-dims stages disagreed with itself.)  Ends behind a
+// barrier.
+template <int MT, int NT, int WAVES>
+__device__ __forceinline__ void sk_reduce_lds(float* red, const f32x4 (&acc)[MT][NT], int lane, int wv) {
   constexpr int BN = NT * 16;
   const int r = lane & 15, g = lane >> 4;
+#pragma unroll 1
+  for (int w = 0; w < WAVES; ++w) {
+    if (wv == w) {
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+        for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(&red[(mt * 16 + 4 * g + i) * BN + nt * 16 + r], acc[mt][nt][i]);
+          for (int i = 0; i < 4; ++i) red[(mt * 16 + 4 * g + i) * BN + nt * 16 + r] += acc[mt][nt][i];
+    }
+    __syncthreads();
+  }
 }
 
 }  // namespace dllm

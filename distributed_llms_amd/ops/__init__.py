@@ -345,6 +345,16 @@ def paged_attention_decode_rope(qkv, positions, cos_sin, k_cache, v_cache, slot_
     return out
 
 
+def prefill_attn_version(max_q_len: int, head_dim: int) -> int:
+    """The prefill attention kernel for a batch: knobs.prefill_attn, or with 0 (auto) the 32x32x16
+    pipelined kernel (7) from knobs.prefill_w32_min_q query rows at head_dim 128 -- 1.2-1.3x v4 on
+    1k-16k-token prompts -- and v4 below (256 x 128-token prompts: v4 182-190 us, v7 214-219)."""
+    v = knobs.K.prefill_attn
+    if v:
+        return v
+    return 7 if head_dim == 128 and max_q_len >= knobs.K.prefill_w32_min_q else 4
+
+
 def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, scale: float,
                             max_q_len: Optional[int] = None, version: int = 0, out: Optional[torch.Tensor] = None):
     """``version``: prefill kernel 3, 4, 6 or 7 (0: knobs.prefill_attn); ``out`` as paged_attention_decode."""
@@ -368,7 +378,8 @@ def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq
     _ext.kernels().paged_attention_prefill(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                            block_tables.data_ptr(), cu_seqlens_q.data_ptr(), seq_lens.data_ptr(),
                                            b, hq, k_cache.shape[1], d, k_cache.shape[2], block_tables.shape[1],
-                                           int(max_q_len), float(scale), version or knobs.K.prefill_attn, 0, 0, 0,
+                                           int(max_q_len), float(scale), version or prefill_attn_version(int(max_q_len), d),
+                                           0, 0, 0,
                                            _stream())
     return out
 
@@ -383,7 +394,7 @@ def prefill_rope_in_attention(max_blocks: Optional[int] = None) -> bool:
     must take ``rope_cache_append(write_q=True)`` + the plain prefill kernel instead."""
     if max_blocks is not None and max_blocks > PF_MAX_CHUNKS:
         return False
-    return knobs.K.prefill_fused_rope and knobs.K.prefill_attn in (4, 6, 7)
+    return knobs.K.prefill_fused_rope and knobs.K.prefill_attn in (0, 4, 6, 7)
 
 
 def paged_attention_prefill_rope(qkv, positions, cos_sin, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens,
@@ -410,7 +421,7 @@ def paged_attention_prefill_rope(qkv, positions, cos_sin, k_cache, v_cache, bloc
     if cos_sin is not None:
         _ck(cos_sin, "cos_sin", torch.float32)
     if not prefill_rope_in_attention(block_tables.shape[1]):
-        raise ValueError("in-kernel prefill RoPE needs an LDS prefill kernel (knobs.prefill_attn 4, 6 or 7) and "
+        raise ValueError("in-kernel prefill RoPE needs an LDS prefill kernel (knobs.prefill_attn 0, 4, 6 or 7) and "
                          f"block tables of <= {PF_MAX_CHUNKS} blocks")
     b = seq_lens.shape[0]
     if max_q_len is None:
@@ -420,7 +431,8 @@ def paged_attention_prefill_rope(qkv, positions, cos_sin, k_cache, v_cache, bloc
     _ext.kernels().paged_attention_prefill(out.data_ptr(), qkv.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                            block_tables.data_ptr(), cu_seqlens_q.data_ptr(), seq_lens.data_ptr(),
                                            b, num_heads, hkv, head_dim, k_cache.shape[2], block_tables.shape[1],
-                                           int(max_q_len), float(scale), knobs.K.prefill_attn, positions.data_ptr(),
+                                           int(max_q_len), float(scale), prefill_attn_version(int(max_q_len), head_dim),
+                                           positions.data_ptr(),
                                            0 if cos_sin is None else cos_sin.data_ptr(), width, _stream())
     return out
 
