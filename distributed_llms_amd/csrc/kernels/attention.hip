@@ -867,6 +867,43 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
   const bool ok = crow < ql;
   const int kmax_col = ok ? qpos0 + crow : -1;
   const int tok = qs + (ok ? crow : 0);
+  const int wg_kmax = qpos0 + min(wg_row0 + WV * R, ql) - 1;
+  const int nch = wg_kmax / kBS + 1;              // 32-key blocks the workgroup reads
+  const int ntile = (nch + 1) / 2;
+  const int wave_kmax = active ? qpos0 + min(row0 + R, ql) - 1 : -1;
+  const int wave_kmin = row0 + R <= ql ? qpos0 + row0 : -1;   // -1: a column past the sequence
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  const size_t head_off = (size_t)kvh * BLK;
+  const size_t blk_stride = (size_t)hkv * BLK;
+  // wave w stages 1 KiB pieces 4 w .. 4 w + 3 of tile t (block ids from id_of): pieces 0-7 K block
+  // 0, 8-15 K block 1, 16-23 V^T block 0, 24-31 V^T block 1 (a block past the sequence re-reads the
+  // last one: its keys are masked for every column)
+  auto stage = [&](int t, int buf, auto id_of) {
+    bf16* dst = smem + buf * TILE;
+#pragma unroll
+    for (int j = 0; j < GL; ++j) {
+      const int i = w * GL + j, part = i >> 3;
+      const int c = min(2 * t + (part & 1), nch - 1);
+      const size_t base = (size_t)id_of(c) * blk_stride + head_off;
+      const bf16* src;
+      if (part < 2) {
+        const int rr = (i & 7) * 4 + lane / 16, cs = lane % 16;
+        src = k_cache + base + (size_t)rr * D + (cs ^ (rr & 15)) * 8;
+      } else {
+        src = v_cache + base + (size_t)(i & 7) * 512 + lane * 8;
+      }
+      __builtin_amdgcn_global_load_lds((glb_vptr_a)src, (lds_vptr_a)(dst + i * 512), 16, 0, 0);
+    }
+  };
+  auto lds_id = [&](int c) { return ids[c]; };
+  // the first two tiles' K / V go out first, their block ids read straight from the table: with one
+  // workgroup per CU nothing else hides a workgroup's prologue, and the DMA no longer waits for the
+  // q loads, the rotation and the id staging in turn
+  {
+    auto table_id = [&](int c) { return bt[c]; };
+    stage(0, 0, table_id);
+    if (ntile > 1) stage(1, 1, table_id);
+  }
   // Q^T fragments (B operand): column m, dims 16 ks + 8 hi + 0..7; RoPE partners (d, d + 64) are
   // fragments ks and ks + 4 of the same lane
   bf16x8 qf[D / 16];
@@ -896,40 +933,13 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
       for (int ks = 0; ks < D / 16; ++ks) qf[ks] = bf16x8{};
     }
   }
-  const int wg_kmax = qpos0 + min(wg_row0 + WV * R, ql) - 1;
-  const int nch = wg_kmax / kBS + 1;              // 32-key blocks the workgroup reads
-  const int ntile = (nch + 1) / 2;
-  const int wave_kmax = active ? qpos0 + min(row0 + R, ql) - 1 : -1;
-  const int wave_kmin = row0 + R <= ql ? qpos0 + row0 : -1;   // -1: a column past the sequence
-  const int32_t* bt = block_tables + (size_t)b * max_blocks;
   for (int i = threadIdx.x; i < nch; i += WV * 64) ids[i] = bt[i];
-  // retire the q loads before the first LDS-DMA (a use inside the loop would wait vmcnt(0) there)
+  // retire the q loads (and with them the first tiles' DMA) here: a use inside the loop would wait
+  // vmcnt(0) there
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) asm volatile("" ::"v"(qf[ks]));
   __syncthreads();
 
-  const size_t head_off = (size_t)kvh * BLK;
-  const size_t blk_stride = (size_t)hkv * BLK;
-  // wave w stages 1 KiB pieces 4 w .. 4 w + 3 of tile t: pieces 0-7 K block 0, 8-15 K block 1,
-  // 16-23 V^T block 0, 24-31 V^T block 1 (a block past the sequence re-reads the last one: its keys
-  // are masked for every column)
-  auto stage = [&](int t, int buf) {
-    bf16* dst = smem + buf * TILE;
-#pragma unroll
-    for (int j = 0; j < GL; ++j) {
-      const int i = w * GL + j, part = i >> 3;
-      const int c = min(2 * t + (part & 1), nch - 1);
-      const size_t base = (size_t)ids[c] * blk_stride + head_off;
-      const bf16* src;
-      if (part < 2) {
-        const int rr = (i & 7) * 4 + lane / 16, cs = lane % 16;
-        src = k_cache + base + (size_t)rr * D + (cs ^ (rr & 15)) * 8;
-      } else {
-        src = v_cache + base + (size_t)(i & 7) * 512 + lane * 8;
-      }
-      __builtin_amdgcn_global_load_lds((glb_vptr_a)src, (lds_vptr_a)(dst + i * 512), 16, 0, 0);
-    }
-  };
   const int krow = w32_krow(m), kswz = krow & 15;
   f32x16 acc[D / 32];                             // O^T: dims 32 dt + 8 (r / 4) + 4 hi + r % 4, column m
 #pragma unroll
@@ -1006,8 +1016,6 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
     }
   };
 
-  stage(0, 0);
-  if (ntile > 1) stage(1, 1);
   // PIPE: the previous tile's P.V MFMAs go out right behind this tile's QK^T and run while the VALU
   // does this tile's softmax (MFMA and VALU are separate pipes; without it a wave's P.V waits for
   // its own softmax, and only the other wave on the SIMD can fill the gap).  The ring is one deeper:
@@ -1024,7 +1032,7 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
     asm volatile("" ::: "memory");
     // slot (t + 2) % NB was last read in iteration t - 1 (PIPE: t - 2's V^T in iteration t - 1), which
     // every wave finished before the barrier
-    if (t + 2 < ntile) stage(t + 2, (t + 2) % NB);
+    if (t + 2 < ntile) stage(t + 2, (t + 2) % NB, lds_id);
     const bf16* tb = smem + (t % NB) * TILE;
     const int k0 = t * TK;
     if constexpr (PIPE) {
