@@ -816,7 +816,7 @@ __device__ __forceinline__ float half_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-template <int G, bool PIPE>
+template <int G, int PIPE>
 __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
     bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
@@ -1024,6 +1024,12 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
   // accumulators see one straight-line path per iteration -- a skip path made hipcc copy all 64 of
   // them in and out of the tile code
   bf16x8 pbp[4] = {};                             // PIPE: P of the previous tile (zeros: a no-op P.V)
+  // PIPE 2: the previous tile's (masked) scores and the reference they are exponentiated against;
+  // -inf before the first tile, so that tile's "previous" P is exactly zero
+  f32x16 sp0, sp1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sp0[r] = sp1[r] = -INFINITY;
+  float mref_p = 0.f;
   int vprev = 0;                                  // PIPE: its ring slot
   for (int t = 0; t < ntile; ++t) {
     if (t + 1 < ntile) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -1035,7 +1041,88 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
     if (t + 2 < ntile) stage(t + 2, (t + 2) % NB, lds_id);
     const bf16* tb = smem + (t % NB) * TILE;
     const int k0 = t * TK;
-    if constexpr (PIPE) {
+    if constexpr (PIPE == 2) {
+      if (!active) continue;
+      // phase A: this tile's 16 QK^T MFMAs with the PREVIOUS tile's exponentials in their gaps (one
+      // score pair per gap: FMA, two exp, cvt, sum -- against that tile's reference mref_p)
+      auto kread = [&](int bb, int ks) {
+        return *reinterpret_cast<const bf16x8*>(tb + bb * BLK + krow * D + (((2 * ks + hi) ^ kswz) * 8));
+      };
+      f32x16 s0 = {}, s1 = {};
+      bf16x8 pb[4];
+      f32x2 sum2 = {0.f, 0.f};
+      const f32x2 mr2 = {-mref_p, -mref_p};
+      bf16x8 ka = kread(0, 0), kb = kread(1, 0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ks = i >> 1;
+        if ((i & 1) == 0) {
+          s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s0, 0, 0, 0);
+          if (ks + 1 < D / 16) ka = kread(0, ks + 1);
+        } else {
+          s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[ks], s1, 0, 0, 0);
+          if (ks + 1 < D / 16) kb = kread(1, ks + 1);
+        }
+        const f32x16& sv = i < 8 ? sp0 : sp1;
+        const int r = 2 * (i & 7);
+        const f32x2 x = __builtin_elementwise_fma(f32x2{sv[r], sv[r + 1]}, sc2, mr2);
+        const f32x2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+        sum2 += e;
+        pb[i >> 2][r & 7] = f2bf(e[0]);
+        pb[i >> 2][(r & 7) + 1] = f2bf(e[1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // pinned here, or hipcc sinks the exponentials (which need nothing from this phase) past the
+      // mask branch into phase B, next to their P.V use
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(pb[i]));
+      asm volatile("" : "+v"(sum2));
+      lsum += sum2[0] + sum2[1];                      // the previous tile's P, at its own scale
+      if (k0 + TK - 1 > wave_kmin) mask(s0, s1, k0);   // unmasked below every column's diagonal
+      // phase B: the previous tile's 16 P.V MFMAs with this tile's column max in their gaps
+      const bf16* vt = smem + vprev * TILE;
+      auto vread = [&](int i) {
+        const int dt = i & 3, bh = i >> 2;
+        return *reinterpret_cast<const bf16x8*>(vt + 2 * BLK + (bh >> 1) * BLK +
+                                                ((2 * (bh & 1) + hi) * D + 32 * dt + m) * 8);
+      };
+      bf16x8 va[4], vn[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) va[j] = vread(j);
+      float cmp[8], alpha = 1.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if ((i & 3) == 0 && i + 4 < 16) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vn[j] = vread(i + 4 + j);
+        }
+        acc[i & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[i & 3], pb[i >> 2], acc[i & 3], 0, 0, 0);
+        if ((i & 3) == 3 && i + 1 < 16) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) va[j] = vn[j];
+        }
+        if (i < 8) {
+          const f32x16& sv = i < 4 ? s0 : s1;
+          const int r = 4 * (i & 3);
+          cmp[i] = fmaxf(fmaxf(sv[r], sv[r + 1]), fmaxf(sv[r + 2], sv[r + 3]));
+        } else if (i == 8) {
+          const float cm = half_max(fmaxf(fmaxf(fmaxf(cmp[0], cmp[1]), fmaxf(cmp[2], cmp[3])),
+                                          fmaxf(fmaxf(cmp[4], cmp[5]), fmaxf(cmp[6], cmp[7])))) * scale_log2;
+          const float mn = fmaxf(mrun, cm);
+          mref_p = (mn == -INFINITY) ? 0.f : mn;
+          alpha = __builtin_amdgcn_exp2f(mrun - mref_p);
+          mrun = mn;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // acc now holds every earlier tile at the previous scale: move it (and the denominator) to this
+      // tile's reference; this tile's P is exponentiated next iteration, against mref_p
+      lsum *= alpha;
+      rescale(alpha);
+      sp0 = s0;
+      sp1 = s1;
+      vprev = t % NB;
+    } else if constexpr (PIPE == 1) {
       if (!active) continue;
       f32x16 s0, s1;
       qk(tb, s0, s1);
@@ -1112,7 +1199,24 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
       pv(tb, pb);
     }
   }
-  if (PIPE && active) pv(smem + vprev * TILE, pbp);
+  if (PIPE == 1 && active) pv(smem + vprev * TILE, pbp);
+  if (PIPE == 2 && active) {                      // the last tile's exponentials and P.V
+    bf16x8 pb[4];
+    f32x2 sum2 = {0.f, 0.f};
+    const f32x2 mr2 = {-mref_p, -mref_p};
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const f32x16& sv = p < 8 ? sp0 : sp1;
+      const int r = 2 * (p & 7);
+      const f32x2 x = __builtin_elementwise_fma(f32x2{sv[r], sv[r + 1]}, sc2, mr2);
+      const f32x2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+      sum2 += e;
+      pb[p >> 2][r & 7] = f2bf(e[0]);
+      pb[p >> 2][(r & 7) + 1] = f2bf(e[1]);
+    }
+    lsum += sum2[0] + sum2[1];
+    pv(smem + vprev * TILE, pb);
+  }
   const float lt = half_sum(lsum);
   // output through a wave-private LDS image (the ring is free once every wave is past its last
   // tile): whole 16-byte pieces of a column per store, G heads of a row contiguous -- whole lines
@@ -1225,7 +1329,8 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
                            int hq, int max_blocks, float sl2, uintptr_t pos, uintptr_t cs, int q_stride) {
   // version 3: the register-tiled kernel, two tiles per wave; 4: the LDS-shared kernel, two tiles per
   // wave; 6: the LDS-shared kernel on 32x32x16 MFMAs, 8 waves x 32 columns (head_dim 128); 7: 6 with
-  // the previous tile's P.V overlapping this tile's softmax
+  // the previous tile's P.V overlapping this tile's softmax; 8: three phases, this tile's QK^T
+  // overlapping the previous tile's exponentials and its P.V this tile's max
   const int nt = 2;
   const int rows_per_wg = version >= 6 ? kW32Waves * (32 / g) : kWaves * (16 / g) * nt;
   const dim3 grid((max_q_len + rows_per_wg - 1) / rows_per_wg, hkv, batch);
@@ -1233,7 +1338,8 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
   do {                                                                                                      \
     if (version >= 6) {                                                                                     \
       if constexpr (D == 128) {                                                                             \
-        auto kern = version == 7 ? attn_prefill_w32_kernel<GG, true> : attn_prefill_w32_kernel<GG, false>;   \
+        auto kern = version == 8 ? attn_prefill_w32_kernel<GG, 2>                                           \
+                    : version == 7 ? attn_prefill_w32_kernel<GG, 1> : attn_prefill_w32_kernel<GG, 0>;       \
         hipLaunchKernelGGL(kern, grid, dim3(kW32Waves * 64), 0, s, (bf16*)out, (const bf16*)q,                \
                            (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,                    \
                            (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2,                 \
@@ -1279,7 +1385,7 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
   // version (knobs.prefill_attn): 4 = the LDS-shared kernel (default; bench/prefill_attn_bench.py:
   // 1.6-1.7x v3 from 128- to 8192-token prompts); 3 = the register-tiled kernel, which also serves
   // block tables wider than the 32k tokens of block ids the LDS kernel stages
-  DLLM_HOST_CHECK(version == 3 || version == 4 || version == 6 || version == 7, "prefill attention version 3, 4, 6 or 7");
+  DLLM_HOST_CHECK(version == 3 || version == 4 || (version >= 6 && version <= 8), "prefill attention version 3, 4, 6, 7 or 8");
   if (version >= 6 && (d != 128 || G > 16)) version = 4;           // the 32x32 kernels: head_dim 128, G | 32
   if (version != 3 && max_blocks > kPfMaxChunks) version = 3;
   DLLM_HOST_CHECK(q_stride == hq * d || version != 3, "in-kernel RoPE / strided q: LDS kernels only (<= 32k context)");
