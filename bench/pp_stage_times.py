@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import torch
 
-from distributed_llms_amd.config import EngineConfig
+from distributed_llms_amd.config import EngineConfig, get_model_config
 from distributed_llms_amd.engine.batch import build_host_batch
 from distributed_llms_amd.engine.llm_engine import build_stage, make_block_manager
 from distributed_llms_amd.engine.runner import StageRunner
@@ -28,16 +28,19 @@ from distributed_llms_amd.engine.sequence import SamplingParams, Sequence
 from distributed_llms_amd.parallel.planner import plan_units
 
 
-def decode_batch(ecfg, batch, ctx, nb):
+def decode_batch(ecfg, batch, ctx, nb, vocab=32000):
     """A decode HostBatch of ``batch`` sequences whose context reaches ``ctx`` (bookkeeping only:
-    the prefill is scheduled and completed on the host, its KV left as allocated)."""
+    the prefill is scheduled and completed on the host, its KV left as allocated).  The decode
+    step's input ids are random: with one shared id every sequence's first-stage activations are
+    identical, and an MoE router sends the whole batch to the same two experts -- the first stage
+    of Mixtral then streamed a quarter of the expert weights of the others and timed 0.57x."""
     bm = make_block_manager(nb, ecfg.kv_block_size)
     sch = Scheduler(bm, 1, batch, batch * ctx, ecfg.max_seq_len)
     for _ in range(batch):
         sch.add(Sequence([7] * (ctx - 1), SamplingParams(max_new_tokens=64, ignore_eos=True)))
     step = sch.schedule(0)
     assert step.is_prefill and step.size == batch
-    sch.complete(step, np.full(batch, 11, dtype=np.int32), 0.0)
+    sch.complete(step, np.random.default_rng(0).integers(3, vocab, batch).astype(np.int32), 0.0)
     step = sch.schedule(0)
     assert not step.is_prefill
     return build_host_batch(step, bm, ecfg.kv_block_size, -(-ecfg.max_seq_len // ecfg.kv_block_size), 1)
@@ -81,7 +84,7 @@ def main():
                         dtype="bfloat16" if a.device != "cpu" else "float32")
     cfg = ecfg.model_config()
     nb = a.batch * -(-(a.ctx + 64) // ecfg.kv_block_size) + 2
-    hb = decode_batch(ecfg, a.batch, a.ctx, nb)
+    hb = decode_batch(ecfg, a.batch, a.ctx, nb, vocab=get_model_config(a.model).vocab_size)
     for pp in a.pp:
         for fine in (False, True):
             plan = plan_units(cfg, pp, batch=a.batch, ctx=a.ctx, device="cuda", fine=fine)

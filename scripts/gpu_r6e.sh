@@ -29,5 +29,5 @@ else
   # stage-balance tables: every stage of the plan built and timed one at a time (decode graph replay)
   $T 400 python -u bench/pp_stage_times.py --model llama3-70b --pp 4 8 --batch 64 > gpurun_out/r6e_stages_70b.txt 2>&1 || { tail -30 gpurun_out/r6e_stages_70b.txt; exit 1; }
   $T 300 python -u bench/pp_stage_times.py --model mixtral-8x7b --pp 4 --batch 128 > gpurun_out/r6e_stages_mixtral.txt 2>&1 || { tail -30 gpurun_out/r6e_stages_mixtral.txt; exit 1; }
-  tail -12 gpurun_out/r6e_stages_70b.txt gpurun_out/r6e_stages_mixtral.txt
+  tail -n 12 gpurun_out/r6e_stages_70b.txt gpurun_out/r6e_stages_mixtral.txt
 fi

@@ -26,3 +26,6 @@ for v in v8 new v8 new; do
 done
 use v8
 grep -v amdgpu.ids gpurun_out/r6i_pattn.txt
+# Mixtral stage balance again, decode ids now random (bench/pp_stage_times.py decode_batch)
+timeout -k 10 300 python -u bench/pp_stage_times.py --model mixtral-8x7b --pp 4 --batch 128 > gpurun_out/r6i_stages_mixtral.txt 2>&1 || { tail -n 30 gpurun_out/r6i_stages_mixtral.txt; exit 1; }
+tail -n 6 gpurun_out/r6i_stages_mixtral.txt
