@@ -816,7 +816,7 @@ __device__ __forceinline__ float half_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-template <int G, int PIPE>
+template <int G, bool PIPE>
 __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
     bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
@@ -867,43 +867,6 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
   const bool ok = crow < ql;
   const int kmax_col = ok ? qpos0 + crow : -1;
   const int tok = qs + (ok ? crow : 0);
-  const int wg_kmax = qpos0 + min(wg_row0 + WV * R, ql) - 1;
-  const int nch = wg_kmax / kBS + 1;              // 32-key blocks the workgroup reads
-  const int ntile = (nch + 1) / 2;
-  const int wave_kmax = active ? qpos0 + min(row0 + R, ql) - 1 : -1;
-  const int wave_kmin = row0 + R <= ql ? qpos0 + row0 : -1;   // -1: a column past the sequence
-  const int32_t* bt = block_tables + (size_t)b * max_blocks;
-  const size_t head_off = (size_t)kvh * BLK;
-  const size_t blk_stride = (size_t)hkv * BLK;
-  // wave w stages 1 KiB pieces 4 w .. 4 w + 3 of tile t (block ids from id_of): pieces 0-7 K block
-  // 0, 8-15 K block 1, 16-23 V^T block 0, 24-31 V^T block 1 (a block past the sequence re-reads the
-  // last one: its keys are masked for every column)
-  auto stage = [&](int t, int buf, auto id_of) {
-    bf16* dst = smem + buf * TILE;
-#pragma unroll
-    for (int j = 0; j < GL; ++j) {
-      const int i = w * GL + j, part = i >> 3;
-      const int c = min(2 * t + (part & 1), nch - 1);
-      const size_t base = (size_t)id_of(c) * blk_stride + head_off;
-      const bf16* src;
-      if (part < 2) {
-        const int rr = (i & 7) * 4 + lane / 16, cs = lane % 16;
-        src = k_cache + base + (size_t)rr * D + (cs ^ (rr & 15)) * 8;
-      } else {
-        src = v_cache + base + (size_t)(i & 7) * 512 + lane * 8;
-      }
-      __builtin_amdgcn_global_load_lds((glb_vptr_a)src, (lds_vptr_a)(dst + i * 512), 16, 0, 0);
-    }
-  };
-  auto lds_id = [&](int c) { return ids[c]; };
-  // the first two tiles' K / V go out first, their block ids read straight from the table: with one
-  // workgroup per CU nothing else hides a workgroup's prologue, and the DMA no longer waits for the
-  // q loads, the rotation and the id staging in turn
-  {
-    auto table_id = [&](int c) { return bt[c]; };
-    stage(0, 0, table_id);
-    if (ntile > 1) stage(1, 1, table_id);
-  }
   // Q^T fragments (B operand): column m, dims 16 ks + 8 hi + 0..7; RoPE partners (d, d + 64) are
   // fragments ks and ks + 4 of the same lane
   bf16x8 qf[D / 16];
@@ -933,13 +896,40 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
       for (int ks = 0; ks < D / 16; ++ks) qf[ks] = bf16x8{};
     }
   }
+  const int wg_kmax = qpos0 + min(wg_row0 + WV * R, ql) - 1;
+  const int nch = wg_kmax / kBS + 1;              // 32-key blocks the workgroup reads
+  const int ntile = (nch + 1) / 2;
+  const int wave_kmax = active ? qpos0 + min(row0 + R, ql) - 1 : -1;
+  const int wave_kmin = row0 + R <= ql ? qpos0 + row0 : -1;   // -1: a column past the sequence
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
   for (int i = threadIdx.x; i < nch; i += WV * 64) ids[i] = bt[i];
-  // retire the q loads (and with them the first tiles' DMA) here: a use inside the loop would wait
-  // vmcnt(0) there
+  // retire the q loads before the first LDS-DMA (a use inside the loop would wait vmcnt(0) there)
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) asm volatile("" ::"v"(qf[ks]));
   __syncthreads();
 
+  const size_t head_off = (size_t)kvh * BLK;
+  const size_t blk_stride = (size_t)hkv * BLK;
+  // wave w stages 1 KiB pieces 4 w .. 4 w + 3 of tile t: pieces 0-7 K block 0, 8-15 K block 1,
+  // 16-23 V^T block 0, 24-31 V^T block 1 (a block past the sequence re-reads the last one: its keys
+  // are masked for every column)
+  auto stage = [&](int t, int buf) {
+    bf16* dst = smem + buf * TILE;
+#pragma unroll
+    for (int j = 0; j < GL; ++j) {
+      const int i = w * GL + j, part = i >> 3;
+      const int c = min(2 * t + (part & 1), nch - 1);
+      const size_t base = (size_t)ids[c] * blk_stride + head_off;
+      const bf16* src;
+      if (part < 2) {
+        const int rr = (i & 7) * 4 + lane / 16, cs = lane % 16;
+        src = k_cache + base + (size_t)rr * D + (cs ^ (rr & 15)) * 8;
+      } else {
+        src = v_cache + base + (size_t)(i & 7) * 512 + lane * 8;
+      }
+      __builtin_amdgcn_global_load_lds((glb_vptr_a)src, (lds_vptr_a)(dst + i * 512), 16, 0, 0);
+    }
+  };
   const int krow = w32_krow(m), kswz = krow & 15;
   f32x16 acc[D / 32];                             // O^T: dims 32 dt + 8 (r / 4) + 4 hi + r % 4, column m
 #pragma unroll
@@ -1016,6 +1006,8 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
     }
   };
 
+  stage(0, 0);
+  if (ntile > 1) stage(1, 1);
   // PIPE: the previous tile's P.V MFMAs go out right behind this tile's QK^T and run while the VALU
   // does this tile's softmax (MFMA and VALU are separate pipes; without it a wave's P.V waits for
   // its own softmax, and only the other wave on the SIMD can fill the gap).  The ring is one deeper:
@@ -1024,12 +1016,6 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
   // accumulators see one straight-line path per iteration -- a skip path made hipcc copy all 64 of
   // them in and out of the tile code
   bf16x8 pbp[4] = {};                             // PIPE: P of the previous tile (zeros: a no-op P.V)
-  // PIPE 2: the previous tile's (masked) scores and the reference they are exponentiated against;
-  // -inf before the first tile, so that tile's "previous" P is exactly zero
-  f32x16 sp0, sp1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) sp0[r] = sp1[r] = -INFINITY;
-  float mref_p = 0.f;
   int vprev = 0;                                  // PIPE: its ring slot
   for (int t = 0; t < ntile; ++t) {
     if (t + 1 < ntile) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -1038,91 +1024,10 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
     asm volatile("" ::: "memory");
     // slot (t + 2) % NB was last read in iteration t - 1 (PIPE: t - 2's V^T in iteration t - 1), which
     // every wave finished before the barrier
-    if (t + 2 < ntile) stage(t + 2, (t + 2) % NB, lds_id);
+    if (t + 2 < ntile) stage(t + 2, (t + 2) % NB);
     const bf16* tb = smem + (t % NB) * TILE;
     const int k0 = t * TK;
-    if constexpr (PIPE == 2) {
-      if (!active) continue;
-      // phase A: this tile's 16 QK^T MFMAs with the PREVIOUS tile's exponentials in their gaps (one
-      // score pair per gap: FMA, two exp, cvt, sum -- against that tile's reference mref_p)
-      auto kread = [&](int bb, int ks) {
-        return *reinterpret_cast<const bf16x8*>(tb + bb * BLK + krow * D + (((2 * ks + hi) ^ kswz) * 8));
-      };
-      f32x16 s0 = {}, s1 = {};
-      bf16x8 pb[4];
-      f32x2 sum2 = {0.f, 0.f};
-      const f32x2 mr2 = {-mref_p, -mref_p};
-      bf16x8 ka = kread(0, 0), kb = kread(1, 0);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int ks = i >> 1;
-        if ((i & 1) == 0) {
-          s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s0, 0, 0, 0);
-          if (ks + 1 < D / 16) ka = kread(0, ks + 1);
-        } else {
-          s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[ks], s1, 0, 0, 0);
-          if (ks + 1 < D / 16) kb = kread(1, ks + 1);
-        }
-        const f32x16& sv = i < 8 ? sp0 : sp1;
-        const int r = 2 * (i & 7);
-        const f32x2 x = __builtin_elementwise_fma(f32x2{sv[r], sv[r + 1]}, sc2, mr2);
-        const f32x2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
-        sum2 += e;
-        pb[i >> 2][r & 7] = f2bf(e[0]);
-        pb[i >> 2][(r & 7) + 1] = f2bf(e[1]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // pinned here, or hipcc sinks the exponentials (which need nothing from this phase) past the
-      // mask branch into phase B, next to their P.V use
-#pragma unroll
-      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(pb[i]));
-      asm volatile("" : "+v"(sum2));
-      lsum += sum2[0] + sum2[1];                      // the previous tile's P, at its own scale
-      if (k0 + TK - 1 > wave_kmin) mask(s0, s1, k0);   // unmasked below every column's diagonal
-      // phase B: the previous tile's 16 P.V MFMAs with this tile's column max in their gaps
-      const bf16* vt = smem + vprev * TILE;
-      auto vread = [&](int i) {
-        const int dt = i & 3, bh = i >> 2;
-        return *reinterpret_cast<const bf16x8*>(vt + 2 * BLK + (bh >> 1) * BLK +
-                                                ((2 * (bh & 1) + hi) * D + 32 * dt + m) * 8);
-      };
-      bf16x8 va[4], vn[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) va[j] = vread(j);
-      float cmp[8], alpha = 1.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if ((i & 3) == 0 && i + 4 < 16) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) vn[j] = vread(i + 4 + j);
-        }
-        acc[i & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[i & 3], pb[i >> 2], acc[i & 3], 0, 0, 0);
-        if ((i & 3) == 3 && i + 1 < 16) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) va[j] = vn[j];
-        }
-        if (i < 8) {
-          const f32x16& sv = i < 4 ? s0 : s1;
-          const int r = 4 * (i & 3);
-          cmp[i] = fmaxf(fmaxf(sv[r], sv[r + 1]), fmaxf(sv[r + 2], sv[r + 3]));
-        } else if (i == 8) {
-          const float cm = half_max(fmaxf(fmaxf(fmaxf(cmp[0], cmp[1]), fmaxf(cmp[2], cmp[3])),
-                                          fmaxf(fmaxf(cmp[4], cmp[5]), fmaxf(cmp[6], cmp[7])))) * scale_log2;
-          const float mn = fmaxf(mrun, cm);
-          mref_p = (mn == -INFINITY) ? 0.f : mn;
-          alpha = __builtin_amdgcn_exp2f(mrun - mref_p);
-          mrun = mn;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // acc now holds every earlier tile at the previous scale: move it (and the denominator) to this
-      // tile's reference; this tile's P is exponentiated next iteration, against mref_p
-      lsum *= alpha;
-      rescale(alpha);
-      sp0 = s0;
-      sp1 = s1;
-      vprev = t % NB;
-    } else if constexpr (PIPE == 1) {
+    if constexpr (PIPE) {
       if (!active) continue;
       f32x16 s0, s1;
       qk(tb, s0, s1);
@@ -1199,24 +1104,7 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
       pv(tb, pb);
     }
   }
-  if (PIPE == 1 && active) pv(smem + vprev * TILE, pbp);
-  if (PIPE == 2 && active) {                      // the last tile's exponentials and P.V
-    bf16x8 pb[4];
-    f32x2 sum2 = {0.f, 0.f};
-    const f32x2 mr2 = {-mref_p, -mref_p};
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const f32x16& sv = p < 8 ? sp0 : sp1;
-      const int r = 2 * (p & 7);
-      const f32x2 x = __builtin_elementwise_fma(f32x2{sv[r], sv[r + 1]}, sc2, mr2);
-      const f32x2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
-      sum2 += e;
-      pb[p >> 2][r & 7] = f2bf(e[0]);
-      pb[p >> 2][(r & 7) + 1] = f2bf(e[1]);
-    }
-    lsum += sum2[0] + sum2[1];
-    pv(smem + vprev * TILE, pb);
-  }
+  if (PIPE && active) pv(smem + vprev * TILE, pbp);
   const float lt = half_sum(lsum);
   // output through a wave-private LDS image (the ring is free once every wave is past its last
   // tile): whole 16-byte pieces of a column per store, G heads of a row contiguous -- whole lines
@@ -1329,8 +1217,7 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
                            int hq, int max_blocks, float sl2, uintptr_t pos, uintptr_t cs, int q_stride) {
   // version 3: the register-tiled kernel, two tiles per wave; 4: the LDS-shared kernel, two tiles per
   // wave; 6: the LDS-shared kernel on 32x32x16 MFMAs, 8 waves x 32 columns (head_dim 128); 7: 6 with
-  // the previous tile's P.V overlapping this tile's softmax; 8: three phases, this tile's QK^T
-  // overlapping the previous tile's exponentials and its P.V this tile's max
+  // the previous tile's P.V overlapping this tile's softmax
   const int nt = 2;
   const int rows_per_wg = version >= 6 ? kW32Waves * (32 / g) : kWaves * (16 / g) * nt;
   const dim3 grid((max_q_len + rows_per_wg - 1) / rows_per_wg, hkv, batch);
@@ -1338,8 +1225,7 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
   do {                                                                                                      \
     if (version >= 6) {                                                                                     \
       if constexpr (D == 128) {                                                                             \
-        auto kern = version == 8 ? attn_prefill_w32_kernel<GG, 2>                                           \
-                    : version == 7 ? attn_prefill_w32_kernel<GG, 1> : attn_prefill_w32_kernel<GG, 0>;       \
+        auto kern = version == 7 ? attn_prefill_w32_kernel<GG, true> : attn_prefill_w32_kernel<GG, false>;   \
         hipLaunchKernelGGL(kern, grid, dim3(kW32Waves * 64), 0, s, (bf16*)out, (const bf16*)q,                \
                            (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,                    \
                            (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2,                 \
@@ -1385,7 +1271,7 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
   // version (knobs.prefill_attn): 4 = the LDS-shared kernel (default; bench/prefill_attn_bench.py:
   // 1.6-1.7x v3 from 128- to 8192-token prompts); 3 = the register-tiled kernel, which also serves
   // block tables wider than the 32k tokens of block ids the LDS kernel stages
-  DLLM_HOST_CHECK(version == 3 || version == 4 || (version >= 6 && version <= 8), "prefill attention version 3, 4, 6, 7 or 8");
+  DLLM_HOST_CHECK(version == 3 || version == 4 || version == 6 || version == 7, "prefill attention version 3, 4, 6 or 7");
   if (version >= 6 && (d != 128 || G > 16)) version = 4;           // the 32x32 kernels: head_dim 128, G | 32
   if (version != 3 && max_blocks > kPfMaxChunks) version = 3;
   DLLM_HOST_CHECK(q_stride == hq * d || version != 3, "in-kernel RoPE / strided q: LDS kernels only (<= 32k context)");
