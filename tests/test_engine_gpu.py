@@ -117,6 +117,31 @@ def test_chunked_prefill_gpu_matches_cpu_logits(cuda, name, attn):
     torch.testing.assert_close(logits[1], logits[0], atol=6e-2, rtol=5e-2)
 
 
+def test_long_prompt_prefill_default_kernel_matches_cpu_logits(cuda):
+    """The default prefill attention choice (knobs.prefill_attn = 0: the 32x32x16 pipelined kernel
+    from 512 query rows at head_dim 128) on a 600-token prompt prefilled in one step, with the
+    q-RoPE inside the kernel: logits vs the CPU fp32 prefill."""
+    from distributed_llms_amd import knobs, ops
+    name = "tiny-llama-d128"
+    cfg = get_model_config(name)
+    assert ops.prefill_attn_version(600, cfg.head_dim) == 7 and knobs.K.prefill_attn == 0
+    sd = W.synth_hf_state_dict(cfg, seed=6, dtype=torch.float32)
+    prompt = [(17 * j) % 450 + 5 for j in range(600)]
+    e_cpu = LLMEngine(EngineConfig(model=name, dtype="float32", device="cpu", max_batch=2, max_seq_len=1024,
+                                   use_graphs=False),
+                      ModelStage(cfg, 0, cfg.num_layers, "cpu", torch.float32).load_hf_state(sd))
+    e_gpu = LLMEngine(EngineConfig(model=name, dtype="bfloat16", device="cuda", max_batch=2, max_seq_len=1024,
+                                   use_graphs=False, num_kv_blocks=64, max_prefill_tokens=1024),
+                      ModelStage(cfg, 0, cfg.num_layers, "cuda", torch.bfloat16).load_hf_state(sd))
+    logits = []
+    for eng in (e_cpu, e_gpu):
+        eng.add_request(prompt, SamplingParams(max_new_tokens=1))
+        st = eng.scheduler.schedule(0)
+        assert st.is_prefill and st.seqs[0].chunk == 0            # the whole prompt in one step
+        logits.append(eng.runner.execute(build_host_batch(st, eng.bm, 32)).float().cpu())
+    torch.testing.assert_close(logits[1], logits[0], atol=6e-2, rtol=5e-2)
+
+
 def test_mixed_prefill_decode_steps_gpu(cuda):
     """Arrivals during decode ride along with the running rows (mixed steps, eager prefill path with
     split decode / prefill attention) on the HIP kernels.  Batch composition changes the GEMMs'
