@@ -6,6 +6,12 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T="timeout -k 10"
+$T 600 python -u -m pytest -v --timeout 240 --timeout-method thread tests/test_engine_gpu.py tests/test_kernels_gpu.py \
+  -m gpu > gpurun_out/r6z_tests.txt 2>&1
+rc=$?
+tail -n 3 gpurun_out/r6z_tests.txt
+grep FAILED gpurun_out/r6z_tests.txt | head
+[ $rc -gt 1 ] && exit $rc
 $T 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r6z_smoke.txt 2>&1 || { tail -20 gpurun_out/r6z_smoke.txt; exit 1; }
 tail -1 gpurun_out/r6z_smoke.txt
 for i in 1 2; do
