@@ -56,6 +56,18 @@ def test_argmax(cuda, rows, vocab):
     torch.testing.assert_close(ops.argmax(logits), expect)
 
 
+@pytest.mark.parametrize("rows,vocab", [(256, 128256), (3, 50257)])
+def test_argmax_ties_take_the_first_index(cuda, rows, vocab):
+    """Coarse logits (many equal maxima per row, spread over every thread's strided scan), an
+    all-equal row and a row whose maximum sits in the ragged tail: the first maximal index, as torch."""
+    logits = (_bf(rows, vocab, scale=3.0).float().round()).to(torch.bfloat16)
+    logits[0] = 1.0
+    logits[-1, :] = -5.0
+    logits[-1, vocab - 3:] = 7.0
+    expect = logits.float().argmax(-1).to(torch.int32)
+    torch.testing.assert_close(ops.argmax(logits), expect)
+
+
 def _cache(nb, hkv, d, bs=32):
     k = torch.zeros(nb, hkv, bs, d, dtype=torch.bfloat16, device="cuda")
     v = torch.zeros(nb, hkv, d, bs, dtype=torch.bfloat16, device="cuda")
