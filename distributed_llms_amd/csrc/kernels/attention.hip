@@ -1136,6 +1136,324 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Prefill v9: v7 made persistent.  A fit of v7's times from 128- to 16k-token prompts gives ~12 us
+// per 64-row workgroup on top of the streaming work (prologue, first-tile latency, output), and with
+// one 8-wave workgroup per CU nothing else runs meanwhile.  Here one workgroup per CU walks row tiles
+// ("items") of its XCD's (sequence, kv head) groups -- group g on XCD g % 8, as v7's order -- in a
+// snake over heavy-first order (round r of the XCD's PX workgroups runs left to right, r + 1 right to
+// left: a workgroup's heavy and light row tiles pair up).  The LDS ring runs on a global tile count
+// across items: the next item's first two K / V tiles are staged under the current item's last two
+// (their block ids straight from the table), so an item starts on landed data; its q loads and the
+// previous item's output stores are the only latency left at a switch.  Output goes straight from
+// the accumulators (the ring is busy): the two half-waves swap dword pairs with v_permlane32_swap so
+// that every lane stores 16 contiguous bytes of its column.
+// ---------------------------------------------------------------------------
+template <int G>
+__global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
+    bf16* __restrict__ out, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
+    const int32_t* __restrict__ cu_seqlens_q, const int32_t* __restrict__ seq_lens, int hq, int hkv,
+    int max_blocks, float scale_log2, const int32_t* __restrict__ positions, const float* __restrict__ cos_sin,
+    int q_stride, int nx, int ngroups) {
+  constexpr int D = 128;
+  constexpr int WV = kW32Waves;
+  constexpr int R = 32 / G;                       // query rows per wave
+  constexpr int RWG = WV * R;                     // query rows per item
+  constexpr int TK = 2 * kBS;
+  constexpr int BLK = kBS * D;
+  constexpr int TILE = 4 * BLK;
+  constexpr int NB = 4;
+  constexpr int GL = TILE / 512 / WV;
+  static_assert(GL == 4 && 32 % G == 0, "tile pieces / column tiling");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NB * TILE + 2 * kPfMaxChunks];
+  int* ids = reinterpret_cast<int*>(smem + NB * TILE);
+
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m = lane & 31, hi = lane >> 5;
+  const int xcd = blockIdx.x & 7, wx = blockIdx.x >> 3, PX = gridDim.x >> 3;
+  const int gx = ngroups > xcd ? (ngroups - 1 - xcd) / 8 + 1 : 0;   // groups on this XCD
+  const int nitems = gx * nx;
+
+  struct Item {
+    int b, kvh, qs, ql, qpos0, row0, ntile, nch;
+    int bid[4];                                   // block ids of tiles 0 / 1 (scalar loads)
+  };
+  // r-th item of this workgroup (snake over rounds); false past the end
+  auto pos_of = [&](int r) { return r * PX + ((r & 1) ? PX - 1 - wx : wx); };
+  auto load_item = [&](int p, Item& it) {
+    const int gi = p / nx, qt = nx - 1 - p % nx;
+    const int g = xcd + 8 * gi;
+    it.b = g / hkv;
+    it.kvh = g % hkv;
+    it.qs = cu_seqlens_q[it.b];
+    it.ql = cu_seqlens_q[it.b + 1] - it.qs;
+    it.row0 = qt * RWG;
+    const int ctx = seq_lens[it.b];
+    it.qpos0 = ctx - it.ql;
+    const int kmax = it.qpos0 + min(it.row0 + RWG, it.ql) - 1;
+    it.nch = kmax / kBS + 1;
+    it.ntile = (it.nch + 1) / 2;
+    const int32_t* bt = block_tables + (size_t)it.b * max_blocks;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) it.bid[c] = bt[min(c, it.nch - 1)];
+    return it.row0 < it.ql;                       // rows past the sequence: an empty item
+  };
+  // the next non-empty item at or after round r: its round, or -1
+  auto next_item = [&](int r, Item& it) {
+    for (; pos_of(r) < nitems; ++r)
+      if (load_item(pos_of(r), it)) return r;
+    return -1;
+  };
+
+  Item cur, nxt;
+  int rc = next_item(0, cur);
+  if (rc < 0) return;                             // workgroup-uniform
+  int rn = next_item(rc + 1, nxt);
+
+  const size_t blk_stride = (size_t)hkv * BLK;
+  // stage local tile t of item it into ring slot buf; block ids of tiles 0 / 1 from the item's
+  // registers (its LDS ids are not written yet when they are staged), later ones from LDS.  (A
+  // select between a table pointer and an LDS pointer becomes a flat load, whose wait drains the
+  // DMA just issued.)
+  auto stage = [&](const Item& it, int t, int buf) {
+    bf16* dst = smem + buf * TILE;
+    const size_t head_off = (size_t)it.kvh * BLK;
+#pragma unroll
+    for (int j = 0; j < GL; ++j) {
+      const int i = w * GL + j, part = i >> 3;
+      const int c = min(2 * t + (part & 1), it.nch - 1);
+      int id;
+      if (t < 2) id = c == 0 ? it.bid[0] : c == 1 ? it.bid[1] : c == 2 ? it.bid[2] : it.bid[3];
+      else id = ids[c];
+      const size_t base = (size_t)id * blk_stride + head_off;
+      const bf16* src;
+      if (part < 2) {
+        const int rr = (i & 7) * 4 + lane / 16, cs = lane % 16;
+        src = k_cache + base + (size_t)rr * D + (cs ^ (rr & 15)) * 8;
+      } else {
+        src = v_cache + base + (size_t)(i & 7) * 512 + lane * 8;
+      }
+      __builtin_amdgcn_global_load_lds((glb_vptr_a)src, (lds_vptr_a)(dst + i * 512), 16, 0, 0);
+    }
+  };
+  // global tile gt + d, where cur's tile 0 is global tile g0: cur's, else nxt's, else none
+  int g0 = 0, staged = 0;                         // global tiles [0, staged) have been issued
+  auto stage_global = [&](int gidx) {
+    const int lt = gidx - g0;
+    if (lt < cur.ntile) {
+      stage(cur, lt, gidx % NB);
+    } else if (rn >= 0 && lt - cur.ntile < nxt.ntile) {
+      stage(nxt, lt - cur.ntile, gidx % NB);
+    } else {
+      return;
+    }
+    staged = gidx + 1;
+  };
+  stage_global(0);
+  stage_global(1);
+
+  const int krow = w32_krow(m), kswz = krow & 15;
+  const f32x2 sc2 = {scale_log2, scale_log2};
+  while (true) {
+    // ---- item prologue: this lane's column, q (rotated), LDS block ids of tiles >= 2
+    const int row0 = cur.row0 + w * R;
+    const bool active = row0 < cur.ql;
+    const int crow = row0 + m / G, ch = m % G;
+    const bool ok = crow < cur.ql;
+    const int kmax_col = ok ? cur.qpos0 + crow : -1;
+    const int tok = cur.qs + (ok ? crow : 0);
+    const int wave_kmin = row0 + R <= cur.ql ? cur.qpos0 + row0 : -1;
+    bf16x8 qf[D / 16];
+    {
+      const bf16* qrow = q + (size_t)tok * q_stride + (size_t)(cur.kvh * G + ch) * D + 8 * hi;
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qrow + 16 * ks);
+      if (cos_sin != nullptr) {
+        const float* cs = cos_sin + (size_t)positions[tok] * D + 8 * hi;
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) {
+          const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + 16 * ks);
+          const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + 16 * ks + 4);
+          const f32x4 s0 = *reinterpret_cast<const f32x4*>(cs + D / 2 + 16 * ks);
+          const f32x4 s1 = *reinterpret_cast<const f32x4*>(cs + D / 2 + 16 * ks + 4);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float c = j < 4 ? c0[j] : c1[j - 4], s = j < 4 ? s0[j] : s1[j - 4];
+            const float a = bf2f(qf[ks][j]), bq = bf2f(qf[ks + D / 32][j]);
+            qf[ks][j] = f2bf(__builtin_fmaf(a, c, -(bq * s)));
+            qf[ks + D / 32][j] = f2bf(__builtin_fmaf(bq, c, a * s));
+          }
+        }
+      }
+      if (!ok) {
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) qf[ks] = bf16x8{};
+      }
+    }
+    {
+      const int32_t* bt = block_tables + (size_t)cur.b * max_blocks;
+      for (int i = 2 * 2 + threadIdx.x; i < cur.nch; i += WV * 64) ids[i] = bt[i];   // tiles >= 2
+    }
+    // everything issued so far (q, ids, this item's first tiles, the previous item's stores) lands
+    // here: the tile loop's counted waits then see only its own LDS-DMA
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) asm volatile("" ::"v"(qf[ks]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    f32x16 acc[D / 32];
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) acc[dt] = f32x16{};
+    float mrun = -INFINITY, lsum = 0.f;
+    bf16x8 pbp[4] = {};
+    int vprev = g0 % NB;
+    for (int t = 0; t < cur.ntile; ++t) {
+      const int gidx = g0 + t;
+      if (staged > gidx + 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // ring slot (gidx + 2) % NB was last read in iteration gidx - 1 (its V^T), finished by every wave
+      if (staged == gidx + 2) stage_global(gidx + 2);
+      if (!active) continue;
+      const bf16* tb = smem + (gidx % NB) * TILE;
+      const int k0 = t * TK;
+      f32x16 s0 = {}, s1 = {};
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        const int slot = ((2 * ks + hi) ^ kswz) * 8;
+        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(tb + krow * D + slot);
+        const bf16x8 kb = *reinterpret_cast<const bf16x8*>(tb + BLK + krow * D + slot);
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s0, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[ks], s1, 0, 0, 0);
+      }
+      if (k0 + TK - 1 > wave_kmin) {
+        const int kl = kmax_col - k0 - 8 * hi;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = 16 * (r >> 3) + (r & 7);
+          s0[r] = key <= kl ? s0[r] : -INFINITY;
+          s1[r] = key + kBS <= kl ? s1[r] : -INFINITY;
+        }
+      }
+      const bf16* vt = smem + vprev * TILE;
+      auto vread = [&](int i) {
+        const int dt = i & 3, bh = i >> 2;
+        return *reinterpret_cast<const bf16x8*>(vt + 2 * BLK + (bh >> 1) * BLK +
+                                                ((2 * (bh & 1) + hi) * D + 32 * dt + m) * 8);
+      };
+      bf16x8 va[4], vn[4], pb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) va[j] = vread(j);
+      float cmp[4], alpha = 1.f, mref = 0.f;
+      f32x2 sum2 = {0.f, 0.f};
+      auto pair = [&](int p) {
+        const f32x16& sv = p < 8 ? s0 : s1;
+        const int r = 2 * (p & 7);
+        const f32x2 x = __builtin_elementwise_fma(f32x2{sv[r], sv[r + 1]}, sc2, f32x2{-mref, -mref});
+        const f32x2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+        sum2 += e;
+        pb[p >> 2][r & 7] = f2bf(e[0]);
+        pb[p >> 2][(r & 7) + 1] = f2bf(e[1]);
+      };
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {                // as v7: the previous tile's P.V under this softmax
+        if ((i & 3) == 0 && i + 4 < 16) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vn[j] = vread(i + 4 + j);
+        }
+        acc[i & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[i & 3], pbp[i >> 2], acc[i & 3], 0, 0, 0);
+        if ((i & 3) == 3 && i + 1 < 16) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) va[j] = vn[j];
+        }
+        if (i < 4) {
+          cmp[i] = fmaxf(fmaxf(fmaxf(s0[4 * i], s0[4 * i + 1]), fmaxf(s0[4 * i + 2], s0[4 * i + 3])),
+                         fmaxf(fmaxf(s1[4 * i], s1[4 * i + 1]), fmaxf(s1[4 * i + 2], s1[4 * i + 3])));
+        } else if (i == 4) {
+          const float cm = half_max(fmaxf(fmaxf(cmp[0], cmp[1]), fmaxf(cmp[2], cmp[3]))) * scale_log2;
+          const float mn = fmaxf(mrun, cm);
+          mref = (mn == -INFINITY) ? 0.f : mn;
+          alpha = __builtin_amdgcn_exp2f(mrun - mref);
+          mrun = mn;
+        } else if (i < 10) {
+          pair(2 * (i - 5));
+          pair(2 * (i - 5) + 1);
+        } else {
+          pair(i);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(pb[i]));
+      asm volatile("" : "+v"(sum2));
+      lsum = lsum * alpha + (sum2[0] + sum2[1]);
+      if (__any(alpha != 1.f)) {
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) acc[dt] *= alpha;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pbp[i] = pb[i];
+      vprev = gidx % NB;
+    }
+    if (active) {
+      // the last tile's P.V
+      const bf16* vt = smem + vprev * TILE;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+        for (int bh = 0; bh < 4; ++bh) {
+          const bf16x8 va = *reinterpret_cast<const bf16x8*>(
+              vt + 2 * BLK + (bh >> 1) * BLK + ((2 * (bh & 1) + hi) * D + 32 * dt + m) * 8);
+          acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pbp[bh], acc[dt], 0, 0, 0);
+        }
+      }
+      // output: lane (m, hi) holds dims 32 dt + 8 j + 4 hi + 0..3 of column m; for each pair of j
+      // (2p, 2p + 1) the half-waves swap one 8-byte quad (v_permlane32_swap: lanes 32-63 of the
+      // first operand <-> lanes 0-31 of the second), after which lane (m, hi) holds the 8 dims
+      // 32 dt + 8 (2p + hi) + 0..7: one 16-byte store
+      const float lt = half_sum(lsum);
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      bf16* orow = out + ((size_t)(cur.qs + (ok ? crow : 0)) * hq + cur.kvh * G + ch) * D;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          bf16x4 u0, u1;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            u0[i] = f2bf(acc[dt][4 * (2 * pp) + i] * inv);
+            u1[i] = f2bf(acc[dt][4 * (2 * pp + 1) + i] * inv);
+          }
+          typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+          u32x2v a = __builtin_bit_cast(u32x2v, u0), bb = __builtin_bit_cast(u32x2v, u1);
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(a[k], bb[k], false, false);
+            a[k] = sw[0];
+            bb[k] = sw[1];
+          }
+          typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+          const u32x4v o = {a[0], a[1], bb[0], bb[1]};
+          if (ok) *reinterpret_cast<u32x4v*>(orow + 32 * dt + 8 * (2 * pp + hi)) = o;
+        }
+      }
+    }
+    // ---- next item: its first tiles are staged (or in flight); move the window
+    if (rn < 0) break;
+    g0 += cur.ntile;
+    cur = nxt;
+    rc = rn;
+    rn = next_item(rc + 1, nxt);
+    while (staged < g0 + 2) {                       // an item shorter than two tiles left gaps
+      const int before = staged;
+      stage_global(staged);
+      if (staged == before) break;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ launchers
 static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr_t v_cache, uintptr_t block_tables,
                           uintptr_t seq_lens, uintptr_t part_o, uintptr_t part_ml, int batch, int hq, int hkv, int d,
@@ -1217,13 +1535,28 @@ static void launch_prefill(int g, int version, int max_q_len, int batch, int hkv
                            int hq, int max_blocks, float sl2, uintptr_t pos, uintptr_t cs, int q_stride) {
   // version 3: the register-tiled kernel, two tiles per wave; 4: the LDS-shared kernel, two tiles per
   // wave; 6: the LDS-shared kernel on 32x32x16 MFMAs, 8 waves x 32 columns (head_dim 128); 7: 6 with
-  // the previous tile's P.V overlapping this tile's softmax
+  // the previous tile's P.V overlapping this tile's softmax; 9: 7 persistent (one workgroup per CU)
   const int nt = 2;
   const int rows_per_wg = version >= 6 ? kW32Waves * (32 / g) : kWaves * (16 / g) * nt;
   const dim3 grid((max_q_len + rows_per_wg - 1) / rows_per_wg, hkv, batch);
+  // version 9 (persistent): one workgroup per CU, 8 XCDs
+  int cus = 0;
+  if (version == 9) {
+    int dev = 0;
+    DLLM_HIP_CHECK(hipGetDevice(&dev));
+    DLLM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    cus -= cus % 8;
+    DLLM_HOST_CHECK(cus >= 8, "persistent prefill attention: CU count");
+  }
 #define DLLM_PF(GG)                                                                                         \
   do {                                                                                                      \
-    if (version >= 6) {                                                                                     \
+    if (version == 9) {                                                                                     \
+      if constexpr (D == 128)                                                                               \
+        hipLaunchKernelGGL((attn_prefill_w32p_kernel<GG>), dim3(cus), dim3(kW32Waves * 64), 0, s, (bf16*)out, \
+                           (const bf16*)q, (const bf16*)k_cache, (const bf16*)v_cache, (const int32_t*)bt,    \
+                           (const int32_t*)cu, (const int32_t*)sl, hq, hkv, max_blocks, sl2,                 \
+                           (const int32_t*)pos, (const float*)cs, q_stride, (int)grid.x, batch * hkv);       \
+    } else if (version >= 6) {                                                                              \
       if constexpr (D == 128) {                                                                             \
         auto kern = version == 7 ? attn_prefill_w32_kernel<GG, true> : attn_prefill_w32_kernel<GG, false>;   \
         hipLaunchKernelGGL(kern, grid, dim3(kW32Waves * 64), 0, s, (bf16*)out, (const bf16*)q,                \
@@ -1271,7 +1604,8 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
   // version (knobs.prefill_attn): 4 = the LDS-shared kernel (default; bench/prefill_attn_bench.py:
   // 1.6-1.7x v3 from 128- to 8192-token prompts); 3 = the register-tiled kernel, which also serves
   // block tables wider than the 32k tokens of block ids the LDS kernel stages
-  DLLM_HOST_CHECK(version == 3 || version == 4 || version == 6 || version == 7, "prefill attention version 3, 4, 6 or 7");
+  DLLM_HOST_CHECK(version == 3 || version == 4 || version == 6 || version == 7 || version == 9,
+                  "prefill attention version 3, 4, 6, 7 or 9");
   if (version >= 6 && (d != 128 || G > 16)) version = 4;           // the 32x32 kernels: head_dim 128, G | 32
   if (version != 3 && max_blocks > kPfMaxChunks) version = 3;
   DLLM_HOST_CHECK(q_stride == hq * d || version != 3, "in-kernel RoPE / strided q: LDS kernels only (<= 32k context)");

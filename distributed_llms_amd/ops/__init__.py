@@ -357,7 +357,7 @@ def prefill_attn_version(max_q_len: int, head_dim: int) -> int:
 
 def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, scale: float,
                             max_q_len: Optional[int] = None, version: int = 0, out: Optional[torch.Tensor] = None):
-    """``version``: prefill kernel 3, 4, 6 or 7 (0: prefill_attn_version); ``out`` as paged_attention_decode."""
+    """``version``: prefill kernel 3, 4, 6, 7 or 9 (0: prefill_attn_version); ``out`` as paged_attention_decode."""
     if not _gpu(q):
         return _into(out, ref.paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens,
                                                       scale))
@@ -394,7 +394,7 @@ def prefill_rope_in_attention(max_blocks: Optional[int] = None) -> bool:
     must take ``rope_cache_append(write_q=True)`` + the plain prefill kernel instead."""
     if max_blocks is not None and max_blocks > PF_MAX_CHUNKS:
         return False
-    return knobs.K.prefill_fused_rope and knobs.K.prefill_attn in (0, 4, 6, 7)
+    return knobs.K.prefill_fused_rope and knobs.K.prefill_attn in (0, 4, 6, 7, 9)
 
 
 def paged_attention_prefill_rope(qkv, positions, cos_sin, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens,
@@ -421,7 +421,7 @@ def paged_attention_prefill_rope(qkv, positions, cos_sin, k_cache, v_cache, bloc
     if cos_sin is not None:
         _ck(cos_sin, "cos_sin", torch.float32)
     if not prefill_rope_in_attention(block_tables.shape[1]):
-        raise ValueError("in-kernel prefill RoPE needs an LDS prefill kernel (knobs.prefill_attn 0, 4, 6 or 7) and "
+        raise ValueError("in-kernel prefill RoPE needs an LDS prefill kernel (knobs.prefill_attn 0, 4, 6, 7 or 9) and "
                          f"block tables of <= {PF_MAX_CHUNKS} blocks")
     b = seq_lens.shape[0]
     if max_q_len is None:

@@ -86,7 +86,7 @@ def test_lookahead_decode_matches_synchronous(cuda, graphs):
     assert any(len(o) < n for o, n in zip(sync_e, lens)), "EOS never fired"
 
 
-@pytest.mark.parametrize("attn", [4, 6, 7])
+@pytest.mark.parametrize("attn", [4, 6, 7, 9])
 @pytest.mark.parametrize("name", ["tiny-llama-d128", "tiny-mixtral"])
 def test_chunked_prefill_gpu_matches_cpu_logits(cuda, name, attn):
     """A 300-token prompt prefilled in 64-token chunks on the GPU (each chunk's attention reads the

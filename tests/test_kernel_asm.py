@@ -129,3 +129,22 @@ def test_prefill_w32_kernels_keep_softmax_in_registers(attn_asm):
             assert fused[0].count("sched_barrier") >= 15 or fused[0].count("v_exp_f32") >= 32
             loop_movs = sum(b.count("v_mov_b64") for b in blocks if "v_mfma" in b or "v_exp" in b)
             assert loop_movs < 8, (name, loop_movs)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_prefill_persistent_kernel_stages_without_flat_loads(attn_asm):
+    """Version 9 (attn_prefill_w32p_kernel, v7 persistent): the same fused softmax / P.V block as v7,
+    no spills, and no flat loads -- a block id picked between the block table and the LDS id list
+    through one pointer compiles to flat_load_dword, whose wait (vmcnt(0) lgkmcnt(0)) drains the
+    LDS-DMA issued just before it, once per staged tile piece."""
+    names = re.findall(r"^(_ZN4dllm24attn_prefill_w32p_kernel\w+):", attn_asm, re.M)
+    assert len(names) == 5
+    for name in names:
+        body = _kernel_body(attn_asm, name)
+        meta = attn_asm[attn_asm.index(".amdhsa_kernel " + name):]
+        assert int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", meta).group(1)) == 0, name
+        assert "flat_load" not in body and "scratch_" not in body, name
+        blocks = re.split(r"\n(?=\.LBB\w+:|\s*; %bb)", body)
+        assert [b for b in blocks if b.count("v_exp_f32") >= 32 and b.count("v_mfma_f32_32x32x16_bf16") >= 16], name
+        loop_movs = sum(b.count("v_mov_b64") for b in blocks if "v_mfma" in b or "v_exp" in b)
+        assert loop_movs < 8, (name, loop_movs)

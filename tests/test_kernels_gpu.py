@@ -167,7 +167,7 @@ def test_paged_attention_decode_fused_rope(cuda, hq, hkv, d, lens, rope):
     torch.testing.assert_close(v1.float(), v2, atol=0, rtol=0)
 
 
-@pytest.mark.parametrize("version", ["3", "4", "6", "7"])
+@pytest.mark.parametrize("version", ["3", "4", "6", "7", "9"])
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 64), (16, 16, 128),
                                       (32, 2, 128)])
 def test_paged_attention_prefill(cuda, hq, hkv, d, version):
@@ -183,7 +183,7 @@ def test_paged_attention_prefill(cuda, hq, hkv, d, version):
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("version", ["3", "4", "6", "7"])
+@pytest.mark.parametrize("version", ["3", "4", "6", "7", "9"])
 def test_paged_attention_prefill_long(cuda, version):
     """Long prompts: > 64 KV chunks per sequence (block-id reloads), many workgroups per
     (sequence, kv head), a chunked prefill that starts mid-block."""
@@ -239,7 +239,7 @@ def test_decode_rope_consumes_splitk_qkv_bit_exact(cuda, b):
     torch.testing.assert_close(v1, v2, atol=0, rtol=0)
 
 
-@pytest.mark.parametrize("version", [4, 6, 7])
+@pytest.mark.parametrize("version", [4, 6, 7, 9])
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (8, 4, 64)])
 def test_prefill_attention_with_q_rope_in_kernel(cuda, hq, hkv, d, version):
     """knobs.prefill_fused_rope: rope_cache_append(write_q=False) appends K / V only and the LDS prefill
