@@ -913,13 +913,15 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
   // wave w stages 1 KiB pieces 4 w .. 4 w + 3 of tile t: pieces 0-7 K block 0, 8-15 K block 1,
   // 16-23 V^T block 0, 24-31 V^T block 1 (a block past the sequence re-reads the last one: its keys
   // are masked for every column)
+  // (a wave's four pieces are one part: one block id per wave, read once and made scalar)
   auto stage = [&](int t, int buf) {
     bf16* dst = smem + buf * TILE;
+    static_assert(GL * 2 == 8, "one part per wave");
+    const int c = min(2 * t + ((w >> 1) & 1), nch - 1);
+    const size_t base = (size_t)__builtin_amdgcn_readfirstlane(ids[c]) * blk_stride + head_off;
 #pragma unroll
     for (int j = 0; j < GL; ++j) {
       const int i = w * GL + j, part = i >> 3;
-      const int c = min(2 * t + (part & 1), nch - 1);
-      const size_t base = (size_t)ids[c] * blk_stride + head_off;
       const bf16* src;
       if (part < 2) {
         const int rr = (i & 7) * 4 + lane / 16, cs = lane % 16;
@@ -1024,13 +1026,19 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
     asm volatile("" ::: "memory");
     // slot (t + 2) % NB was last read in iteration t - 1 (PIPE: t - 2's V^T in iteration t - 1), which
     // every wave finished before the barrier
-    if (t + 2 < ntile) stage(t + 2, (t + 2) % NB);
     const bf16* tb = smem + (t % NB) * TILE;
     const int k0 = t * TK;
     if constexpr (PIPE) {
-      if (!active) continue;
+      // PIPE stages behind this tile's QK^T: the block-id read and address work then run under the
+      // MFMAs instead of between the barrier and the first of them
+      if (!active) {
+        if (t + 2 < ntile) stage(t + 2, (t + 2) % NB);
+        continue;
+      }
       f32x16 s0, s1;
       qk(tb, s0, s1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 2 < ntile) stage(t + 2, (t + 2) % NB);
       if (k0 + TK - 1 > wave_kmin) mask(s0, s1, k0);   // unmasked below every column's diagonal
       // the previous tile's 16 P.V MFMAs with this tile's softmax in their gaps, one slice per gap
       // (sched_barrier(0) fences each gap): gaps 0-3 the column max over registers 4 k .. 4 k + 3 of
@@ -1095,7 +1103,10 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) pbp[i] = pb[i];
       vprev = t % NB;
-    } else if (k0 <= wave_kmax) {
+    } else if (t + 2 < ntile) {
+      stage(t + 2, (t + 2) % NB);
+    }
+    if (!PIPE && k0 <= wave_kmax) {
       f32x16 s0, s1;
       qk(tb, s0, s1);
       if (k0 + TK - 1 > wave_kmin) mask(s0, s1, k0);
@@ -1166,8 +1177,8 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
   constexpr int NB = 4;
   constexpr int GL = TILE / 512 / WV;
   static_assert(GL == 4 && 32 % G == 0, "tile pieces / column tiling");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NB * TILE + 2 * kPfMaxChunks];
-  int* ids = reinterpret_cast<int*>(smem + NB * TILE);
+  __shared__ __attribute__((aligned(16))) bf16 smem[NB * TILE + 4 * kPfMaxChunks];
+  int* ids = reinterpret_cast<int*>(smem + NB * TILE);   // two block-id lists: this item's, the next's
 
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m = lane & 31, hi = lane >> 5;
@@ -1177,7 +1188,6 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
 
   struct Item {
     int b, kvh, qs, ql, qpos0, row0, ntile, nch;
-    int bid[4];                                   // block ids of tiles 0 / 1 (scalar loads)
   };
   // r-th item of this workgroup (snake over rounds); false past the end
   auto pos_of = [&](int r) { return r * PX + ((r & 1) ? PX - 1 - wx : wx); };
@@ -1194,9 +1204,6 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
     const int kmax = it.qpos0 + min(it.row0 + RWG, it.ql) - 1;
     it.nch = kmax / kBS + 1;
     it.ntile = (it.nch + 1) / 2;
-    const int32_t* bt = block_tables + (size_t)it.b * max_blocks;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) it.bid[c] = bt[min(c, it.nch - 1)];
     return it.row0 < it.ql;                       // rows past the sequence: an empty item
   };
   // the next non-empty item at or after round r: its round, or -1
@@ -1212,21 +1219,19 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
   int rn = next_item(rc + 1, nxt);
 
   const size_t blk_stride = (size_t)hkv * BLK;
-  // stage local tile t of item it into ring slot buf; block ids of tiles 0 / 1 from the item's
-  // registers (its LDS ids are not written yet when they are staged), later ones from LDS.  (A
-  // select between a table pointer and an LDS pointer becomes a flat load, whose wait drains the
-  // DMA just issued.)
-  auto stage = [&](const Item& it, int t, int buf) {
+  // stage local tile t of item it, block ids in list il, into ring slot buf.  The ids come from
+  // LDS: the next item's list is written in this item's prologue, so its first tiles can be staged
+  // under this item's last ones.  (Reading them from the table for the first tiles instead made a
+  // select between a global and an LDS pointer, a flat load, whose wait drains the DMA just issued.)
+  auto stage = [&](const Item& it, int il, int t, int buf) {
     bf16* dst = smem + buf * TILE;
     const size_t head_off = (size_t)it.kvh * BLK;
+    const int c = min(2 * t + ((w >> 1) & 1), it.nch - 1);
+    const int id = __builtin_amdgcn_readfirstlane(ids[il * kPfMaxChunks + c]);
+    const size_t base = (size_t)id * blk_stride + head_off;
 #pragma unroll
     for (int j = 0; j < GL; ++j) {
       const int i = w * GL + j, part = i >> 3;
-      const int c = min(2 * t + (part & 1), it.nch - 1);
-      int id;
-      if (t < 2) id = c == 0 ? it.bid[0] : c == 1 ? it.bid[1] : c == 2 ? it.bid[2] : it.bid[3];
-      else id = ids[c];
-      const size_t base = (size_t)id * blk_stride + head_off;
       const bf16* src;
       if (part < 2) {
         const int rr = (i & 7) * 4 + lane / 16, cs = lane % 16;
@@ -1239,19 +1244,26 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
   };
   // global tile gt + d, where cur's tile 0 is global tile g0: cur's, else nxt's, else none
   int g0 = 0, staged = 0;                         // global tiles [0, staged) have been issued
-  auto stage_global = [&](int gidx) {
+  int il = 0;                                     // cur's block-id list (nxt's: il ^ 1)
+  // nxt's tiles only from inside cur's tile loop: nxt's list is written in cur's prologue
+  auto stage_global = [&](int gidx, bool may_next) {
     const int lt = gidx - g0;
     if (lt < cur.ntile) {
-      stage(cur, lt, gidx % NB);
-    } else if (rn >= 0 && lt - cur.ntile < nxt.ntile) {
-      stage(nxt, lt - cur.ntile, gidx % NB);
+      stage(cur, il, lt, gidx % NB);
+    } else if (may_next && rn >= 0 && lt - cur.ntile < nxt.ntile) {
+      stage(nxt, il ^ 1, lt - cur.ntile, gidx % NB);
     } else {
       return;
     }
     staged = gidx + 1;
   };
-  stage_global(0);
-  stage_global(1);
+  {
+    const int32_t* bt = block_tables + (size_t)cur.b * max_blocks;
+    for (int i = threadIdx.x; i < cur.nch; i += WV * 64) ids[i] = bt[i];
+  }
+  __syncthreads();
+  stage_global(0, false);
+  stage_global(1, false);
 
   const int krow = w32_krow(m), kswz = krow & 15;
   const f32x2 sc2 = {scale_log2, scale_log2};
@@ -1291,9 +1303,10 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
         for (int ks = 0; ks < D / 16; ++ks) qf[ks] = bf16x8{};
       }
     }
-    {
-      const int32_t* bt = block_tables + (size_t)cur.b * max_blocks;
-      for (int i = 2 * 2 + threadIdx.x; i < cur.nch; i += WV * 64) ids[i] = bt[i];   // tiles >= 2
+    if (rn >= 0) {                                  // the next item's block ids (its list was the
+      const int32_t* bt = block_tables + (size_t)nxt.b * max_blocks;   // previous item's: all read)
+      int* dst = ids + (il ^ 1) * kPfMaxChunks;
+      for (int i = threadIdx.x; i < nxt.nch; i += WV * 64) dst[i] = bt[i];
     }
     // everything issued so far (q, ids, this item's first tiles, the previous item's stores) lands
     // here: the tile loop's counted waits then see only its own LDS-DMA
@@ -1314,9 +1327,15 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      // ring slot (gidx + 2) % NB was last read in iteration gidx - 1 (its V^T), finished by every wave
-      if (staged == gidx + 2) stage_global(gidx + 2);
-      if (!active) continue;
+      // ring slot (gidx + 2) % NB was last read in iteration gidx - 1 (its V^T), finished by every wave;
+      // active waves stage it behind this tile's QK^T MFMAs
+      // (gidx + 1 too when a one-tile item left it unstaged: its slot was read in iterations gidx - 3
+      // and gidx - 2)
+      if (!active) {
+        if (staged == gidx + 1) stage_global(gidx + 1, true);
+        if (staged == gidx + 2) stage_global(gidx + 2, true);
+        continue;
+      }
       const bf16* tb = smem + (gidx % NB) * TILE;
       const int k0 = t * TK;
       f32x16 s0 = {}, s1 = {};
@@ -1328,6 +1347,9 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
         s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s0, 0, 0, 0);
         s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[ks], s1, 0, 0, 0);
       }
+      __builtin_amdgcn_sched_barrier(0);
+      if (staged == gidx + 1) stage_global(gidx + 1, true);
+      if (staged == gidx + 2) stage_global(gidx + 2, true);
       if (k0 + TK - 1 > wave_kmin) {
         const int kl = kmax_col - k0 - 8 * hi;
 #pragma unroll
@@ -1444,11 +1466,12 @@ __global__ void __launch_bounds__(kW32Waves * 64, 1) attn_prefill_w32p_kernel(
     if (rn < 0) break;
     g0 += cur.ntile;
     cur = nxt;
+    il ^= 1;
     rc = rn;
     rn = next_item(rc + 1, nxt);
     while (staged < g0 + 2) {                       // an item shorter than two tiles left gaps
       const int before = staged;
-      stage_global(staged);
+      stage_global(staged, false);
       if (staged == before) break;
     }
   }

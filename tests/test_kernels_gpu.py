@@ -200,6 +200,25 @@ def test_paged_attention_prefill_long(cuda, version):
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("version", ["4", "7", "9"])
+def test_paged_attention_prefill_many_short(cuda, version):
+    """Many short prompts (a few with prior context): 512 (sequence, kv head) groups of one- and
+    two-tile row blocks -- the persistent kernel (9) walks several per workgroup, switching items
+    every tile or two."""
+    hq, hkv, d = 32, 8, 128
+    g = torch.Generator().manual_seed(3)
+    qlen = [int(x) for x in torch.randint(1, 200, (64,), generator=g)]
+    ctx = [q + (40 if i % 7 == 0 else 0) for i, q in enumerate(qlen)]
+    k, v, bt = _fill_paged(ctx, hkv, d)
+    cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32, device="cuda")
+    sl = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+    q = _bf(sum(qlen), hq, d)
+    scale = 1 / math.sqrt(d)
+    out = ops.paged_attention_prefill(q, k, v, bt, cu, sl, scale, version=int(version))
+    expect = ref.paged_attention_prefill(q.float(), k.float(), v.float(), bt, cu, sl, scale)
+    torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
+
+
 def test_attention_masked_spike(cuda):
     """Force the online-softmax rescale: one key far above the rest, late in the sequence."""
     hq, hkv, d = 32, 8, 128
