@@ -1624,9 +1624,10 @@ void paged_attention_prefill(uintptr_t out, uintptr_t q, uintptr_t k_cache, uint
   const int G = hq / hkv;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float sl2 = scale * 1.4426950408889634f;
-  // version (knobs.prefill_attn): 4 = the LDS-shared kernel (default; bench/prefill_attn_bench.py:
-  // 1.6-1.7x v3 from 128- to 8192-token prompts); 3 = the register-tiled kernel, which also serves
-  // block tables wider than the 32k tokens of block ids the LDS kernel stages
+  // version (ops.prefill_attn_version): 4 = the LDS-shared kernel (short prompts); 6 / 7 / 9 = the
+  // 32x32x16 kernels (9, persistent, by default from 512 query rows; profiles/round6_attention.md);
+  // 3 = the register-tiled kernel, which also serves block tables wider than the 32k tokens of
+  // block ids the LDS kernels stage
   DLLM_HOST_CHECK(version == 3 || version == 4 || version == 6 || version == 7 || version == 9,
                   "prefill attention version 3, 4, 6, 7 or 9");
   if (version >= 6 && (d != 128 || G > 16)) version = 4;           // the 32x32 kernels: head_dim 128, G | 32

@@ -346,13 +346,18 @@ def paged_attention_decode_rope(qkv, positions, cos_sin, k_cache, v_cache, slot_
 
 
 def prefill_attn_version(max_q_len: int, head_dim: int) -> int:
-    """The prefill attention kernel for a batch: knobs.prefill_attn, or with 0 (auto) the 32x32x16
-    pipelined kernel (7) from knobs.prefill_w32_min_q query rows at head_dim 128 -- 1.2-1.3x v4 on
-    1k-16k-token prompts -- and v4 below (256 x 128-token prompts: v4 182-190 us, v7 214-219)."""
+    """The prefill attention kernel for a batch: knobs.prefill_attn, or with 0 (auto) from
+    knobs.prefill_w32_min_q query rows at head_dim 128 the persistent 32x32x16 kernel (9: 1.1x v4 at
+    64 x 512-token prompts, 1.35x at 1 x 16k; profiles/round6_attention.md) -- or its one-shot form (7)
+    while spinning comm kernels hold CUs (ops.gemm.reserve_cus_for_comm: a persistent grid sized to
+    every CU would wait for them) -- and v4 below (256 x 128-token prompts: v4 180-185 us, v9 185-193)."""
     v = knobs.K.prefill_attn
     if v:
         return v
-    return 7 if head_dim == 128 and max_q_len >= knobs.K.prefill_w32_min_q else 4
+    if head_dim != 128 or max_q_len < knobs.K.prefill_w32_min_q:
+        return 4
+    from . import gemm
+    return 7 if gemm._comm_cus else 9
 
 
 def paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, seq_lens, scale: float,

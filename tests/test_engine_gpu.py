@@ -118,13 +118,13 @@ def test_chunked_prefill_gpu_matches_cpu_logits(cuda, name, attn):
 
 
 def test_long_prompt_prefill_default_kernel_matches_cpu_logits(cuda):
-    """The default prefill attention choice (knobs.prefill_attn = 0: the 32x32x16 pipelined kernel
+    """The default prefill attention choice (knobs.prefill_attn = 0: the persistent 32x32x16 kernel
     from 512 query rows at head_dim 128) on a 600-token prompt prefilled in one step, with the
     q-RoPE inside the kernel: logits vs the CPU fp32 prefill."""
     from distributed_llms_amd import knobs, ops
     name = "tiny-llama-d128"
     cfg = get_model_config(name)
-    assert ops.prefill_attn_version(600, cfg.head_dim) == 7 and knobs.K.prefill_attn == 0
+    assert ops.prefill_attn_version(600, cfg.head_dim) == 9 and knobs.K.prefill_attn == 0
     sd = W.synth_hf_state_dict(cfg, seed=6, dtype=torch.float32)
     prompt = [(17 * j) % 450 + 5 for j in range(600)]
     e_cpu = LLMEngine(EngineConfig(model=name, dtype="float32", device="cpu", max_batch=2, max_seq_len=1024,

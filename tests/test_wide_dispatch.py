@@ -222,17 +222,24 @@ def test_prefill_rope_in_attention_gated_on_block_table_width():
 
 
 def test_prefill_attention_auto_version():
-    """knobs.prefill_attn = 0 (default): the 32x32x16 pipelined kernel (7) from prefill_w32_min_q
-    query rows at head_dim 128 (1.2-1.3x v4 on 1k-16k-token prompts), v4 for short prompts and for
-    head_dim 64; an explicit knob wins.  Every auto choice takes the in-kernel q-RoPE."""
+    """knobs.prefill_attn = 0 (default): the persistent 32x32x16 kernel (9) from prefill_w32_min_q
+    query rows at head_dim 128, its one-shot form (7) while comm kernels reserve CUs, v4 for short
+    prompts and for head_dim 64; an explicit knob wins.  Every auto choice takes the in-kernel q-RoPE."""
     from distributed_llms_amd import knobs, ops
+    from distributed_llms_amd.ops import gemm
     with knobs.override(prefill_attn=0, prefill_w32_min_q=512, prefill_fused_rope=True):
         assert ops.prefill_attn_version(128, 128) == 4
         assert ops.prefill_attn_version(511, 128) == 4
-        assert ops.prefill_attn_version(512, 128) == 7
-        assert ops.prefill_attn_version(16384, 128) == 7
+        assert ops.prefill_attn_version(512, 128) == 9
+        assert ops.prefill_attn_version(16384, 128) == 9
         assert ops.prefill_attn_version(4096, 64) == 4
         assert ops.prefill_rope_in_attention(64)
-    for v in (3, 4, 6, 7):
+        gemm.reserve_cus_for_comm(16)
+        try:
+            assert ops.prefill_attn_version(4096, 128) == 7
+        finally:
+            gemm.release_cus_for_comm()
+        assert ops.prefill_attn_version(4096, 128) == 9
+    for v in (3, 4, 6, 7, 9):
         with knobs.override(prefill_attn=v):
             assert ops.prefill_attn_version(4096, 128) == v
