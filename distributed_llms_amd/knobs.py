@@ -78,7 +78,7 @@ class Knobs:
     # ---- attention (ops/__init__.py)
     attn_target_waves: int = 1024     # decode split-KV: waves to aim for (profiles/attn_decode_sweep.txt)
     prefill_attn: int = 0             # prefill kernel: 0 = auto (9 from prefill_w32_min_q query rows at head_dim 128 -- 7 while comm kernels hold CUs -- else 4); 4 = LDS-shared K/V tiles on 16x16 MFMAs, 6 / 7 = the same on 32x32x16 MFMAs (7: P.V overlapping the softmax), 9 = 7 persistent (one workgroup per CU), 3 = register-tiled (> 32k fallback)
-    prefill_w32_min_q: int = 512      # auto: the 32x32 kernel from this many query rows (256 x 128-token prompts: v4 182-190 us, v7 214-219; 32 x 1k: 469 vs 442; profiles/round6_attention.md)
+    prefill_w32_min_q: int = 384      # auto: the 32x32 kernel from this many query rows (128 x 256-token prompts: v4 209-215 us, v9 210-212; 96 x 384: 267-272 vs 260-262; profiles/round6_attention.md)
     # prefill q-RoPE in the attention kernel's q load (rope_cache appends K / V only): no rotated-q
     # round trip through HBM (268 MB per layer at T = 32768)
     prefill_fused_rope: bool = True

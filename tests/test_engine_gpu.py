@@ -119,7 +119,7 @@ def test_chunked_prefill_gpu_matches_cpu_logits(cuda, name, attn):
 
 def test_long_prompt_prefill_default_kernel_matches_cpu_logits(cuda):
     """The default prefill attention choice (knobs.prefill_attn = 0: the persistent 32x32x16 kernel
-    from 512 query rows at head_dim 128) on a 600-token prompt prefilled in one step, with the
+    from knobs.prefill_w32_min_q query rows at head_dim 128) on a 600-token prompt prefilled in one step, with the
     q-RoPE inside the kernel: logits vs the CPU fp32 prefill."""
     from distributed_llms_amd import knobs, ops
     name = "tiny-llama-d128"
