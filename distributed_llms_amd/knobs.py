@@ -45,11 +45,6 @@ class Knobs:
     # on gemm_pp with split-K; the square o-projection stays on gemm_wide up to wide_o_max_m
     pf_min_eff: float = 0.85
     wide_o_max_m: int = 512
-    # widening projections (qkv-like: N > K, K <= 4096) at wide_proj_max_m < M <= this: gemm_wide with
-    # row tile 192 / K split 2 up to M = 384, row tile 128 unsplit above (8B qkv at M = 320 / 384 / 512 /
-    # 640: 31.8 / 32.6 / 36.9 / 37.8 us vs 35.4 / 38.4 / 40.8 / 44.1 for split gemm_pp;
-    # bench/debug/medium_m_sweep.py, profiles/round6_medium_m.md); 0 = off
-    wide_qkv_mid_max_m: int = 640
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),

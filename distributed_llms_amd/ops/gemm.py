@@ -127,35 +127,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         return linear_pp(x, w, splits=1, variant=PP_HEAD_VARIANT)           # decode LM head
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
-    mid = wide_qkv_mid(m, n, k, x, w) if bias is None else None
-    if mid is not None:
-        return linear_wide(x, w, splits=mid[1], defer=defer, variant=mid[2])
     if bias is None and _use_pp(m, n, k, x, w, knobs.K.pp_proj_min_m):
         if kn.pp_persistent and m * n * 2 < (1 << 31) and pf_fills(m, n, x.device):
             return linear_pf(x, w)
         # medium M (mixed prefill + decode steps, short prompts): split-K tiles fill the CUs
         return linear_pp(x, w, variant=PP_PREFILL_VARIANT, defer=defer)
     return F.linear(x, w, bias)
-
-
-def wide_qkv_mid(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor):
-    """(row tile, K splits, variant) of gemm_wide for a widening projection (qkv-like: N > K,
-    K <= 4096, not an LM head) at medium M (knobs.wide_qkv_mid_max_m), else None.  Split gemm_pp
-    moves 256 x 256 f16 partial tiles per K slice there; gemm_wide's 128-row tiles fill 192 CUs
-    unsplit at M = 512 (bench/debug/medium_m_sweep.py)."""
-    kn = knobs.K
-    if not (kn.wide_proj_max_m < m <= kn.wide_qkv_mid_max_m and k < n <= 4 * k and k <= 4096):
-        return None
-    if n % 128 or k % 64 or not (x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()):
-        return None
-    if m <= 384:
-        bm, s = 192, 2
-    else:
-        bm, s = 128, 1
-    v = kn.wide_variant_split if s > 1 else kn.wide_variant
-    if bm != wide_bm(m):
-        v |= bm << 8
-    return bm, s, v
 
 
 PP_PREFILL_VARIANT = 64 | 4        # gemm_pp: schedule 2, grouped row-tile order, 256-column tile

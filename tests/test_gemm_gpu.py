@@ -47,24 +47,8 @@ def test_large_m_uses_hand_written_prefill_gemm(cuda):
     x, w = _bf(300, 256), _bf(512, 256, scale=0.05)          # a qkv-like (N > K) projection
     assert not gemm._use_wide(300, 512, 256, x, w)
     assert gemm._use_pp(300, 512, 256, x, w, gemm.knobs.K.pp_proj_min_m)
-    with gemm.knobs.override(wide_qkv_mid_max_m=0):          # (else the medium-M gemm_wide rule)
-        y = ops.linear(x, w)
+    y = ops.linear(x, w)
     torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=3e-2, rtol=3e-2)
-
-
-@pytest.mark.parametrize("m", [300, 384, 512, 640])
-def test_medium_m_qkv_on_gemm_wide(cuda, m):
-    """knobs.wide_qkv_mid_max_m: 8B qkv shapes at medium M on gemm_wide's 192-row split / 128-row
-    unsplit tiles, deferred (split partials reduced by the consumer) and direct."""
-    x, w = _bf(m, 4096), _bf(6144, 4096, scale=0.02)
-    assert gemm.wide_qkv_mid(m, 6144, 4096, x, w) is not None
-    ref = x.float() @ w.float().t()
-    y = gemm.linear(x, w)
-    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
-    d = gemm.linear(x, w, defer=True)
-    if isinstance(d, gemm.SplitKPartial):
-        d = d.materialize()
-    torch.testing.assert_close(d.float(), ref, atol=3e-2, rtol=3e-2)
 
 
 def test_small_m_graph_replay(cuda):

@@ -191,40 +191,6 @@ def test_medium_m_dispatch_follows_the_measured_table():
     assert not gemm._use_wide(512, 4096, 14336, x, w)
 
 
-def test_medium_m_qkv_takes_gemm_wide_row_tiles():
-    """knobs.wide_qkv_mid_max_m: a widening projection (8B qkv) above the decode cutover runs on
-    gemm_wide -- 192-row tiles split in 2 up to M = 384, 128-row tiles unsplit above (192 workgroups
-    at M = 512) -- instead of split gemm_pp; not the LM head, not the 70B qkv (K = 8192), not past
-    the knob."""
-    from distributed_llms_amd import knobs
-    from distributed_llms_amd.ops import gemm
-    x, w = _xw(320, 6144, 4096)
-    assert gemm.wide_qkv_mid(320, 6144, 4096, x, w)[:2] == (192, 2)
-    x, w = _xw(512, 6144, 4096)
-    bm, s, v = gemm.wide_qkv_mid(512, 6144, 4096, x, w)
-    assert (bm, s, v >> 8) == (128, 1, 128)
-    x, w = _xw(512, 128256, 4096)
-    assert gemm.wide_qkv_mid(512, 128256, 4096, x, w) is None
-    x, w = _xw(512, 10240, 8192)
-    assert gemm.wide_qkv_mid(512, 10240, 8192, x, w) is None
-    x, w = _xw(768, 6144, 4096)
-    assert gemm.wide_qkv_mid(768, 6144, 4096, x, w) is None
-    x, w = _xw(256, 6144, 4096)
-    assert gemm.wide_qkv_mid(256, 6144, 4096, x, w) is None          # decode: gemm_wide's own rule
-    with knobs.override(wide_qkv_mid_max_m=0):
-        x, w = _xw(512, 6144, 4096)
-        assert gemm.wide_qkv_mid(512, 6144, 4096, x, w) is None
-    calls = []
-    orig = gemm.linear_wide
-    gemm.linear_wide = lambda *a, **k: calls.append(k)
-    try:
-        x, w = _xw(512, 6144, 4096)
-        gemm.linear(x, w, defer=True)
-    finally:
-        gemm.linear_wide = orig
-    assert calls and calls[0]["splits"] == 1 and calls[0]["defer"]
-
-
 def test_lm_head_leaves_gemm_pp_while_comm_cus_are_reserved():
     from distributed_llms_amd.ops import gemm
     x, w = _xw(256, 128256, 4096)
