@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--bms", type=int, nargs="+", default=[128, 256])
     ap.add_argument("--splits", type=int, nargs="+", default=[1, 2, 3, 4])
+    ap.add_argument("--pp", nargs="*", default=[],
+                    help="gemm_pp candidates BN:SPLITS[:nt], e.g. 128:1:nt 256:2 (schedule 2)")
+    ap.add_argument("--no-wide", action="store_true", help="skip the gemm_wide grid")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--calls", type=int, default=8)
     a = ap.parse_args()
@@ -44,7 +47,13 @@ def main():
                 fns["dispatch"] = lambda x, w: ops.linear_swiglu(x, w)
             else:
                 fns["dispatch"] = lambda x, w: gemm.linear(x, w)
-            for bm in a.bms:
+            for spec in a.pp:
+                f = spec.split(":")
+                bn, sp, nt = int(f[0]), int(f[1]), len(f) > 2 and f[2] == "nt"
+                var = 64 | (1 if bn == 128 else 0) | (2 if nt else 0)
+                fns[f"pp{bn}s{sp}{'nt' if nt else ''}"] = (lambda sp, var: lambda x, w: gemm.linear_pp(
+                    x, w, splits=sp, swiglu=sw, variant=var))(sp, var)
+            for bm in ([] if a.no_wide else a.bms):
                 for s in a.splits:
                     v = knobs.K.wide_variant_split if s > 1 else knobs.K.wide_variant
                     fns[f"w{bm}s{s}"] = (lambda bm, s, v: lambda x, w: gemm.linear_wide(
