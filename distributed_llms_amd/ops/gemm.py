@@ -136,6 +136,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 PP_PREFILL_VARIANT = 64 | 4        # gemm_pp: schedule 2, grouped row-tile order, 256-column tile
+PP_GATE_UP_VARIANT = 64 | 2 | 1    # gemm_pp: schedule 2, nontemporal weights, 128-column tile
 PP_HEAD_VARIANT = 64 | 2           # gemm_pp: schedule 2, nontemporal weights (read once per step)
 
 
@@ -383,6 +384,12 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Te
     k = x.shape[-1]
     n = w_gate_up.shape[0]
     m = x.numel() // k
+    kn = knobs.K
+    if 0 < kn.pp_gate_up_min_m <= m <= 256 and not _comm_cus and n % 256 == 0 \
+            and _use_pp(m, n, k, x, w_gate_up, 1) and _cus(x.device) // 2 <= n // 128 <= _cus(x.device):
+        # decode gate|up on gemm_pp's 4-wave 256 x 128 tile, weights nontemporal (8B at M = 256:
+        # 62.1 vs 64.1 us for gemm_wide; bench/debug/medium_m_sweep.py --pp)
+        return linear_pp(x, w_gate_up, splits=1, swiglu=True, variant=PP_GATE_UP_VARIANT)
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
     if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):
