@@ -46,8 +46,10 @@ class Knobs:
     pf_min_eff: float = 0.85
     wide_o_max_m: int = 512
     # decode SwiGLU gate|up from this M up to 256 on gemm_pp's 128-column tile with nontemporal
-    # weights instead of gemm_wide (0 = off; not while comm kernels reserve CUs)
-    pp_gate_up_min_m: int = 0
+    # weights instead of gemm_wide, for grids of CUs / 2 .. CUs tiles (0 = off; not while comm kernels
+    # reserve CUs).  8B at B = 256: 62.1 vs 64.1 us, engine +0.45 % tok/s over three interleaved pairs
+    # (profiles/round6_gate_up_pp.md)
+    pp_gate_up_min_m: int = 225
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),

@@ -191,6 +191,32 @@ def test_medium_m_dispatch_follows_the_measured_table():
     assert not gemm._use_wide(512, 4096, 14336, x, w)
 
 
+def test_decode_gate_up_on_gemm_pp_128_column_tile():
+    """knobs.pp_gate_up_min_m: the 8B gate|up at 225 <= M <= 256 runs on gemm_pp's 128-column tile
+    with nontemporal weights (224 tiles: one round); not below the cutover, not the 70B gate|up
+    (448 tiles: gemm_sq's unsplit grid), not while comm kernels reserve CUs."""
+    from distributed_llms_amd.ops import gemm
+    calls = []
+    orig_pp, orig_wide, orig_sq = gemm.linear_pp, gemm.linear_wide, gemm.linear_sq
+    gemm.linear_pp = lambda *a, **k: calls.append(("pp", k.get("variant"), k.get("splits")))
+    gemm.linear_wide = lambda *a, **k: calls.append(("wide",))
+    gemm.linear_sq = lambda *a, **k: calls.append(("sq",))
+    try:
+        gemm.linear_swiglu(*_xw(256, 28672, 4096))
+        gemm.linear_swiglu(*_xw(224, 28672, 4096))
+        gemm.linear_swiglu(*_xw(256, 57344, 8192))
+        gemm.reserve_cus_for_comm(16)
+        try:
+            gemm.linear_swiglu(*_xw(256, 28672, 4096))
+        finally:
+            gemm.release_cus_for_comm()
+    finally:
+        gemm.linear_pp, gemm.linear_wide, gemm.linear_sq = orig_pp, orig_wide, orig_sq
+    assert calls[0] == ("pp", gemm.PP_GATE_UP_VARIANT, 1)
+    assert calls[1][0] == "wide" and calls[3][0] == "wide"
+    assert calls[2][0] != "pp"
+
+
 def test_lm_head_leaves_gemm_pp_while_comm_cus_are_reserved():
     from distributed_llms_amd.ops import gemm
     x, w = _xw(256, 128256, 4096)
