@@ -125,10 +125,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if bias is None and n > 65536 and 0 < kn.pp_head_min_m <= m <= 256 \
             and (not _comm_cus or kn.head_beside_comm == "pp") and _use_pp(m, n, k, x, w, 1):
         return linear_pp(x, w, splits=1, variant=PP_HEAD_VARIANT)           # decode LM head
-    if bias is None and kn.pp_decode_proj and 225 <= m <= 256 and not _comm_cus:
-        sv = pp_decode_split(m, n, k, x, w)
-        if sv is not None:
-            return linear_pp(x, w, splits=sv[0], defer=defer, variant=sv[1])
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
     if bias is None and _use_pp(m, n, k, x, w, knobs.K.pp_proj_min_m):
@@ -140,20 +136,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 PP_PREFILL_VARIANT = 64 | 4        # gemm_pp: schedule 2, grouped row-tile order, 256-column tile
-def pp_decode_split(m: int, n: int, k: int, x: torch.Tensor, w: torch.Tensor):
-    """(K splits, variant) for a decode projection on gemm_pp's 128-column tile (knobs.pp_decode_proj):
-    K slices filling the CUs with one workgroup each, nontemporal weights for the long-K down
-    projection; None for shapes outside the measured 8B range (N K <= 4096 x 14336, not an LM head)."""
-    if n > 65536 or n % 128 or n * k > 4096 * 14336 or not _use_pp(m, n, k, x, w, 1):
-        return None
-    cus = _cus(x.device)
-    tiles = n // 128
-    s = max(1, min(16, round(cus / tiles), (k // 64) // 4))
-    if not (0.85 * cus <= tiles * s <= cus):
-        return None
-    return s, 64 | 1 | (2 if is_down_proj(n, k) else 0)
-
-
 PP_GATE_UP_VARIANT = 64 | 2 | 1    # gemm_pp: schedule 2, nontemporal weights, 128-column tile
 PP_HEAD_VARIANT = 64 | 2           # gemm_pp: schedule 2, nontemporal weights (read once per step)
 
