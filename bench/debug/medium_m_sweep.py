@@ -20,7 +20,9 @@ from distributed_llms_amd import knobs, ops
 from distributed_llms_amd.ops import gemm
 
 SHAPES = {"qkv": (6144, 4096, False), "o": (4096, 4096, False), "gate_up": (28672, 4096, True),
-          "down": (4096, 14336, False)}
+          "down": (4096, 14336, False), "head": (128256, 4096, False),
+          "qkv70": (10240, 8192, False), "o70": (8192, 8192, False), "gate_up70": (57344, 8192, True),
+          "down70": (8192, 28672, False)}
 
 
 def main():
