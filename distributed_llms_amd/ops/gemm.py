@@ -385,11 +385,15 @@ def linear_swiglu(x: torch.Tensor, w_gate_up: torch.Tensor) -> Optional[torch.Te
     n = w_gate_up.shape[0]
     m = x.numel() // k
     kn = knobs.K
-    if 0 < kn.pp_gate_up_min_m <= m <= 256 and not _comm_cus and n % 256 == 0 \
-            and _use_pp(m, n, k, x, w_gate_up, 1) and _cus(x.device) // 2 <= n // 128 <= _cus(x.device):
-        # decode gate|up on gemm_pp's 4-wave 256 x 128 tile, weights nontemporal (8B at M = 256:
-        # 62.1 vs 64.1 us for gemm_wide; bench/debug/medium_m_sweep.py --pp)
-        return linear_pp(x, w_gate_up, splits=1, swiglu=True, variant=PP_GATE_UP_VARIANT)
+    if 0 < kn.pp_gate_up_min_m <= m <= 256 and not _comm_cus and _use_pp(m, n, k, x, w_gate_up, 1):
+        # decode gate|up on gemm_pp, unsplit, weights nontemporal, on the column tile that gives one
+        # round of CUs / 2 .. CUs tiles: 8B (224 x 128 columns) 62.1 vs 64.1 us for gemm_wide, 70B
+        # (224 x 256 columns) 204 vs 259 us for gemm_sq (bench/debug/medium_m_sweep.py --pp)
+        cus = _cus(x.device)
+        if n % 128 == 0 and cus // 2 <= n // 128 <= cus:
+            return linear_pp(x, w_gate_up, splits=1, swiglu=True, variant=PP_GATE_UP_VARIANT)
+        if n % 256 == 0 and cus // 2 <= n // 256 <= cus:
+            return linear_pp(x, w_gate_up, splits=1, swiglu=True, variant=PP_GATE_UP_VARIANT & ~1)
     if _use_wide(m, n, k, x, w_gate_up, swiglu=True):
         return linear_wide(x, w_gate_up, swiglu=True)
     if _use_pp(m, n, k, x, w_gate_up, knobs.K.pp_swiglu_min_m):

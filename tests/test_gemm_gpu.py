@@ -34,7 +34,7 @@ def test_bias_uses_library_gemm(cuda):
 
 
 @pytest.mark.parametrize("m", [1, 16, 64, 240, 256])
-@pytest.mark.parametrize("inter,k", [(14336, 4096), (512, 256), (1024, 512)])
+@pytest.mark.parametrize("inter,k", [(14336, 4096), (28672, 8192), (512, 256), (1024, 512)])
 def test_small_m_swiglu(cuda, m, inter, k):
     x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)
     y = gemm.linear_swiglu(x, w)

@@ -193,8 +193,8 @@ def test_medium_m_dispatch_follows_the_measured_table():
 
 def test_decode_gate_up_on_gemm_pp_128_column_tile():
     """knobs.pp_gate_up_min_m: the 8B gate|up at 225 <= M <= 256 runs on gemm_pp's 128-column tile
-    with nontemporal weights (224 tiles: one round); not below the cutover, not the 70B gate|up
-    (448 tiles: gemm_sq's unsplit grid), not while comm kernels reserve CUs."""
+    with nontemporal weights (224 tiles: one round), the 70B gate|up on its 256-column tile (224
+    tiles); not below the cutover, not while comm kernels reserve CUs."""
     from distributed_llms_amd.ops import gemm
     calls = []
     orig_pp, orig_wide, orig_sq = gemm.linear_pp, gemm.linear_wide, gemm.linear_sq
@@ -214,7 +214,7 @@ def test_decode_gate_up_on_gemm_pp_128_column_tile():
         gemm.linear_pp, gemm.linear_wide, gemm.linear_sq = orig_pp, orig_wide, orig_sq
     assert calls[0] == ("pp", gemm.PP_GATE_UP_VARIANT, 1)
     assert calls[1][0] == "wide" and calls[3][0] == "wide"
-    assert calls[2][0] != "pp"
+    assert calls[2] == ("pp", gemm.PP_GATE_UP_VARIANT & ~1, 1)       # 70B: 224 x 256-column tiles
 
 
 def test_lm_head_leaves_gemm_pp_while_comm_cus_are_reserved():
