@@ -50,6 +50,9 @@ class Knobs:
     # reserve CUs).  8B at B = 256: 62.1 vs 64.1 us, engine +0.45 % tok/s over three interleaved pairs
     # (profiles/round6_gate_up_pp.md)
     pp_gate_up_min_m: int = 225
+    # decode down projections with K >= this (225 <= M <= 256) on split gemm_pp 128-column tiles with
+    # nontemporal weights (0 = off; A/B knob)
+    pp_down_min_k: int = 0
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),

@@ -125,6 +125,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if bias is None and n > 65536 and 0 < kn.pp_head_min_m <= m <= 256 \
             and (not _comm_cus or kn.head_beside_comm == "pp") and _use_pp(m, n, k, x, w, 1):
         return linear_pp(x, w, splits=1, variant=PP_HEAD_VARIANT)           # decode LM head
+    if bias is None and 0 < kn.pp_down_min_k <= k and 225 <= m <= 256 and is_down_proj(n, k) and not _comm_cus \
+            and n % 128 == 0 and _use_pp(m, n, k, x, w, 1):
+        # long-K decode down projection (70B: K = 28672) on gemm_pp's 128-column tile, K slices filling
+        # the CUs, weights nontemporal: 126 vs 135 us for gemm_wide (bench/debug/medium_m_sweep.py)
+        s = max(1, min(16, _cus(x.device) // (n // 128)))
+        return linear_pp(x, w, splits=s, defer=defer, variant=64 | 2 | 1)
     if bias is None and _use_wide(m, n, k, x, w):
         return linear_wide(x, w, defer=defer)
     if bias is None and _use_pp(m, n, k, x, w, knobs.K.pp_proj_min_m):

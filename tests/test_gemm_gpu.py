@@ -384,3 +384,19 @@ def test_pp_graph_replay_and_determinism(cuda):
         g.replay()
     torch.cuda.synchronize()
     assert torch.equal(y, y0)
+
+
+@pytest.mark.parametrize("m", [225, 256])
+def test_long_k_down_on_split_gemm_pp(cuda, m):
+    """knobs.pp_down_min_k: a long-K down projection (K >= the knob) at decode M on split gemm_pp
+    128-column tiles with nontemporal weights -- direct and deferred (partials reduced by the
+    consumer) against fp32."""
+    x, w = _bf(m, 16384), _bf(2048, 16384, scale=0.02)
+    ref = x.float() @ w.float().t()
+    with gemm.knobs.override(pp_down_min_k=16384):
+        y = gemm.linear(x, w)
+        d = gemm.linear(x, w, defer=True)
+        assert isinstance(d, gemm.SplitKPartial)
+        d = d.materialize()
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(d.float(), ref, atol=3e-2, rtol=3e-2)
