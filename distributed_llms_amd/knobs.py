@@ -51,8 +51,9 @@ class Knobs:
     # (profiles/round6_gate_up_pp.md)
     pp_gate_up_min_m: int = 225
     # decode down projections with K >= this (225 <= M <= 256) on split gemm_pp 128-column tiles with
-    # nontemporal weights (0 = off; A/B knob)
-    pp_down_min_k: int = 0
+    # nontemporal weights (0 = off): the 70B down (K = 28672) 126 vs 135 us, engine +0.85 % tok/s
+    # (profiles/round6_gate_up_pp.md); the 8B down (K = 14336) stays on gemm_wide
+    pp_down_min_k: int = 16384
     wide_small_bm: int = 0            # row-tile override for small split grids (0: off)
     wide_small_bm_maxw: int = 4096 * 4096
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),

@@ -217,6 +217,24 @@ def test_decode_gate_up_on_gemm_pp_128_column_tile():
     assert calls[2] == ("pp", gemm.PP_GATE_UP_VARIANT & ~1, 1)       # 70B: 224 x 256-column tiles
 
 
+def test_long_k_down_on_split_gemm_pp():
+    """knobs.pp_down_min_k: the 70B down projection (K = 28672) at decode M on split gemm_pp
+    128-column tiles (64 tiles x 4 slices, nontemporal weights); the 8B down (K = 14336) and other
+    projections keep gemm_wide."""
+    from distributed_llms_amd.ops import gemm
+    calls = []
+    orig_pp, orig_wide = gemm.linear_pp, gemm.linear_wide
+    gemm.linear_pp = lambda *a, **k: calls.append(("pp", k.get("splits"), k.get("variant")))
+    gemm.linear_wide = lambda *a, **k: calls.append(("wide",))
+    try:
+        gemm.linear(*_xw(256, 8192, 28672), defer=True)
+        gemm.linear(*_xw(256, 4096, 14336), defer=True)
+        gemm.linear(*_xw(128, 8192, 28672), defer=True)
+    finally:
+        gemm.linear_pp, gemm.linear_wide = orig_pp, orig_wide
+    assert calls == [("pp", 4, 64 | 2 | 1), ("wide",), ("wide",)]
+
+
 def test_lm_head_leaves_gemm_pp_while_comm_cus_are_reserved():
     from distributed_llms_amd.ops import gemm
     x, w = _xw(256, 128256, 4096)
