@@ -47,9 +47,10 @@ class Knobs:
     wide_o_max_m: int = 512
     # decode SwiGLU gate|up from this M up to 256 on gemm_pp's 128-column tile with nontemporal
     # weights instead of gemm_wide, for grids of CUs / 2 .. CUs tiles (0 = off; not while comm kernels
-    # reserve CUs).  8B at B = 256: 62.1 vs 64.1 us, engine +0.45 % tok/s over three interleaved pairs
+    # reserve CUs).  8B at B = 256: 62.1 vs 64.1 us, engine +0.45 % tok/s over three interleaved pairs;
+    # at M = 224: 8B 61.4 vs 65.7, 70B (256-column tile) 206 vs 244; at M = 192 the 8B loses
     # (profiles/round6_gate_up_pp.md)
-    pp_gate_up_min_m: int = 225
+    pp_gate_up_min_m: int = 200
     # decode down projections with K >= this (225 <= M <= 256) on split gemm_pp 128-column tiles with
     # nontemporal weights (0 = off): the 70B down (K = 28672) 126 vs 135 us, engine +0.85 % tok/s
     # (profiles/round6_gate_up_pp.md); the 8B down (K = 14336) stays on gemm_wide

@@ -33,7 +33,7 @@ def test_bias_uses_library_gemm(cuda):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("m", [1, 16, 64, 240, 256])
+@pytest.mark.parametrize("m", [1, 16, 64, 200, 240, 256])
 @pytest.mark.parametrize("inter,k", [(14336, 4096), (28672, 8192), (512, 256), (1024, 512)])
 def test_small_m_swiglu(cuda, m, inter, k):
     x, w = _bf(m, k), _bf(2 * inter, k, scale=0.05)

@@ -192,7 +192,7 @@ def test_medium_m_dispatch_follows_the_measured_table():
 
 
 def test_decode_gate_up_on_gemm_pp_128_column_tile():
-    """knobs.pp_gate_up_min_m: the 8B gate|up at 225 <= M <= 256 runs on gemm_pp's 128-column tile
+    """knobs.pp_gate_up_min_m: the 8B gate|up at 200 <= M <= 256 runs on gemm_pp's 128-column tile
     with nontemporal weights (224 tiles: one round), the 70B gate|up on its 256-column tile (224
     tiles); not below the cutover, not while comm kernels reserve CUs."""
     from distributed_llms_amd.ops import gemm
@@ -203,7 +203,7 @@ def test_decode_gate_up_on_gemm_pp_128_column_tile():
     gemm.linear_sq = lambda *a, **k: calls.append(("sq",))
     try:
         gemm.linear_swiglu(*_xw(256, 28672, 4096))
-        gemm.linear_swiglu(*_xw(224, 28672, 4096))
+        gemm.linear_swiglu(*_xw(192, 28672, 4096))
         gemm.linear_swiglu(*_xw(256, 57344, 8192))
         gemm.reserve_cus_for_comm(16)
         try:
