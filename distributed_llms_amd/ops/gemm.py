@@ -12,6 +12,10 @@ the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..
   with the 256 x 256 tile (gemm_sq.hip) taking unsplit grids at 225 <= M <= 256 (70B gate|up);
 * the decode LM head at 225 <= M <= 256: gemm_pp.hip schedule 2 with nontemporal weights
   (knobs.pp_head_min_m);
+* the decode SwiGLU gate|up at 200 <= M <= 256 on gemm_pp unsplit with nontemporal weights, on the
+  column tile (128, else 256) that makes one round of CUs / 2 .. CUs tiles (8B: 224 x 128, 70B:
+  224 x 256; knobs.pp_gate_up_min_m), and the long-K down projection (K >= knobs.pp_down_min_k,
+  70B) at 225 <= M <= 256 on split gemm_pp 128-column tiles (profiles/round6_gate_up_pp.md);
 * prefill (M >= knobs.pp_swiglu_min_m / pp_proj_min_m, above the decode ranges): the 4-wave
   256 x 256-tile schedule-2 kernel in its persistent form (gemm_pf in gemm_pp.hip, knobs.pp_persistent)
   -- gate|up with the SwiGLU fused into its epilogue, qkv / o / down plain
