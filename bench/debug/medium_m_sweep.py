@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--pp", nargs="*", default=[],
                     help="gemm_pp candidates BN:SPLITS[:nt], e.g. 128:1:nt 256:2 (schedule 2)")
     ap.add_argument("--no-wide", action="store_true", help="skip the gemm_wide grid")
+    ap.add_argument("--sq", type=int, nargs="*", default=[], help="gemm_sq (256 x 256 tiles) at these K splits")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--calls", type=int, default=8)
     a = ap.parse_args()
@@ -55,6 +56,8 @@ def main():
                 var = 64 | (1 if bn == 128 else 0) | (2 if nt else 0)
                 fns[f"pp{bn}s{sp}{'nt' if nt else ''}"] = (lambda sp, var: lambda x, w: gemm.linear_pp(
                     x, w, splits=sp, swiglu=sw, variant=var))(sp, var)
+            for sp in a.sq:
+                fns[f"sq{sp}"] = (lambda sp: lambda x, w: gemm.linear_sq(x, w, splits=sp, swiglu=sw))(sp)
             for bm in ([] if a.no_wide else a.bms):
                 for s in a.splits:
                     v = knobs.K.wide_variant_split if s > 1 else knobs.K.wide_variant
