@@ -1,6 +1,6 @@
 """Prefill attention microbenchmark: the kernel versions of csrc/kernels/attention.hip side by side.
 
-    python bench/prefill_attn_bench.py [--versions 4 7]
+    python bench/prefill_attn_bench.py [--versions 4 7 9]
 
 Shapes: Llama-3 GQA (Hq 32, Hkv 8, D 128), whole prompts already in the paged cache (the
 engine's prefill: rope_cache_append first, then attention over the sequence's own keys).
@@ -21,7 +21,7 @@ from distributed_llms_amd.ops import reference as ref
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--versions", nargs="+", default=["4", "7"])
+    ap.add_argument("--versions", nargs="+", default=["4", "7", "9"])
     ap.add_argument("--shapes", nargs="+", default=["256x128", "32x1024", "8x4096", "1x8192"],
                     help="BATCHxPROMPT_LEN")
     ap.add_argument("--reps", type=int, default=10)
