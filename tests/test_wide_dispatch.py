@@ -235,6 +235,19 @@ def test_long_k_down_on_split_gemm_pp():
     assert calls == [("pp", 4, 64 | 2 | 1), ("wide",), ("wide",)]
 
 
+def test_o_projection_runs_as_two_128_row_tiles_at_decode():
+    """knobs.wide_small_bm = 128 (default): the 8B o-projection (N K <= 4096^2) at M = 256 runs as
+    2 x 128-row tiles x 4 K slices (engine +0.75 %); qkv, the down projection and the SwiGLU keep
+    the 256-row tile."""
+    from distributed_llms_amd.ops import gemm
+    assert gemm.wide_row_tile(256, 4096, 4096) == 128
+    assert gemm.wide_splits(256, 4096, 4096) == 4
+    assert gemm.wide_row_tile(256, 6144, 4096) == 256
+    assert gemm.wide_row_tile(256, 4096, 14336) == 256
+    assert gemm.wide_row_tile(256, 28672, 4096, swiglu=True) == 256
+    assert gemm.wide_row_tile(64, 4096, 4096) == 64
+
+
 def test_lm_head_leaves_gemm_pp_while_comm_cus_are_reserved():
     from distributed_llms_amd.ops import gemm
     x, w = _xw(256, 128256, 4096)
