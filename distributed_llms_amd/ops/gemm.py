@@ -8,7 +8,8 @@ the engine on Llama-3-8B, profiles/wide_gemm.md; each one is a field of :mod:`..
   - gate|up (SwiGLU fused into the epilogue): M <= knobs.wide_gate_up_max_m (256);
   - down (K >= 8192 and K > N; split-K partials deferred into the next norm):
     M <= knobs.wide_down_max_m (512);
-  - the other projections (qkv, o, LM head): M <= knobs.wide_proj_max_m (256);
+  - the other projections (qkv, o, LM head): M <= knobs.wide_proj_max_m (256); the o-projection
+    (N K <= knobs.wide_small_bm_maxw) on 128-row tiles with half the K slices (knobs.wide_small_bm);
   with the 256 x 256 tile (gemm_sq.hip) taking unsplit grids at 225 <= M <= 256 (70B gate|up);
 * the decode LM head at 225 <= M <= 256: gemm_pp.hip schedule 2 with nontemporal weights
   (knobs.pp_head_min_m);
