@@ -188,8 +188,6 @@ def wide_row_tile(m: int, n: int, k: int, swiglu: bool = False) -> int:
     kn = knobs.K
     if kn.wide_small_bm and not swiglu and n * k <= kn.wide_small_bm_maxw and kn.wide_small_bm < wide_bm(m):
         return kn.wide_small_bm
-    if kn.wide_small_bm_down and not swiglu and is_down_proj(n, k) and 128 < wide_bm(m) and n * k <= 4096 * 14336:
-        return 128
     return wide_bm(m)
 
 
