@@ -57,7 +57,6 @@ class Knobs:
     pp_down_min_k: int = 16384
     wide_small_bm: int = 128          # row-tile override for small split grids (0: off): the 8B o-projection at M = 256 as 2 x 128-row tiles x 4 K slices, engine +0.75 % tok/s (profiles/round6_gate_up_pp.md)
     wide_small_bm_maxw: int = 4096 * 4096
-    wide_qkv_splits: int = 0          # K slices for widening decode projections (qkv; 0 = wide_splits) (A/B knob)
     # 256 x 256 decode GEMM (gemm_sq.hip): roles ("all", "none", or gate_up / down / proj / head),
     # from this M up to 256, unsplit grids only unless sq_split
     sq: str = "all"

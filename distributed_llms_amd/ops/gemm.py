@@ -251,8 +251,6 @@ def linear_wide(x: torch.Tensor, w: torch.Tensor, splits: int = 0, swiglu: bool 
     if n % 128 or k % 64:
         raise ValueError("linear_wide: N % 128 and K % 64")
     s = splits or wide_splits(m, n, k, swiglu)
-    if not splits and knobs.K.wide_qkv_splits and not swiglu and k < n <= 65536 and m <= 256:
-        s = knobs.K.wide_qkv_splits
     ws = _workspace(x.device)
     if s > 1 and s * m * n > ws.numel():
         s = max(1, ws.numel() // (m * n))
