@@ -1513,6 +1513,7 @@ static void decode_launch(uintptr_t out, uintptr_t q, uintptr_t k_cache, uintptr
     if (parts) {
       if (ra.nparts == 5) DLLM_DEC(128, true, 5);
       else if (ra.nparts == 4) DLLM_DEC(128, true, 4);
+      else if (ra.nparts == 3) DLLM_DEC(128, true, 3);   // the 70B qkv (K = 8192, 3 slices)
       else if (ra.nparts == 8) DLLM_DEC(128, true, 8);
       else DLLM_DEC(128, true, -1);
     } else if (fused) DLLM_DEC(128, true, 0); else DLLM_DEC(128, false, 0);

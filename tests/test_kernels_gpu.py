@@ -233,8 +233,9 @@ def test_attention_masked_spike(cuda):
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("splits", [3, 5, 6])
 @pytest.mark.parametrize("b", [100, 256])
-def test_decode_rope_consumes_splitk_qkv_bit_exact(cuda, b):
+def test_decode_rope_consumes_splitk_qkv_bit_exact(cuda, b, splits):
     """The fused decode kernel summing the qkv projection's f32 split-K slabs itself gives exactly
     the result of reducing first (same slab order, same bf16 rounding)."""
     from distributed_llms_amd.ops import gemm
@@ -247,7 +248,7 @@ def test_decode_rope_consumes_splitk_qkv_bit_exact(cuda, b):
     pos = sl - 1
     slots = torch.stack([bt[i, (lens[i] - 1) // 32] * 32 + (lens[i] - 1) % 32 for i in range(b)]).to(torch.int32)
     cs = ref.rope_cos_sin(d, 4096, 500000.0, device="cuda")
-    part = gemm.linear_wide(x, w, splits=5, defer=True)
+    part = gemm.linear_wide(x, w, splits=splits, defer=True)
     assert isinstance(part, gemm.SplitKPartial)
     k1, v1, k2, v2 = k.clone(), v.clone(), k.clone(), v.clone()
     o1 = ops.paged_attention_decode_rope(part, pos, cs, k1, v1, slots, bt, sl, hq, hkv, d, 1 / math.sqrt(d))
